@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training tokens/sec of Transformer-base
+(6 layers, d_model 512, 8 heads, d_ff 2048, vocab pt 7765 / en 7010) on
+synthetic (source, target) pairs of length 128, bf16 compute, synchronous data
+parallelism over RCCL on N MI355X GPUs (one process per GPU).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+A timed step is the full training step: forward, masked cross-entropy,
+backward, bucketed gradient all-reduce, Adam update. Weak scaling: the local
+batch (default 64 sentence pairs per GPU, the reference's local_batch_size,
+configuration/settings.yaml) is fixed, so the global batch is 64*N.
+tokens/step = global_batch * (src_len + tgt_len) = 64*N*256.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config  # noqa: E402
+from tensorflow_distributed_on_gke_amd.parallel import dist as tdist  # noqa: E402
+from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel  # noqa: E402
+from tensorflow_distributed_on_gke_amd.train.optim import Adam  # noqa: E402
+from tensorflow_distributed_on_gke_amd.train.step import TrainStep  # noqa: E402
+from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs  # noqa: E402
+
+METRIC = "tokens/sec (whole node), Transformer-base en-pt at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--preset", default="base")
+    ap.add_argument("--local-batch", type=int, default=64)
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    info = tdist.init_distributed()
+    world = info.world
+    if world != args.gpus and info.rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = info.device
+    cfg = model_config(args.preset, max_src_len=max(1000, args.seq_len), max_tgt_len=max(1000, args.seq_len))
+    model = Transformer(cfg).build(dev, seed=args.seed)
+    opt = Adam(model.store, cfg.d_model)
+    ddp = DataParallel(model.store, bucket_mb=args.bucket_mb) if world > 1 else None
+    if ddp is not None:
+        ddp.broadcast_params(0)
+    step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17)
+
+    S = T = args.seq_len
+    data = SyntheticPairs(batch=args.local_batch, src_len=S, tgt_len=T + 1, src_vocab=cfg.src_vocab,
+                          tgt_vocab=cfg.tgt_vocab, seed=args.seed, rank=info.rank, world=world, pin=True)
+    # pre-stage a few device batches so the timed loop measures the step
+    batches = []
+    for i in range(4):
+        s, t = data.batch(i)
+        batches.append((s.to(dev, non_blocking=True), t.to(dev, non_blocking=True)))
+
+    use_graph = args.graph if args.graph >= 0 else int(world == 1 and dev.type == "cuda")
+    if use_graph:
+        step.capture(*batches[0])
+    for i in range(args.warmup):
+        step(*batches[i % len(batches)])
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    tdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(*batches[i % len(batches)])
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    tdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms = elapsed / args.steps * 1000.0
+    global_batch = args.local_batch * world
+    tokens = global_batch * (S + T) * args.steps
+    value = tokens / elapsed
+    loss = float(step.last[0].item()) * world if dev.type == "cuda" else float(step.last[0])
+    if info.rank == 0:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, synthetic pt/en token pairs, full-length 128)",
+            "config": {
+                "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "
+                         f"heads={cfg.heads}, d_ff={cfg.d_ff}, vocab {cfg.src_vocab}/{cfg.tgt_vocab})",
+                "global_batch": global_batch,
+                "local_batch": args.local_batch,
+                "seq_len": S,
+                "parallelism": f"dp{world}",
+                "hip_graph": bool(use_graph),
+                "last_loss": round(loss, 4),
+            },
+        }), flush=True)
+    tdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,504 @@
+// Python bindings for the gfx950 kernels (module `_C`).
+// Every op launches on the current HIP stream of the tensors' device, takes
+// caller-allocated outputs (no allocation inside an op: HIP-graph capturable)
+// and validates dtypes / shapes / strides on the host before launching, so a
+// kernel never sees operands its grid does not assume.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "tdg_attn.h"
+
+using at::Tensor;
+using c10::optional;
+
+extern "C" {
+int tdg_gemm(const void* A, const void* B, void* C, const float* bias, const void* aux, int M,
+             int N, int K, int lda, int ldb, int ldc, int ldaux, int a_kc, int b_kc, int epi,
+             int out_f32, float alpha, float beta, int tile_cfg, int splits, float* ws,
+             hipStream_t st);
+void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld, int rows_per_block,
+                float beta, hipStream_t st);
+int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
+int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
+int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
+int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
+               void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
+               const long long* ctr, uint64_t site, float eps, hipStream_t st);
+int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
+               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
+               float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
+               const long long* ctr, uint64_t site, int accumulate, hipStream_t st);
+int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe, void* out, int M,
+                  int L, int D, float scale, float p, uint64_t seed, const long long* ctr,
+                  uint64_t site, hipStream_t st);
+int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, int M, int D,
+                  float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
+                  hipStream_t st);
+int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
+int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64, const float* ntok,
+             float workers, float smoothing, float* row_loss, float* row_correct, int write_grad,
+             hipStream_t st);
+int tdg_xent_stats(const float* row_loss, const float* row_correct, int M, const float* ntok,
+                   float workers, float* step_out, float* accum, hipStream_t st);
+int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, long long* step,
+             float beta1, float beta2, float eps, float lr_const, float d_model, float warmup,
+             float grad_scale, float weight_decay, int sched, int zero_grad, hipStream_t st);
+int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t stream_of(const Tensor& t) {
+  TORCH_CHECK(t.is_cuda(), "tdg op: tensor must be on the GPU");
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_bf16(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, " must be bfloat16");
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+}
+void check_f32(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat, n, " must be float32");
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+}
+void check_contig(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+}
+// The extent [0, rows*ld) (minus trailing) must lie inside the storage.
+void check_extent(const Tensor& t, long long rows, long long ld, long long cols, const char* n) {
+  const long long need = rows > 0 ? (rows - 1) * ld + cols : 0;
+  const long long have = (long long)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+  TORCH_CHECK(need <= have, n, ": operand extent ", need, " exceeds storage ", have);
+}
+void check_err(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, ": unsupported configuration (rc=", rc, ")");
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, what, ": launch failed: ", hipGetErrorString(e));
+}
+
+// ---------------------------------------------------------------- GEMM
+void gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
+          const optional<Tensor>& aux, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+          int64_t ldc, int64_t ldaux, bool a_kc, bool b_kc, int64_t epi, double alpha,
+          double beta, int64_t tile_cfg, int64_t splits, const optional<Tensor>& ws) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  TORCH_CHECK(C.is_cuda(), "C must be a GPU tensor");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "C must be f32 or bf16");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm: empty problem");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(B.data_ptr()) % 16) == 0,
+              "gemm: A/B must be 16-byte aligned");
+  // A(m,k): KC -> [M][lda] ; MC -> [K][lda]
+  if (a_kc) {
+    TORCH_CHECK(lda >= K, "gemm: lda < K");
+    check_extent(A, M, lda, K, "A");
+  } else {
+    TORCH_CHECK(lda >= M, "gemm: lda < M");
+    check_extent(A, K, lda, M, "A");
+  }
+  if (b_kc) {
+    TORCH_CHECK(ldb >= K, "gemm: ldb < K");
+    check_extent(B, N, ldb, K, "B");
+  } else {
+    TORCH_CHECK(ldb >= N, "gemm: ldb < N");
+    check_extent(B, K, ldb, N, "B");
+  }
+  TORCH_CHECK(ldc >= N, "gemm: ldc < N");
+  check_extent(C, M, ldc, N, "C");
+  const float* bptr = nullptr;
+  if (epi == 1 || epi == 2) {
+    TORCH_CHECK(bias.has_value(), "gemm: bias epilogue needs bias");
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() >= N, "gemm: bias too short");
+    bptr = bias->data_ptr<float>();
+  }
+  const void* xptr = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(aux.has_value(), "gemm: DRELU epilogue needs aux");
+    check_bf16(*aux, "aux");
+    check_extent(*aux, M, ldaux, N, "aux");
+    xptr = aux->data_ptr();
+  }
+  float* wptr = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(ws.has_value(), "gemm: split-K needs a workspace");
+    check_f32(*ws, "ws");
+    TORCH_CHECK(ws->numel() >= splits * M * ldc, "gemm: workspace too small");
+    wptr = ws->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(A.device());
+  const int rc = tdg_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bptr, xptr, (int)M, (int)N,
+                          (int)K, (int)lda, (int)ldb, (int)ldc, (int)ldaux, a_kc, b_kc, (int)epi,
+                          f32, (float)alpha, (float)beta, (int)tile_cfg, (int)splits, wptr,
+                          stream_of(A));
+  check_err(rc, "tdg gemm");
+}
+
+void colsum(const Tensor& X, const Tensor& out, const Tensor& part, int64_t M, int64_t N,
+            int64_t ld, int64_t rows_per_block, double beta) {
+  check_bf16(X, "X");
+  check_f32(out, "out");
+  check_f32(part, "part");
+  check_extent(X, M, ld, N, "X");
+  TORCH_CHECK(out.numel() >= N, "colsum: out too short");
+  TORCH_CHECK(part.numel() >= ((M + rows_per_block - 1) / rows_per_block) * N,
+              "colsum: partial buffer too small");
+  c10::hip::HIPGuard g(X.device());
+  tdg_colsum(X.data_ptr(), out.data_ptr<float>(), part.data_ptr<float>(), (int)M, (int)N, (int)ld,
+             (int)rows_per_block, (float)beta, stream_of(X));
+  check_err(0, "tdg colsum");
+}
+
+// ---------------------------------------------------------------- attention
+// q/k/v/o/do/dq/dk/dv are 4-D [B, L, H, hd] views (any strides, hd contiguous).
+void fill_qkv(tdg::AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
+  for (auto* t : {&q, &k, &v}) {
+    check_bf16(*t, "q/k/v");
+    TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1, "q/k/v must be [B,L,H,hd] with hd contiguous");
+  }
+  a.B = (int)q.size(0);
+  a.Lq = (int)q.size(1);
+  a.H = (int)q.size(2);
+  a.Lk = (int)k.size(1);
+  TORCH_CHECK(k.size(0) == a.B && v.size(0) == a.B && k.size(2) == a.H && v.size(2) == a.H &&
+                  v.size(1) == a.Lk && k.size(3) == q.size(3) && v.size(3) == q.size(3),
+              "attention: q/k/v shape mismatch");
+  a.q = (const uint16_t*)q.data_ptr();
+  a.k = (const uint16_t*)k.data_ptr();
+  a.v = (const uint16_t*)v.data_ptr();
+  a.q_sb = q.stride(0); a.q_sl = q.stride(1); a.q_sh = (int)q.stride(2);
+  a.k_sb = k.stride(0); a.k_sl = k.stride(1); a.k_sh = (int)k.stride(2);
+  a.v_sb = v.stride(0); a.v_sl = v.stride(1); a.v_sh = (int)v.stride(2);
+  for (auto* t : {&q, &k, &v}) {
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) == 0 &&
+                    t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 && t->stride(0) % 8 == 0,
+                "attention: q/k/v rows must be 16-byte aligned");
+  }
+}
+void check_like(const Tensor& t, const tdg::AttnArgs& a, int L, const char* n) {
+  check_bf16(t, n);
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.size(0) == a.B && t.size(1) == L &&
+                  t.size(2) == a.H,
+              n, ": bad shape/stride");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 8) == 0 && t.stride(1) % 4 == 0 &&
+                  t.stride(2) % 4 == 0,
+              n, ": rows must be 8-byte aligned");
+}
+
+void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out,
+              const Tensor& lse, const optional<Tensor>& kv_len, double scale, bool causal) {
+  tdg::AttnArgs a{};
+  fill_qkv(a, q, k, v);
+  check_like(out, a, a.Lq, "out");
+  check_f32(lse, "lse");
+  check_contig(lse, "lse");
+  TORCH_CHECK(lse.numel() == (int64_t)a.B * a.H * a.Lq, "lse must be [B,H,Lq]");
+  a.out = (uint16_t*)out.data_ptr();
+  a.o_sb = out.stride(0); a.o_sl = out.stride(1); a.o_sh = (int)out.stride(2);
+  a.lse = lse.data_ptr<float>();
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.scale = (float)scale;
+  a.causal = causal;
+  c10::hip::HIPGuard g(q.device());
+  check_err(tdg_attn_fwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_fwd");
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+              const Tensor& dout, const Tensor& lse, const Tensor& delta, const Tensor& dq,
+              const Tensor& dk, const Tensor& dv, const optional<Tensor>& kv_len, double scale,
+              bool causal) {
+  tdg::AttnArgs a{};
+  fill_qkv(a, q, k, v);
+  check_like(o, a, a.Lq, "o");
+  check_like(dout, a, a.Lq, "dout");
+  check_like(dq, a, a.Lq, "dq");
+  check_like(dk, a, a.Lk, "dk");
+  check_like(dv, a, a.Lk, "dv");
+  TORCH_CHECK(dout.stride(1) % 8 == 0 && o.stride(1) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(dout.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(o.data_ptr()) % 16) == 0,
+              "attn_bwd: o/dout rows must be 16-byte aligned");
+  check_f32(lse, "lse");
+  check_f32(delta, "delta");
+  TORCH_CHECK(lse.numel() == (int64_t)a.B * a.H * a.Lq && delta.numel() == lse.numel(),
+              "lse/delta must be [B,H,Lq]");
+  a.o = (const uint16_t*)o.data_ptr();
+  a.o_sb = o.stride(0); a.o_sl = o.stride(1); a.o_sh = (int)o.stride(2);
+  a.dout = (const uint16_t*)dout.data_ptr();
+  a.do_sb = dout.stride(0); a.do_sl = dout.stride(1); a.do_sh = (int)dout.stride(2);
+  a.dq = (uint16_t*)dq.data_ptr();
+  a.dq_sb = dq.stride(0); a.dq_sl = dq.stride(1); a.dq_sh = (int)dq.stride(2);
+  a.dk = (uint16_t*)dk.data_ptr();
+  a.dk_sb = dk.stride(0); a.dk_sl = dk.stride(1); a.dk_sh = (int)dk.stride(2);
+  a.dv = (uint16_t*)dv.data_ptr();
+  a.dv_sb = dv.stride(0); a.dv_sl = dv.stride(1); a.dv_sh = (int)dv.stride(2);
+  a.lse = lse.data_ptr<float>();
+  a.delta = delta.data_ptr<float>();
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.scale = (float)scale;
+  a.causal = causal;
+  c10::hip::HIPGuard g(q.device());
+  check_err(tdg_attn_bwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_bwd");
+}
+
+void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
+                const optional<Tensor>& kv_len, double scale, bool causal) {
+  tdg::AttnArgs a{};
+  fill_qkv(a, q, k, k);
+  check_f32(probs, "probs");
+  check_contig(probs, "probs");
+  TORCH_CHECK(probs.numel() == (int64_t)a.B * a.H * a.Lq * a.Lk, "probs must be [B,H,Lq,Lk]");
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.scale = (float)scale;
+  a.causal = causal;
+  c10::hip::HIPGuard g(q.device());
+  check_err(tdg_attn_probs(&a, (int)q.size(3), probs.data_ptr<float>(), stream_of(q)),
+            "tdg attn_probs");
+}
+
+// ---------------------------------------------------------------- layernorm
+const long long* ctr_ptr(const optional<Tensor>& c) {
+  if (!c.has_value()) return nullptr;
+  TORCH_CHECK(c->scalar_type() == at::kLong && c->numel() >= 1 && c->is_cuda(),
+              "rng counter must be an int64 GPU tensor");
+  return reinterpret_cast<const long long*>(c->data_ptr<int64_t>());
+}
+
+void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, const Tensor& beta,
+            const Tensor& y, const optional<Tensor>& hsave, const optional<Tensor>& mean,
+            const optional<Tensor>& rstd, double p, int64_t seed, const optional<Tensor>& ctr,
+            int64_t site, double eps) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  const int64_t D = x.size(-1), M = x.numel() / D;
+  check_bf16(y, "y");
+  check_contig(y, "y");
+  TORCH_CHECK(y.numel() == x.numel(), "ln: y shape");
+  if (s.has_value()) {
+    check_bf16(*s, "s");
+    check_contig(*s, "s");
+    TORCH_CHECK(s->numel() == x.numel(), "ln: s shape");
+  }
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  TORCH_CHECK(gamma.numel() == D && beta.numel() == D, "ln: gamma/beta shape");
+  if (hsave.has_value()) {
+    check_bf16(*hsave, "hsave");
+    TORCH_CHECK(hsave->numel() == x.numel() && hsave->is_contiguous(), "ln: hsave shape");
+  }
+  for (auto* t : {&mean, &rstd})
+    if (t->has_value()) {
+      check_f32(**t, "mean/rstd");
+      TORCH_CHECK((*t)->numel() == M, "ln: mean/rstd shape");
+    }
+  c10::hip::HIPGuard g(x.device());
+  const int rc = tdg_ln_fwd(x.data_ptr(), s.has_value() ? s->data_ptr() : nullptr,
+                            gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                            hsave.has_value() ? hsave->data_ptr() : nullptr,
+                            mean.has_value() ? mean->data_ptr<float>() : nullptr,
+                            rstd.has_value() ? rstd->data_ptr<float>() : nullptr, (int)M, (int)D,
+                            (float)p, (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, (float)eps,
+                            stream_of(x));
+  check_err(rc, "tdg ln_fwd");
+}
+
+void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Tensor& rstd,
+            const Tensor& gamma, const Tensor& dh, const optional<Tensor>& ds,
+            const optional<Tensor>& dres, const Tensor& dgamma, const Tensor& dbeta,
+            const optional<Tensor>& dbias, const Tensor& ws, double p, int64_t seed,
+            const optional<Tensor>& ctr, int64_t site, bool accumulate) {
+  check_bf16(dy, "dy");
+  check_contig(dy, "dy");
+  const int64_t D = dy.size(-1), M = dy.numel() / D;
+  for (auto* t : {&hsave, &dh}) {
+    check_bf16(*t, "hsave/dh");
+    TORCH_CHECK(t->numel() == dy.numel() && t->is_contiguous(), "ln_bwd: shape");
+  }
+  for (auto* t : {&ds, &dres})
+    if (t->has_value()) {
+      check_bf16(**t, "ds/dres");
+      TORCH_CHECK((*t)->numel() == dy.numel() && (*t)->is_contiguous(), "ln_bwd: ds/dres shape");
+    }
+  check_f32(mean, "mean");
+  check_f32(rstd, "rstd");
+  check_f32(gamma, "gamma");
+  check_f32(dgamma, "dgamma");
+  check_f32(dbeta, "dbeta");
+  TORCH_CHECK(mean.numel() == M && rstd.numel() == M, "ln_bwd: mean/rstd shape");
+  TORCH_CHECK(gamma.numel() == D && dgamma.numel() == D && dbeta.numel() == D, "ln_bwd: D");
+  if (dbias.has_value()) {
+    check_f32(*dbias, "dbias");
+    TORCH_CHECK(dbias->numel() == D && ds.has_value(), "ln_bwd: dbias needs ds");
+  }
+  check_f32(ws, "ws");
+  TORCH_CHECK(ws.numel() >= 3 * ((M + 63) / 64) * D, "ln_bwd: workspace too small");
+  c10::hip::HIPGuard g(dy.device());
+  const int rc = tdg_ln_bwd(
+      dy.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+      gamma.data_ptr<float>(), dh.data_ptr(), ds.has_value() ? ds->data_ptr() : nullptr,
+      dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(),
+      dbeta.data_ptr<float>(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
+      ws.data_ptr<float>(), (int)M, (int)D, (float)p, (uint64_t)seed, ctr_ptr(ctr),
+      (uint64_t)site, accumulate, stream_of(dy));
+  check_err(rc, "tdg ln_bwd");
+}
+
+// ---------------------------------------------------------------- embedding
+void embed_fwd(const Tensor& tok, const Tensor& table, const Tensor& pe, const Tensor& out,
+               double scale, double p, int64_t seed, const optional<Tensor>& ctr, int64_t site) {
+  TORCH_CHECK(tok.dim() == 2 && tok.is_contiguous() && tok.is_cuda(), "tok must be [B,L]");
+  const bool t64 = tok.scalar_type() == at::kLong;
+  TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
+  check_bf16(table, "table");
+  check_contig(table, "table");
+  check_f32(pe, "pe");
+  check_contig(pe, "pe");
+  check_bf16(out, "out");
+  check_contig(out, "out");
+  const int64_t D = table.size(1), L = tok.size(1), M = tok.numel();
+  TORCH_CHECK(pe.dim() == 2 && pe.size(1) == D && pe.size(0) >= L, "pe table too short");
+  TORCH_CHECK(out.numel() == M * D, "out shape");
+  c10::hip::HIPGuard g(tok.device());
+  const int rc = tdg_embed_fwd(tok.data_ptr(), t64, table.data_ptr(), pe.data_ptr<float>(),
+                               out.data_ptr(), (int)M, (int)L, (int)D, (float)scale, (float)p,
+                               (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, stream_of(tok));
+  check_err(rc, "tdg embed_fwd");
+}
+
+void embed_bwd(const Tensor& tok, const Tensor& dout, const Tensor& dtable, double scale,
+               double p, int64_t seed, const optional<Tensor>& ctr, int64_t site) {
+  TORCH_CHECK(tok.is_contiguous() && tok.is_cuda(), "tok");
+  const bool t64 = tok.scalar_type() == at::kLong;
+  TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
+  check_bf16(dout, "dout");
+  check_contig(dout, "dout");
+  check_f32(dtable, "dtable");
+  check_contig(dtable, "dtable");
+  const int64_t D = dtable.size(1), M = tok.numel();
+  TORCH_CHECK(dout.numel() == M * D, "dout shape");
+  c10::hip::HIPGuard g(tok.device());
+  const int rc = tdg_embed_bwd(tok.data_ptr(), t64, dout.data_ptr(), dtable.data_ptr<float>(),
+                               (int)M, (int)D, (float)scale, (float)p, (uint64_t)seed,
+                               ctr_ptr(ctr), (uint64_t)site, stream_of(tok));
+  check_err(rc, "tdg embed_bwd");
+}
+
+// ---------------------------------------------------------------- loss
+void count_tokens(const Tensor& labels, const Tensor& out) {
+  TORCH_CHECK(labels.is_contiguous() && labels.is_cuda(), "labels");
+  const bool l64 = labels.scalar_type() == at::kLong;
+  check_f32(out, "out");
+  c10::hip::HIPGuard g(labels.device());
+  check_err(tdg_count_tokens(labels.data_ptr(), l64, (int)labels.numel(), out.data_ptr<float>(),
+                             stream_of(labels)),
+            "tdg count_tokens");
+}
+
+void xent(const Tensor& logits, int64_t V, const Tensor& labels, const Tensor& ntok,
+          double workers, double smoothing, const Tensor& row_loss, const Tensor& row_correct,
+          bool write_grad) {
+  check_bf16(logits, "logits");
+  check_contig(logits, "logits");
+  const int64_t ldl = logits.size(-1), M = logits.numel() / ldl;
+  TORCH_CHECK(ldl % 2 == 0 && V <= ldl && V > 0, "xent: logits row must be even-padded >= V");
+  TORCH_CHECK(labels.numel() == M && labels.is_contiguous(), "xent: labels");
+  const bool l64 = labels.scalar_type() == at::kLong;
+  TORCH_CHECK(l64 || labels.scalar_type() == at::kInt, "labels int32/int64");
+  check_f32(ntok, "ntok");
+  check_f32(row_loss, "row_loss");
+  check_f32(row_correct, "row_correct");
+  TORCH_CHECK(row_loss.numel() == M && row_correct.numel() == M, "xent: row outputs");
+  c10::hip::HIPGuard g(logits.device());
+  check_err(tdg_xent(logits.data_ptr(), (int)M, (int)V, (int)ldl, labels.data_ptr(), l64,
+                     ntok.data_ptr<float>(), (float)workers, (float)smoothing,
+                     row_loss.data_ptr<float>(), row_correct.data_ptr<float>(), write_grad,
+                     stream_of(logits)),
+            "tdg xent");
+}
+
+void xent_stats(const Tensor& row_loss, const Tensor& row_correct, const Tensor& ntok,
+                double workers, const optional<Tensor>& step_out,
+                const optional<Tensor>& accum) {
+  check_f32(row_loss, "row_loss");
+  check_f32(row_correct, "row_correct");
+  if (step_out.has_value()) check_f32(*step_out, "step_out");
+  if (accum.has_value()) {
+    check_f32(*accum, "accum");
+    TORCH_CHECK(accum->numel() >= 4, "accum needs 4 slots");
+  }
+  c10::hip::HIPGuard g(row_loss.device());
+  check_err(tdg_xent_stats(row_loss.data_ptr<float>(), row_correct.data_ptr<float>(),
+                           (int)row_loss.numel(), ntok.data_ptr<float>(), (float)workers,
+                           step_out.has_value() ? step_out->data_ptr<float>() : nullptr,
+                           accum.has_value() ? accum->data_ptr<float>() : nullptr,
+                           stream_of(row_loss)),
+            "tdg xent_stats");
+}
+
+// ---------------------------------------------------------------- optimizer
+void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
+          const optional<Tensor>& shadow, const Tensor& step, double beta1, double beta2,
+          double eps, double lr_const, double d_model, double warmup, double grad_scale,
+          double weight_decay, int64_t sched, bool zero_grad) {
+  for (auto* t : {&p, &g, &m, &v}) {
+    check_f32(*t, "adam buffers");
+    check_contig(*t, "adam buffers");
+    TORCH_CHECK(t->numel() == p.numel(), "adam: buffer sizes differ");
+  }
+  TORCH_CHECK(p.numel() % 4 == 0, "adam: flat buffer must be a multiple of 4");
+  if (shadow.has_value()) {
+    check_bf16(*shadow, "shadow");
+    TORCH_CHECK(shadow->numel() == p.numel(), "adam: shadow size");
+  }
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.is_cuda(), "adam: step int64 GPU");
+  c10::hip::HIPGuard gd(p.device());
+  check_err(tdg_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                     v.data_ptr<float>(), shadow.has_value() ? shadow->data_ptr() : nullptr,
+                     p.numel(), reinterpret_cast<long long*>(step.data_ptr<int64_t>()), (float)beta1, (float)beta2, (float)eps,
+                     (float)lr_const, (float)d_model, (float)warmup, (float)grad_scale,
+                     (float)weight_decay, (int)sched, zero_grad, stream_of(p)),
+            "tdg adam");
+}
+
+void to_bf16(const Tensor& p, const Tensor& o) {
+  check_f32(p, "p");
+  check_bf16(o, "o");
+  TORCH_CHECK(p.numel() == o.numel() && p.is_contiguous() && o.is_contiguous(), "to_bf16 shape");
+  c10::hip::HIPGuard g(p.device());
+  check_err(tdg_to_bf16(p.data_ptr<float>(), o.data_ptr(), p.numel(), stream_of(p)),
+            "tdg to_bf16");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
+  m.def("gemm", &gemm);
+  m.def("colsum", &colsum);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_probs", &attn_probs);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("count_tokens", &count_tokens);
+  m.def("xent", &xent);
+  m.def("xent_stats", &xent_stats);
+  m.def("adam", &adam);
+  m.def("to_bf16", &to_bf16);
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,26 @@
+// Shared argument block for the attention kernels (host <-> device).
+#pragma once
+#include <stdint.h>
+
+namespace tdg {
+struct AttnArgs {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  const uint16_t* o;
+  const uint16_t* dout;
+  uint16_t* out;   // forward O
+  float* lse;    // [B, H, Lq] log2-domain LSE
+  float* delta;  // [B, H, Lq]
+  uint16_t* dq;
+  uint16_t* dk;
+  uint16_t* dv;
+  const int* kv_len;  // [B] valid key count, or null
+  long long q_sb, q_sl, k_sb, k_sl, v_sb, v_sl, o_sb, o_sl;
+  long long dq_sb, dq_sl, dk_sb, dk_sl, dv_sb, dv_sl, do_sb, do_sl;
+  int q_sh, k_sh, v_sh, o_sh, dq_sh, dk_sh, dv_sh, do_sh;
+  int B, H, Lq, Lk;
+  float scale;  // softmax scale (1/sqrt(dk))
+  int causal;
+};
+}  // namespace tdg

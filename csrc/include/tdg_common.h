@@ -1,0 +1,154 @@
+// Common device helpers for the gfx950 (CDNA4 / MI355X) kernels.
+//
+// Everything here is written for 64-lane wavefronts, MFMA 16x16x32 bf16 matrix
+// cores and the 64-bank LDS of gfx950. No portability layer: this is CDNA4 code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdg {
+
+typedef uint16_t bf16_t;  // raw bf16 bits in memory
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+typedef __attribute__((address_space(3))) short4_t lds_short4;
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 via the plain cast: hipcc -O3 emits the
+// gfx950 v_cvt_pk_bf16_f32 for it (keeps NaN a NaN, pairs adjacent converts).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+// Counter-based RNG: dropout masks are a pure function of (seed, offset,
+// element index) so backward regenerates them instead of storing them.
+struct Philox {
+  static __host__ __device__ __forceinline__ void round(uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                                        uint32_t& c3, uint32_t k0, uint32_t k1) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ c1 ^ k0;
+    const uint32_t n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+  }
+  // Returns 4 uint32 random words for counter (idx_lo, idx_hi, off_lo, off_hi).
+  static __host__ __device__ __forceinline__ void gen(uint64_t seed, uint64_t offset, uint64_t idx,
+                                                      uint32_t out[4]) {
+    uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
+    uint32_t c2 = (uint32_t)offset, c3 = (uint32_t)(offset >> 32);
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      round(c0, c1, c2, c3, k0, k1);
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+  }
+};
+
+// Keep-mask for element `e` of a dropout site. One Philox call covers 4
+// consecutive elements (e/4); word e%4 compared against the threshold.
+// keep iff u32 >= p * 2^32.
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t offset, uint64_t e,
+                                             uint32_t thresh) {
+  uint32_t r[4];
+  Philox::gen(seed, offset, e >> 2, r);
+  return r[e & 3] >= thresh;
+}
+
+// Dropout stream offset: a device-resident counter (advanced once per forward,
+// so HIP-graph replays draw fresh masks) times 4096 dropout sites + site id.
+__device__ __forceinline__ uint64_t rng_offset(const long long* ctr, uint64_t site) {
+  return (ctr ? (uint64_t)ctr[0] * 4096ull : 0ull) + site;
+}
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, const long long* ctr, uint64_t site,
+                                             uint64_t e, uint32_t thresh) {
+  return dropout_keep(seed, rng_offset(ctr, site), e, thresh);
+}
+
+// 8 consecutive keep bits for elements e0..e0+7 (e0 % 8 == 0): 2 Philox calls.
+__device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset, uint64_t e0,
+                                                  uint32_t thresh) {
+  uint32_t r[4], s[4];
+  Philox::gen(seed, offset, e0 >> 2, r);
+  Philox::gen(seed, offset, (e0 >> 2) + 1, s);
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m |= (r[i] >= thresh ? 1u : 0u) << i;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m |= (s[i] >= thresh ? 1u : 0u) << (4 + i);
+  return m;
+}
+
+// ---------------------------------------------------------------- MFMA
+__device__ __forceinline__ f32x4 mfma16(const short8_t& a, const short8_t& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, reads 4 rows x 16 columns (16-bit) and
+// delivers lane i column i (row q in element q). `p` is this lane's address:
+// row (base + (lane&15)>>2), columns 4*(lane&3)..+3.
+__device__ __forceinline__ short4_t lds_read_tr(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p));
+}
+
+__device__ __forceinline__ short8_t cat4(short4_t a, short4_t b) {
+  short8_t r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+__device__ __forceinline__ short pack_bf(float f) { return (short)f2bf(f); }
+
+// Pack 8 f32 -> 8 bf16 (as MFMA operand)
+__device__ __forceinline__ short8_t pack8(float a0, float a1, float a2, float a3, float a4, float a5,
+                                          float a6, float a7) {
+  short8_t r;
+  r[0] = pack_bf(a0); r[1] = pack_bf(a1); r[2] = pack_bf(a2); r[3] = pack_bf(a3);
+  r[4] = pack_bf(a4); r[5] = pack_bf(a5); r[6] = pack_bf(a6); r[7] = pack_bf(a7);
+  return r;
+}
+
+// XCD-aware bijective block remap (blocks b and b+8 share an XCD under the
+// observed round-robin dispatch): give each XCD a contiguous chunk of tiles so
+// neighbouring tiles share that XCD's L2. Speed-only; any placement is correct.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  constexpr int NX = 8;
+  if (nwg <= NX) return bid;
+  const int q = nwg / NX, r = nwg % NX;
+  const int x = bid % NX, i = bid / NX;
+  const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + i;
+}
+
+}  // namespace tdg

@@ -1,0 +1,116 @@
+// Fused token embedding + sqrt(d) scale + sinusoidal positional encoding +
+// dropout (forward), and the embedding-table gradient (backward).
+//
+// Replaces reference: distributed_training_transformer/transformer_model.py:
+// 29-53 (positional_encoding, interleaved sin/cos), 270-279 and 301-308
+// (Embedding -> *sqrt(d) -> +PE[:L] -> Dropout). The PE table is computed once
+// at model build (f32, [max_len, d], as the reference does) and read here; it
+// stays L2-resident.
+#include "tdg_common.h"
+
+namespace tdg {
+
+// out[row, :] = drop(table[tok[row]] * scale + pe[row % L])
+// One wave per row, VEC = D/64 elements per lane.
+template <int D, typename TokT>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(
+    const TokT* __restrict__ tok, const bf16_t* __restrict__ table, const float* __restrict__ pe,
+    bf16_t* __restrict__ out, int M, int L, float scale, float p, uint32_t thresh, uint64_t seed,
+    const long long* __restrict__ ctr, uint64_t site) {
+  constexpr int VEC = D / 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int pos = row % L;
+  const long long t = (long long)tok[row];
+  const bf16_t* src = table + t * D + lane * VEC;
+  const float* pr = pe + (size_t)pos * D + lane * VEC;
+  const size_t base = (size_t)row * D + lane * VEC;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+#pragma unroll
+  for (int c = 0; c < VEC; c += 2) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(src + c);
+    float v0 = bf2f((bf16_t)(w & 0xffff)) * scale + pr[c];
+    float v1 = bf2f((bf16_t)(w >> 16)) * scale + pr[c + 1];
+    if (p > 0.f) {
+      v0 = dropout_keep(seed, ctr, site, base + c, thresh) ? v0 * sc : 0.f;
+      v1 = dropout_keep(seed, ctr, site, base + c + 1, thresh) ? v1 * sc : 0.f;
+    }
+    *reinterpret_cast<uint32_t*>(out + base + c) =
+        (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+  }
+}
+
+// dtable[tok[row]] += drop_mask * dout[row] * scale  (f32 atomics into the
+// f32 master-gradient buffer; rows of 2*D bytes per wave-instruction pair).
+template <int D, typename TokT>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(
+    const TokT* __restrict__ tok, const bf16_t* __restrict__ dout, float* __restrict__ dtable,
+    int M, float scale, float p, uint32_t thresh, uint64_t seed, const long long* ctr, uint64_t site) {
+  constexpr int VEC = D / 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const long long t = (long long)tok[row];
+  const size_t rbase = (size_t)row * D;
+  const float sc = p > 0.f ? scale / (1.f - p) : scale;
+  // column c*64+lane: every atomic wave-instruction covers 256 contiguous bytes
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) {
+    const int col = c * 64 + lane;
+    float g = bf2f(dout[rbase + col]) * sc;
+    if (p > 0.f && !dropout_keep(seed, ctr, site, rbase + col, thresh)) g = 0.f;
+    atomicAdd(dtable + t * D + col, g);
+  }
+}
+
+}  // namespace tdg
+
+using namespace tdg;
+
+namespace {
+template <int D, typename TT>
+void fwd_d(const void* tok, const void* table, const float* pe, void* out, int M, int L,
+           float scale, float p, uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
+  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  hipLaunchKernelGGL((embed_fwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
+                     (const TT*)tok, (const bf16_t*)table, pe, (bf16_t*)out, M, L, scale, p,
+                     thresh, seed, ctr, site);
+}
+template <int D, typename TT>
+void bwd_d(const void* tok, const void* dout, float* dtable, int M, float scale, float p,
+           uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
+  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  hipLaunchKernelGGL((embed_bwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
+                     (const TT*)tok, (const bf16_t*)dout, dtable, M, scale, p, thresh, seed, ctr, site);
+}
+}  // namespace
+
+#define TDG_D_SWITCH(F, TT, ...)                  \
+  switch (D) {                                    \
+    case 128: F<128, TT>(__VA_ARGS__); return 0;  \
+    case 256: F<256, TT>(__VA_ARGS__); return 0;  \
+    case 512: F<512, TT>(__VA_ARGS__); return 0;  \
+    case 1024: F<1024, TT>(__VA_ARGS__); return 0; \
+    default: return -1;                           \
+  }
+
+extern "C" int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe,
+                             void* out, int M, int L, int D, float scale, float p, uint64_t seed,
+                             const long long* ctr, uint64_t site, hipStream_t st) {
+  if (tok64) {
+    TDG_D_SWITCH(fwd_d, long long, tok, table, pe, out, M, L, scale, p, seed, ctr, site, st)
+  } else {
+    TDG_D_SWITCH(fwd_d, int, tok, table, pe, out, M, L, scale, p, seed, ctr, site, st)
+  }
+}
+
+extern "C" int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, int M,
+                             int D, float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
+                             hipStream_t st) {
+  if (tok64) {
+    TDG_D_SWITCH(bwd_d, long long, tok, dout, dtable, M, scale, p, seed, ctr, site, st)
+  } else {
+    TDG_D_SWITCH(bwd_d, int, tok, dout, dtable, M, scale, p, seed, ctr, site, st)
+  }
+}

@@ -1,0 +1,292 @@
+// Fused post-LN residual block tail for gfx950:
+//   h = x + dropout(s);  y = LayerNorm(h) * gamma + beta      (eps = 1e-6)
+// Forward saves h (bf16) and per-row mean / rstd (f32); the dropout keep-mask
+// is regenerated from Philox in backward instead of being stored.
+// Backward computes dh (the residual gradient), ds = dh*mask/(1-p) (the
+// sublayer gradient), and deterministic two-stage column sums for dgamma,
+// dbeta and -- fused -- the bias gradient of the sublayer's output projection
+// (sum of ds over rows), saving a separate pass over ds.
+//
+// Replaces the reference's `LayerNormalization(epsilon=1e-6)(x + Dropout(...))`
+// (reference: distributed_training_transformer/transformer_model.py:187-204,
+// 219-248). One wave per row; each lane owns D/64 contiguous elements
+// (vectorised 4..32-byte accesses), so D in {128, 256, 512, 1024}.
+#include "tdg_common.h"
+
+namespace tdg {
+
+template <int VEC>
+struct RowVec {
+  float v[VEC];
+  __device__ __forceinline__ void load_bf(const bf16_t* p) {
+    if constexpr (VEC == 2) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+      v[0] = bf2f((bf16_t)(w & 0xffff));
+      v[1] = bf2f((bf16_t)(w >> 16));
+    } else if constexpr (VEC == 4) {
+      const short4_t w = *reinterpret_cast<const short4_t*>(p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = bf2f((bf16_t)w[i]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC / 8; ++c) {
+        const short8_t w = *reinterpret_cast<const short8_t*>(p + 8 * c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[8 * c + i] = bf2f((bf16_t)w[i]);
+      }
+    }
+  }
+  __device__ __forceinline__ void store_bf(bf16_t* p) const {
+    if constexpr (VEC == 2) {
+      *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    } else if constexpr (VEC == 4) {
+      short4_t w;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = (short)f2bf(v[i]);
+      *reinterpret_cast<short4_t*>(p) = w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC / 8; ++c) {
+        short8_t w;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = (short)f2bf(v[8 * c + i]);
+        *reinterpret_cast<short8_t*>(p + 8 * c) = w;
+      }
+    }
+  }
+};
+
+// keep bits for VEC consecutive elements starting at e0 (e0 % min(VEC,4) == 0)
+template <int VEC>
+__device__ __forceinline__ uint32_t keep_bits(uint64_t seed, const long long* ctr, uint64_t site,
+                                              uint64_t e0, uint32_t thresh) {
+  const uint64_t off = rng_offset(ctr, site);
+  uint32_t m = 0;
+  if constexpr (VEC == 2) {
+    uint32_t r[4];
+    Philox::gen(seed, off, e0 >> 2, r);
+    const int o = (int)(e0 & 3);
+    m = (r[o] >= thresh ? 1u : 0u) | ((r[o + 1] >= thresh ? 1u : 0u) << 1);
+  } else {
+#pragma unroll
+    for (int c = 0; c < VEC / 4; ++c) {
+      uint32_t r[4];
+      Philox::gen(seed, off, (e0 >> 2) + c, r);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) m |= (r[i] >= thresh ? 1u : 0u) << (4 * c + i);
+    }
+  }
+  return m;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ s, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ y, bf16_t* __restrict__ hsave,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, float p, uint32_t thresh,
+    uint64_t seed, const long long* ctr, uint64_t site, float eps) {
+  constexpr int VEC = D / 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const size_t base = (size_t)row * D + lane * VEC;
+  RowVec<VEC> h, t;
+  h.load_bf(x + base);
+  if (s) {
+    t.load_bf(s + base);
+    if (p > 0.f) {
+      const uint32_t km = keep_bits<VEC>(seed, ctr, site, base, thresh);
+      const float sc = 1.f / (1.f - p);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) t.v[i] = ((km >> i) & 1u) ? t.v[i] * sc : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h.v[i] += t.v[i];
+  }
+  // round h to bf16 first so that forward and backward see the same h
+  if (hsave) {
+    h.store_bf(hsave + base);
+    h.load_bf(hsave + base);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) sum += h.v[i];
+  const float mean = wave_sum(sum) * (1.f / D);
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const float d = h.v[i] - mean;
+    sq += d * d;
+  }
+  const float var = wave_sum(sq) * (1.f / D);
+  const float rstd = rsqrtf(var + eps);
+  RowVec<VEC> o;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int col = lane * VEC + i;
+    o.v[i] = (h.v[i] - mean) * rstd * gamma[col] + beta[col];
+  }
+  o.store_bf(y + base);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// rows_per_block rows per 256-thread block (4 waves); partial column sums to
+// part_g / part_b / part_s [gridDim.x, D].
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ hsave,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const float* __restrict__ gamma, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ ds_out,
+    const bf16_t* __restrict__ dres_in, float* __restrict__ part_g, float* __restrict__ part_b,
+    float* __restrict__ part_s, int M, int rows_per_block, float p, uint32_t thresh,
+    uint64_t seed, const long long* ctr, uint64_t site) {
+  constexpr int VEC = D / 64;
+  __shared__ float red[3][4][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ag[VEC], ab[VEC], as[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) ag[i] = ab[i] = as[i] = 0.f;
+  float gm[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) gm[i] = gamma[lane * VEC + i];
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (int row = r0 + w; row < r1; row += 4) {
+    const size_t base = (size_t)row * D + lane * VEC;
+    RowVec<VEC> g, h;
+    g.load_bf(dy + base);
+    h.load_bf(hsave + base);
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float sg = 0.f, sgx = 0.f;
+    float xh[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      xh[i] = (h.v[i] - mean) * rstd;
+      ag[i] += g.v[i] * xh[i];
+      ab[i] += g.v[i];
+      const float gg = g.v[i] * gm[i];
+      sg += gg;
+      sgx += gg * xh[i];
+    }
+    sg = wave_sum(sg) * (1.f / D);
+    sgx = wave_sum(sgx) * (1.f / D);
+    RowVec<VEC> dh;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) dh.v[i] = rstd * (g.v[i] * gm[i] - sg - xh[i] * sgx);
+    RowVec<VEC> ds = dh;
+    if (p > 0.f) {
+      const uint32_t km = keep_bits<VEC>(seed, ctr, site, base, thresh);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) ds.v[i] = ((km >> i) & 1u) ? dh.v[i] * sc : 0.f;
+    }
+    if (ds_out) {
+      ds.store_bf(ds_out + base);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
+    }
+    if (dres_in) {  // fused accumulation of the residual branch's other gradient
+      RowVec<VEC> e;
+      e.load_bf(dres_in + base);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) dh.v[i] += e.v[i];
+    }
+    dh.store_bf(dh_out + base);
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    red[0][w][lane * VEC + i] = ag[i];
+    red[1][w][lane * VEC + i] = ab[i];
+    red[2][w][lane * VEC + i] = as[i];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a0 += red[0][k][col];
+      a1 += red[1][k][col];
+      a2 += red[2][k][col];
+    }
+    part_g[(size_t)blockIdx.x * D + col] = a0;
+    part_b[(size_t)blockIdx.x * D + col] = a1;
+    if (part_s) part_s[(size_t)blockIdx.x * D + col] = a2;
+  }
+}
+
+// out[col] (+)= sum_p part[p, col] for up to 3 partial arrays.
+__global__ void colpart_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                      int D, int nparts, int accumulate) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * D + col];
+  out[col] = accumulate ? out[col] + s : s;
+}
+
+}  // namespace tdg
+
+using namespace tdg;
+
+namespace {
+template <int D>
+void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* beta, void* y,
+              void* hsave, float* mean, float* rstd, int M, float p, uint64_t seed,
+              const long long* ctr, uint64_t site, float eps, hipStream_t st) {
+  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  hipLaunchKernelGGL(ln_fwd_kernel<D>, dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)s, gamma, beta, (bf16_t*)y, (bf16_t*)hsave, mean, rstd, M, p,
+                     thresh, seed, ctr, site, eps);
+}
+template <int D>
+void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
+              const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
+              float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
+              int accumulate, hipStream_t st) {
+  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  const int rpb = 64;
+  const int nb = cdiv(M, rpb);
+  float* pg = ws;
+  float* pb = ws + (size_t)nb * D;
+  float* ps = dbias ? ws + 2 * (size_t)nb * D : nullptr;
+  hipLaunchKernelGGL(ln_bwd_kernel<D>, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
+                     (const bf16_t*)dres, pg, pb, ps, M, rpb, p, thresh, seed, ctr, site);
+  hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, pg, dgamma, D,
+                     nb, accumulate);
+  hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, pb, dbeta, D,
+                     nb, accumulate);
+  if (dbias)
+    hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, ps, dbias, D,
+                       nb, accumulate);
+}
+}  // namespace
+
+extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta,
+                          void* y, void* hsave, float* mean, float* rstd, int M, int D, float p,
+                          uint64_t seed, const long long* ctr, uint64_t site, float eps, hipStream_t st) {
+  switch (D) {
+    case 128: ln_fwd_d<128>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
+    case 256: ln_fwd_d<256>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
+    case 512: ln_fwd_d<512>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
+    case 1024: ln_fwd_d<1024>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
+    default: return -1;
+  }
+}
+
+// ws must hold 3 * ceil(M/64) * D floats.
+extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
+                          const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
+                          float* dbeta, float* dbias, float* ws, int M, int D, float p,
+                          uint64_t seed, const long long* ctr, uint64_t site, int accumulate, hipStream_t st) {
+  switch (D) {
+    case 128: ln_bwd_d<128>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
+    case 256: ln_bwd_d<256>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
+    case 512: ln_bwd_d<512>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
+    case 1024: ln_bwd_d<1024>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
+    default: return -1;
+  }
+}

@@ -1,0 +1,198 @@
+// Fused masked softmax cross-entropy + argmax accuracy, forward and backward
+// in one pass over the logits (gfx950).
+//
+// Replaces reference: distributed_training_transformer/transformer_model.py:7-26
+// (SparseCategoricalCrossentropy(from_logits, reduction='none') masked by
+// target != 0, token mean, divided by workers_count; accuracy = argmax match
+// over non-pad tokens). Optional label smoothing eps (reference: 0).
+//
+// Per row (one 256-thread workgroup): online max / sum-exp / first-argmax over
+// the vocabulary, then a second pass (row is L2-resident) writes
+//   dlogits = (softmax - onehot_smoothed) * scale   (scale = 1/(ntok*workers))
+// in place, or 0 for pad rows. Columns in [V, ldl) are zeroed so the padded
+// logits buffer can feed the dgrad / wgrad GEMMs directly.
+#include "tdg_common.h"
+
+namespace tdg {
+
+__device__ __forceinline__ void merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+template <typename LabT>
+__global__ __launch_bounds__(256) void xent_kernel(bf16_t* __restrict__ logits, int V, int ldl,
+                                                   const LabT* __restrict__ labels,
+                                                   const float* __restrict__ ntok,
+                                                   float workers, float smoothing,
+                                                   float* __restrict__ row_loss,
+                                                   float* __restrict__ row_correct,
+                                                   int write_grad) {
+  __shared__ float sm[4], ss[4], sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16_t* x = logits + (size_t)row * ldl;
+  const int lab = (int)labels[row];
+  // pass 1: max, sum-exp (online), argmax (first max), sum of logits (for smoothing)
+  float m = -INFINITY, s = 0.f, bv = -INFINITY, sumx = 0.f;
+  int bi = 0x7fffffff;
+  for (int c = tid * 2; c < V; c += 512) {
+    float v0, v1;
+    if (c + 1 < V) {
+      const uint32_t w2 = *reinterpret_cast<const uint32_t*>(x + c);
+      v0 = bf2f((bf16_t)(w2 & 0xffff));
+      v1 = bf2f((bf16_t)(w2 >> 16));
+    } else {
+      v0 = bf2f(x[c]);
+      v1 = -INFINITY;
+    }
+    const float mx = fmaxf(v0, v1);
+    if (mx > m) {
+      s = s * __expf(m - mx);
+      m = mx;
+    }
+    s += __expf(v0 - m) + (c + 1 < V ? __expf(v1 - m) : 0.f);
+    sumx += v0 + (c + 1 < V ? v1 : 0.f);
+    if (v0 > bv) { bv = v0; bi = c; }
+    if (c + 1 < V && v1 > bv) { bv = v1; bi = c + 1; }
+  }
+  // wave reduction
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    merge(m, s, m2, s2);
+    sumx += __shfl_xor(sumx, o, 64);
+    const float bv2 = __shfl_xor(bv, o, 64);
+    const int bi2 = __shfl_xor(bi, o, 64);
+    if (bv2 > bv || (bv2 == bv && bi2 < bi)) { bv = bv2; bi = bi2; }
+  }
+  if (lane == 0) { sm[w] = m; ss[w] = s; sv[w] = bv; si[w] = bi; }
+  __shared__ float sx[4];
+  if (lane == 0) sx[w] = sumx;
+  __syncthreads();
+  m = sm[0]; s = ss[0]; bv = sv[0]; bi = si[0]; sumx = sx[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    merge(m, s, sm[k], ss[k]);
+    sumx += sx[k];
+    if (sv[k] > bv || (sv[k] == bv && si[k] < bi)) { bv = sv[k]; bi = si[k]; }
+  }
+  const float lse = m + __logf(s);
+  const bool valid = lab != 0;
+  if (tid == 0) {
+    float loss = 0.f;
+    if (valid) {
+      const float xl = bf2f(x[lab]);
+      loss = (1.f - smoothing) * (lse - xl) + smoothing * (lse - sumx / (float)V);
+    }
+    row_loss[row] = loss;
+    row_correct[row] = (valid && bi == lab) ? 1.f : 0.f;
+  }
+  if (!write_grad) return;
+  __syncthreads();  // everyone read x[lab] before it is overwritten
+  const float scale = valid ? 1.f / (fmaxf(ntok[0], 1.f) * workers) : 0.f;
+  const float off = smoothing / (float)V;
+  for (int c = tid * 2; c < ldl; c += 512) {
+    float g0 = 0.f, g1 = 0.f;
+    if (c < V && valid) {
+      const float v0 = bf2f(x[c]);
+      g0 = (__expf(v0 - lse) - off - (c == lab ? 1.f - smoothing : 0.f)) * scale;
+      if (c + 1 < V) {
+        const float v1 = bf2f(x[c + 1]);
+        g1 = (__expf(v1 - lse) - off - (c + 1 == lab ? 1.f - smoothing : 0.f)) * scale;
+      }
+    }
+    if (c + 1 < ldl) {
+      *reinterpret_cast<uint32_t*>(x + c) = (uint32_t)f2bf(g0) | ((uint32_t)f2bf(g1) << 16);
+    } else {
+      x[c] = f2bf(g0);
+    }
+  }
+}
+
+// ntok = number of non-pad labels
+template <typename LabT>
+__global__ void count_tokens_kernel(const LabT* __restrict__ labels, int M, float* __restrict__ out) {
+  __shared__ float red[4];
+  float c = 0.f;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) c += labels[i] != 0 ? 1.f : 0.f;
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
+}
+
+// stats[0] += sum(row_loss)/(ntok*workers), stats[1] += correct/ntok (accuracy
+// ratio), stats[2] += 1 (batches), stats[3] += ntok; single block.
+__global__ void xent_stats_kernel(const float* __restrict__ row_loss,
+                                  const float* __restrict__ row_correct, int M,
+                                  const float* __restrict__ ntok, float workers,
+                                  float* __restrict__ step_out, float* __restrict__ accum) {
+  __shared__ float r1[4], r2[4];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    a += row_loss[i];
+    b += row_correct[i];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if ((threadIdx.x & 63) == 0) {
+    r1[threadIdx.x >> 6] = a;
+    r2[threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float n = fmaxf(ntok[0], 1.f);
+    const float loss = (r1[0] + r1[1] + r1[2] + r1[3]) / n / workers;
+    const float acc = (r2[0] + r2[1] + r2[2] + r2[3]) / n;
+    if (step_out) {
+      step_out[0] = loss;
+      step_out[1] = acc;
+    }
+    if (accum) {
+      accum[0] += loss;
+      accum[1] += acc;
+      accum[2] += 1.f;
+      accum[3] += ntok[0];
+    }
+  }
+}
+
+}  // namespace tdg
+
+using namespace tdg;
+
+extern "C" int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st) {
+  if (lab64)
+    hipLaunchKernelGGL(count_tokens_kernel<long long>, dim3(1), dim3(256), 0, st,
+                       (const long long*)labels, M, out);
+  else
+    hipLaunchKernelGGL(count_tokens_kernel<int>, dim3(1), dim3(256), 0, st, (const int*)labels, M,
+                       out);
+  return 0;
+}
+
+extern "C" int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64,
+                        const float* ntok, float workers, float smoothing, float* row_loss,
+                        float* row_correct, int write_grad, hipStream_t st) {
+  if (lab64)
+    hipLaunchKernelGGL(xent_kernel<long long>, dim3(M), dim3(256), 0, st, (bf16_t*)logits, V, ldl,
+                       (const long long*)labels, ntok, workers, smoothing, row_loss, row_correct,
+                       write_grad);
+  else
+    hipLaunchKernelGGL(xent_kernel<int>, dim3(M), dim3(256), 0, st, (bf16_t*)logits, V, ldl,
+                       (const int*)labels, ntok, workers, smoothing, row_loss, row_correct,
+                       write_grad);
+  return 0;
+}
+
+extern "C" int tdg_xent_stats(const float* row_loss, const float* row_correct, int M,
+                              const float* ntok, float workers, float* step_out, float* accum,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(xent_stats_kernel, dim3(1), dim3(256), 0, st, row_loss, row_correct, M, ntok,
+                     workers, step_out, accum);
+  return 0;
+}

@@ -1,0 +1,203 @@
+"""Thin, shape-checked launch wrappers over the gfx950 HIP kernels (`_C`).
+
+All GPU compute of the model goes through here. Outputs are allocated from
+the PyTorch caching allocator (stream-ordered, graph-capture safe); scratch
+buffers (split-K slabs, column-sum partials) come from a grow-only per-device
+workspace so a captured HIP graph sees stable addresses.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from tensorflow_distributed_on_gke_amd.ops._ext import C
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_DRELU = 0, 1, 2, 3
+NUM_CU = 256
+
+# ------------------------------------------------------------------ workspace
+_WS: Dict[Tuple[int, str], torch.Tensor] = {}
+
+
+def workspace(name: str, numel: int, device, dtype=torch.float32) -> torch.Tensor:
+    dev = torch.device(device)
+    key = (dev.index or 0, name)
+    t = _WS.get(key)
+    if t is None or t.numel() < numel or t.dtype != dtype:
+        t = torch.empty(max(numel, 1), dtype=dtype, device=dev)
+        _WS[key] = t
+    return t
+
+
+def reset_workspace() -> None:
+    _WS.clear()
+
+
+# ------------------------------------------------------------------ GEMM
+# tile configs (see csrc/kernels/gemm.hip): 0=128x128, 1=128x64, 2=64x128, 3=64x64
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+_CFG_OVERRIDE: Dict[Tuple[int, int, int, bool, bool], Tuple[int, int]] = {}
+
+
+def set_gemm_config(M: int, N: int, K: int, a_kc: bool, b_kc: bool, cfg: int, splits: int) -> None:
+    _CFG_OVERRIDE[(M, N, K, a_kc, b_kc)] = (cfg, splits)
+
+
+def choose_gemm(M: int, N: int, K: int, a_kc: bool = True, b_kc: bool = True) -> Tuple[int, int]:
+    """Pick (tile config, split-K). Aim for >= 2 workgroups per CU so the
+    256 CUs (8 XCDs) are filled; split K when output tiles are too few
+    (weight-gradient GEMMs: small output, K = tokens)."""
+    o = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
+    if o is not None:
+        return o
+    target = 2 * NUM_CU
+    for cfg in (0, 1, 2, 3):
+        bm, bn = _TILES[cfg]
+        if cfg == 1 and M < N:
+            continue
+        if cfg == 2 and N < M:
+            continue
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        if tiles >= target:
+            return cfg, 1
+    bm, bn = _TILES[3]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    splits = 1
+    if tiles < NUM_CU and K >= 1024:
+        splits = min(max(1, target // tiles), K // 256)
+        splits = max(1, splits)
+    return 3, splits
+
+
+def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
+         ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    tile, splits = cfg if cfg is not None else choose_gemm(M, N, K, a_kc, b_kc)
+    ws = None
+    if splits > 1:
+        ws = workspace("splitk", splits * M * ldc, A.device)
+    C().gemm(A, B, Cout, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha, beta,
+             tile, splits, ws)
+    return Cout
+
+
+def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
+               out: Optional[torch.Tensor] = None, ldc: Optional[int] = None) -> torch.Tensor:
+    """y[M,N] = x[M,K] @ w[N,K]^T + bias (bf16 out)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    ldc = ldc or N
+    if out is None:
+        out = torch.empty(M, ldc, dtype=torch.bfloat16, device=x2.device)
+    epi = EPI_BIAS_RELU if relu else (EPI_BIAS if bias is not None else EPI_NONE)
+    return gemm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), ldc, True, True, epi, bias=bias)
+
+
+def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor, N: int, relu_aux: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None, beta: float = 0.0) -> torch.Tensor:
+    """dx[M,K] = dy[M,N] @ w[N,K] (optionally * (relu_aux > 0))."""
+    M = dy2.shape[0]
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
+    epi = EPI_DRELU if relu_aux is not None else EPI_NONE
+    return gemm(dy2, w, out, M, K, N, dy2.stride(0), w.stride(0), out.stride(0), True, False, epi,
+                aux=relu_aux, ldaux=(relu_aux.stride(0) if relu_aux is not None else 0), beta=beta)
+
+
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, N: int, dw: torch.Tensor,
+                 beta: float = 0.0) -> torch.Tensor:
+    """dw[N,K] (f32) (+)= dy[M,N]^T @ x[M,K]."""
+    M, K = x2.shape
+    return gemm(dy2, x2, dw, N, K, M, dy2.stride(0), x2.stride(0), dw.stride(0), False, False,
+                EPI_NONE, beta=beta)
+
+
+def colsum(x2: torch.Tensor, N: int, out: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
+    """out[N] (+)= sum over rows of bf16 x2[M, N]."""
+    M = x2.shape[0]
+    rpb = 128
+    part = workspace("colsum", math.ceil(M / rpb) * N, x2.device)
+    C().colsum(x2, out, part, M, N, x2.stride(0), rpb, beta)
+    return out
+
+
+# ------------------------------------------------------------------ attention
+def attn_fwd(q, k, v, kv_len, scale: float, causal: bool):
+    B, Lq, H, hd = q.shape
+    out = torch.empty(B, Lq, H, hd, dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty(B, H, Lq, dtype=torch.float32, device=q.device)
+    C().attn_fwd(q, k, v, out, lse, kv_len, scale, causal)
+    return out, lse
+
+
+def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bool):
+    delta = workspace("attn_delta", lse.numel(), q.device)[: lse.numel()]
+    C().attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal)
+
+
+def attn_probs(q, k, kv_len, scale: float, causal: bool) -> torch.Tensor:
+    B, Lq, H, hd = q.shape
+    Lk = k.shape[1]
+    probs = torch.empty(B, H, Lq, Lk, dtype=torch.float32, device=q.device)
+    C().attn_probs(q, k, probs, kv_len, scale, causal)
+    return probs
+
+
+# ------------------------------------------------------------------ layernorm
+def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True):
+    D = x.shape[-1]
+    M = x.numel() // D
+    y = torch.empty_like(x)
+    h = torch.empty_like(x) if save else None
+    mean = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
+    C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps)
+    return y, h, mean, rstd
+
+
+def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
+           dres=None, accumulate=False):
+    D = dy.shape[-1]
+    M = dy.numel() // D
+    dh = torch.empty_like(dy)
+    need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
+    ds = torch.empty_like(dy) if need_ds else None
+    ws = workspace("ln_bwd", 3 * math.ceil(M / 64) * D, dy.device)
+    C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
+               accumulate)
+    if ds is None:
+        ds = dh
+    return dh, ds
+
+
+# ------------------------------------------------------------------ embedding / loss / optim
+def embed_fwd(tok, table, pe, scale, p, seed, ctr, site):
+    B, L = tok.shape
+    D = table.shape[1]
+    out = torch.empty(B, L, D, dtype=torch.bfloat16, device=tok.device)
+    C().embed_fwd(tok, table, pe, out, scale, p, seed, ctr, site)
+    return out
+
+
+def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site):
+    C().embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site)
+
+
+def count_tokens(labels, out):
+    C().count_tokens(labels, out)
+
+
+def xent(logits, V, labels, ntok, workers, smoothing, row_loss, row_correct, write_grad=True):
+    C().xent(logits, V, labels, ntok, workers, smoothing, row_loss, row_correct, write_grad)
+
+
+def xent_stats(row_loss, row_correct, ntok, workers, step_out=None, accum=None):
+    C().xent_stats(row_loss, row_correct, ntok, workers, step_out, accum)
+
+
+def adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale=1.0,
+         weight_decay=0.0, sched=1, zero_grad=True):
+    C().adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale,
+             weight_decay, sched, zero_grad)

@@ -1,0 +1,72 @@
+"""Keras-semantics Adam over the flat master buffer.
+
+GPU: one multi-tensor kernel (csrc/kernels/adam.hip) for the whole model,
+reading the step counter and evaluating the Noam schedule on device, fused with
+the bf16 shadow refresh and gradient zeroing. CPU: the same update in PyTorch.
+
+Reference: distributed_training_transformer/__main__.py:72-73
+(Adam(learning_rate=NoamSchedule(d_model), beta_1=0.9, beta_2=0.98, epsilon=1e-9)).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from tensorflow_distributed_on_gke_amd.models.params import ParamStore
+from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.train.schedule import noam_lr
+
+
+class Adam:
+    def __init__(self, store: ParamStore, d_model: int, warmup: float = 4000.0, beta1: float = 0.9,
+                 beta2: float = 0.98, eps: float = 1e-9, lr: Optional[float] = None,
+                 weight_decay: float = 0.0):
+        self.store = store
+        self.d_model = d_model
+        self.warmup = warmup
+        self.beta1, self.beta2, self.eps = beta1, beta2, eps
+        self.lr_const = lr  # None -> Noam schedule
+        self.weight_decay = weight_decay
+        dev = store.flat.device
+        self.m = torch.zeros_like(store.flat)
+        self.v = torch.zeros_like(store.flat)
+        # Keras `iterations`: device-resident so the step is graph-capturable
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    @property
+    def iterations(self) -> int:
+        return int(self.step.item())
+
+    def lr_at(self, step: int) -> float:
+        if self.lr_const is not None:
+            return self.lr_const
+        return noam_lr(step, self.d_model, self.warmup)
+
+    def apply(self, grad_scale: float = 1.0) -> None:
+        s = self.store
+        if s.flat.is_cuda:
+            K.adam(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, self.step, self.beta1,
+                   self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model), float(self.warmup),
+                   grad_scale, self.weight_decay, 0 if self.lr_const is not None else 1, True)
+            return
+        step = int(self.step.item())
+        lr = self.lr_at(step)
+        t = step + 1
+        lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+        g = s.flat_grad * grad_scale
+        self.m.add_((g - self.m) * (1 - self.beta1))
+        self.v.add_((g * g - self.v) * (1 - self.beta2))
+        s.flat.sub_(lr_t * self.m / (self.v.sqrt() + self.eps) + lr * self.weight_decay * s.flat)
+        s.flat_grad.zero_()
+        self.step += 1
+
+    def state_dict(self) -> dict:
+        return {"m": self.m.detach().cpu(), "v": self.v.detach().cpu(),
+                "iterations": torch.tensor(self.iterations)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.step.fill_(int(sd["iterations"]))

@@ -1,0 +1,74 @@
+"""One synchronous data-parallel training step, optionally captured into a HIP
+graph.
+
+step = dropout-stream advance -> teacher-forced forward -> fused CE/accuracy ->
+backward (gradients into the flat buffer, bucketed RCCL all-reduce started
+from inside backward) -> wait for the buckets -> multi-tensor Adam.
+
+Reference: distributed_training_transformer/__main__.py:105-132 (train_step
+inside strategy.run, apply_gradients all-reduce, strategy.reduce(SUM) of the
+per-replica losses). The per-step loss stays on device; it is summed over
+replicas only when the host reads it (log points).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
+from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
+from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
+from tensorflow_distributed_on_gke_amd.train.optim import Adam
+
+
+class TrainStep:
+    def __init__(self, model: Transformer, opt: Adam, ddp: Optional[DataParallel], workers: float,
+                 seed: int = 0, dropout: Optional[float] = None):
+        self.model = model
+        self.opt = opt
+        self.ddp = ddp
+        self.workers = float(workers)
+        dev = model.device
+        self.rt = RunCtx(training=True, dropout=model.cfg.dropout if dropout is None else dropout,
+                         seed=seed, ctr=torch.zeros(1, dtype=torch.int64, device=dev),
+                         store=model.store)
+        # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
+        self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.last = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.graph = None
+        self._static: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+
+    def eager(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        self.rt.ctr.add_(1)
+        self.model.loss_and_backward(src, tgt, self.rt, self.workers, accum=self.accum,
+                                     step_out=self.last)
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.opt.apply()
+        return self.last
+
+    # ------------------------------------------------------------------ HIP graph
+    def capture(self, src: torch.Tensor, tgt: torch.Tensor, warmup: int = 2) -> None:
+        """Capture the whole step (fwd+bwd+optimizer) into one HIP graph on
+        static input buffers. Warm-up iterations run on a side stream first so
+        lazily-allocated workspaces exist before capture."""
+        self._static = (src.clone(), tgt.clone())
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.eager(*self._static)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.eager(*self._static)
+        self.graph = g
+
+    def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        if self.graph is None:
+            return self.eager(src, tgt)
+        self._static[0].copy_(src, non_blocking=True)
+        self._static[1].copy_(tgt, non_blocking=True)
+        self.graph.replay()
+        return self.last

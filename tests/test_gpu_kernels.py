@@ -1,0 +1,286 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch f32 reference of
+the same op (bf16-rounded inputs). Runs on the MI355X box (`-m gpu`)."""
+import math
+
+import pytest
+import torch
+
+from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.ops import philox
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _close(a, b, tol, what):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= tol * ref, f"{what}: max err {err:.3e} vs max |ref| {ref:.3e}"
+
+
+# --------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 7010, 128),
+                                   (64, 64, 4096), (130, 520, 1000)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_gemm_forward_bias_relu(M, N, K, cfg):
+    x = _bf(_rand(M, K, seed=1))
+    w = _bf(_rand(N, K, scale=0.5, seed=2))
+    b = _rand(N, seed=3)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    K.gemm(x.to(DEV), w.to(DEV), out, M, N, K, K, K, N, True, True, K.EPI_BIAS_RELU,
+           bias=b.to(DEV), cfg=(cfg, 1))
+    _close(out, ref, 1e-2, "gemm fwd")
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches transposed C writes
+    n = 128
+    a = torch.eye(n, dtype=torch.bfloat16)
+    bmat = _bf(torch.arange(n * n, dtype=torch.float32).view(n, n) % 251)
+    out = torch.empty(n, n, dtype=torch.float32, device=DEV)
+    K.gemm(a.to(DEV), bmat.to(DEV), out, n, n, n, n, n, n, True, True, K.EPI_NONE, cfg=(0, 1))
+    torch.testing.assert_close(out.cpu(), bmat.float().t())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 128, 512), (300, 96, 200), (8192, 512, 2048)])
+@pytest.mark.parametrize("cfg", [0, 3])
+def test_gemm_dgrad_drelu(M, N, K, cfg):
+    dy = _bf(_rand(M, N, seed=4))
+    w = _bf(_rand(N, K, scale=0.5, seed=5))
+    h = _bf(_rand(M, K, seed=6))
+    ref = (dy.float() @ w.float()) * (h.float() > 0)
+    out = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+    K.gemm(dy.to(DEV), w.to(DEV), out, M, K, N, N, K, K, True, False, K.EPI_DRELU, aux=h.to(DEV),
+           ldaux=K, cfg=(cfg, 1))
+    _close(out, ref, 1e-2, "gemm dgrad")
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 128, 256, 1), (8192, 512, 512, 8), (1000, 7016, 64, 1),
+                                          (4000, 200, 136, 3)])
+def test_gemm_wgrad_f32(M, N, K, splits):
+    # dW[N,K] = dy[M,N]^T x[M,K]  (A and B both M/N-contiguous)
+    dy = _bf(_rand(M, N, seed=7))
+    x = _bf(_rand(M, K, seed=8))
+    ref = dy.float().t() @ x.float()
+    out = torch.full((N, K), 3.0, dtype=torch.float32, device=DEV)
+    ws = torch.empty(splits * N * K, dtype=torch.float32, device=DEV)
+    K_ = K
+    from tensorflow_distributed_on_gke_amd.ops._ext import C
+    C().gemm(dy.to(DEV), x.to(DEV), out, None, None, N, K_, M, N, K_, K_, 0, False, False, 0, 1.0, 0.0,
+             3, splits, ws if splits > 1 else None)
+    _close(out, ref, 2e-3, "gemm wgrad")
+    # beta accumulate
+    C().gemm(dy.to(DEV), x.to(DEV), out, None, None, N, K_, M, N, K_, K_, 0, False, False, 0, 1.0, 1.0,
+             0, 1, None)
+    _close(out, 2 * ref, 2e-3, "gemm wgrad beta=1")
+
+
+def test_linear_wrappers_padded_vocab():
+    M, d, V, Vp = 300, 128, 7010, 7040
+    x = _bf(_rand(M, d, seed=9)).to(DEV)
+    w = _bf(_rand(V, d, scale=0.3, seed=10)).to(DEV)
+    b = _rand(V, seed=11).to(DEV)
+    lg = K.linear_fwd(x, w, b, ldc=Vp)
+    ref = x.float() @ w.float().t() + b
+    _close(lg[:, :V], ref, 1e-2, "vocab fwd")
+    dl = _bf(_rand(M, Vp, seed=12)).to(DEV)
+    dl[:, V:] = 0
+    dx = K.linear_dgrad(dl, w, V)
+    _close(dx, dl[:, :V].float() @ w.float(), 1e-2, "vocab dgrad")
+    dw = torch.empty(V, d, dtype=torch.float32, device=DEV)
+    K.linear_wgrad(dl, x, V, dw)
+    _close(dw, dl[:, :V].float().t() @ x.float(), 2e-3, "vocab wgrad")
+    db = torch.empty(V, dtype=torch.float32, device=DEV)
+    K.colsum(dl, V, db)
+    _close(db, dl[:, :V].float().sum(0), 1e-3, "colsum")
+
+
+# --------------------------------------------------------------------------- attention
+def _ref_attn(q, k, v, kv_len, causal, scale):
+    q, k, v = q.float(), k.float(), v.float()
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    B, H, Lq, Lk = s.shape
+    keys = torch.arange(Lk)
+    mask = torch.zeros(B, 1, Lq, Lk, dtype=torch.bool)
+    if kv_len is not None:
+        mask |= (keys.view(1, 1, 1, Lk) >= kv_len.view(B, 1, 1, 1))
+    if causal:
+        mask |= (keys.view(1, Lk) > torch.arange(Lq).view(Lq, 1)).view(1, 1, Lq, Lk)
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, v), p
+
+
+@pytest.mark.parametrize("hd", [16, 32, 64, 128])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("Lq,Lk", [(128, 128), (70, 200), (1, 33)])
+def test_attention_fwd_bwd(hd, causal, Lq, Lk):
+    if causal and Lq != Lk:
+        pytest.skip("causal self-attention only")
+    B, H = 3, 2
+    torch.manual_seed(0)
+    q = _bf(torch.randn(B, Lq, H, hd))
+    k = _bf(torch.randn(B, Lk, H, hd))
+    v = _bf(torch.randn(B, Lk, H, hd))
+    kv_len = torch.tensor([Lk, max(1, Lk // 2), max(1, Lk - 5)], dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref, _ = _ref_attn(qr, kr, vr, kv_len, causal, scale)
+    out, lse = K.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), kv_len.to(DEV), scale, causal)
+    _close(out, ref.detach(), 2e-2, "attn fwd")
+    dout = _bf(torch.randn(B, Lq, H, hd))
+    ref.backward(dout.float())
+    dq = torch.empty_like(q, device=DEV)
+    dk = torch.empty_like(k, device=DEV)
+    dv = torch.empty_like(v, device=DEV)
+    K.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), out, dout.to(DEV), lse, dq, dk, dv, kv_len.to(DEV),
+               scale, causal)
+    _close(dv, vr.grad, 3e-2, "attn dv")
+    _close(dk, kr.grad, 3e-2, "attn dk")
+    _close(dq, qr.grad, 3e-2, "attn dq")
+
+
+def test_attention_strided_fused_qkv():
+    # q/k/v as strided views into a fused [B, L, 3, H, hd] projection output
+    B, L, H, hd = 2, 96, 8, 64
+    qkv = _bf(torch.randn(B, L, 3, H, hd)).to(DEV)
+    kv_len = torch.tensor([96, 50], dtype=torch.int32, device=DEV)
+    out, _ = K.attn_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], kv_len, 0.125, True)
+    c = qkv.cpu()
+    ref, _ = _ref_attn(c[:, :, 0], c[:, :, 1], c[:, :, 2], kv_len.cpu(), True, 0.125)
+    _close(out, ref, 2e-2, "strided attn")
+
+
+def test_attention_probs():
+    B, Lq, Lk, H, hd = 2, 10, 17, 2, 64
+    q = _bf(torch.randn(B, Lq, H, hd))
+    k = _bf(torch.randn(B, Lk, H, hd))
+    kv_len = torch.tensor([17, 9], dtype=torch.int32)
+    pr = K.attn_probs(q.to(DEV), k.to(DEV), kv_len.to(DEV), 0.125, False)
+    _, ref = _ref_attn(q, k, k, kv_len, False, 0.125)
+    _close(pr, ref, 1e-3, "probs")
+
+
+# --------------------------------------------------------------------------- layernorm
+@pytest.mark.parametrize("D", [128, 512, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_add_ln_fwd_bwd(D, p):
+    M = 300
+    seed, site = 1234, 7
+    ctr = torch.tensor([5], dtype=torch.int64)
+    x = _bf(torch.randn(M, D))
+    s = _bf(torch.randn(M, D))
+    gamma = torch.rand(D) + 0.5
+    beta = torch.randn(D)
+    y, h, mean, rstd = K.ln_fwd(x.to(DEV), s.to(DEV), gamma.to(DEV), beta.to(DEV), p, seed,
+                                ctr.to(DEV), site)
+    keep = philox.keep_mask(seed, philox.rng_offset(5, site), M * D, p).view(M, D).float() if p > 0 else torch.ones(M, D)
+    ks = keep / (1 - p)
+    xr = x.float().requires_grad_()
+    sr = s.float().requires_grad_()
+    gr = gamma.clone().requires_grad_()
+    br = beta.clone().requires_grad_()
+    hr = xr + sr * ks
+    ref = torch.nn.functional.layer_norm(hr, (D,), gr, br, 1e-6)
+    _close(y, ref.detach(), 2e-2, "ln fwd")
+    dy = _bf(torch.randn(M, D))
+    ref.backward(dy.float())
+    dg = torch.empty(D, device=DEV)
+    db = torch.empty(D, device=DEV)
+    dbias = torch.empty(D, device=DEV)
+    dh, ds = K.ln_bwd(dy.to(DEV), h, mean, rstd, gamma.to(DEV), dg, db, dbias, p, seed, ctr.to(DEV), site)
+    _close(dh, xr.grad, 3e-2, "ln dh")
+    _close(ds, sr.grad, 3e-2, "ln ds")
+    _close(dg, gr.grad, 2e-2, "ln dgamma")
+    _close(db, br.grad, 1e-2, "ln dbeta")
+    _close(dbias, sr.grad.sum(0), 2e-2, "ln fused dbias")
+
+
+# --------------------------------------------------------------------------- embedding
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embed_fwd_bwd(p):
+    B, L, D, V = 4, 37, 128, 500
+    from tensorflow_distributed_on_gke_amd.models.transformer import positional_encoding
+    tok = torch.randint(0, V, (B, L))
+    table = _bf(torch.randn(V, D) * 0.05)
+    pe = positional_encoding(64, D)
+    ctr = torch.tensor([3], dtype=torch.int64)
+    out = K.embed_fwd(tok.to(DEV), table.to(DEV), pe.to(DEV), math.sqrt(D), p, 77, ctr.to(DEV), 2)
+    ks = (philox.keep_mask(77, philox.rng_offset(3, 2), B * L * D, p).view(B, L, D).float() / (1 - p)
+          if p > 0 else torch.ones(B, L, D))
+    ref = (table.float()[tok] * math.sqrt(D) + pe[:L]) * ks
+    _close(out, ref, 1e-2, "embed fwd")
+    dout = _bf(torch.randn(B, L, D))
+    dt = torch.zeros(V, D, device=DEV)
+    K.embed_bwd(tok.to(DEV), dout.to(DEV), dt, math.sqrt(D), p, 77, ctr.to(DEV), 2)
+    refg = torch.zeros(V, D).index_add_(0, tok.view(-1), (dout.float() * ks * math.sqrt(D)).view(-1, D))
+    _close(dt, refg, 1e-4, "embed bwd")
+
+
+# --------------------------------------------------------------------------- cross-entropy
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_xent(smoothing):
+    M, V, Vp = 257, 7010, 7040
+    lg = _bf(torch.randn(M, Vp) * 3)
+    lab = torch.randint(1, V, (M,))
+    lab[::7] = 0
+    ntok = torch.zeros(1, device=DEV)
+    lgd = lg.clone().to(DEV)
+    K.count_tokens(lab.to(DEV), ntok)
+    rl = torch.empty(M, device=DEV)
+    rc = torch.empty(M, device=DEV)
+    K.xent(lgd, V, lab.to(DEV), ntok, 2.0, smoothing, rl, rc, True)
+    so = torch.empty(2, device=DEV)
+    acc = torch.zeros(4, device=DEV)
+    K.xent_stats(rl, rc, ntok, 2.0, so, acc)
+    x = lg.float()[:, :V].requires_grad_()
+    mask = (lab != 0).float()
+    n = mask.sum()
+    logp = torch.log_softmax(x, -1)
+    nll = -logp.gather(1, lab.view(-1, 1)).squeeze(1)
+    row = ((1 - smoothing) * nll + smoothing * (-logp.mean(-1))) * mask
+    loss = row.sum() / n / 2.0
+    loss.backward()
+    accr = ((x.argmax(-1) == lab).float() * mask).sum() / n
+    assert ntok.item() == n.item()
+    assert abs(so[0].item() - loss.item()) < 1e-3 * abs(loss.item())
+    assert abs(so[1].item() - accr.item()) < 1e-6
+    _close(lgd[:, :V], x.grad, 2e-2, "dlogits")
+    assert lgd[:, V:].float().abs().max().item() == 0.0
+    assert acc[2].item() == 1.0
+
+
+# --------------------------------------------------------------------------- adam
+def test_adam_keras_semantics():
+    n = 4096
+    p = torch.randn(n)
+    g = torch.randn(n)
+    m = torch.zeros(n)
+    v = torch.zeros(n)
+    pd, gd, md, vd = (t.clone().to(DEV) for t in (p, g, m, v))
+    sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    step = torch.tensor([10], dtype=torch.int64, device=DEV)
+    K.adam(pd, gd, md, vd, sh, step, 0.9, 0.98, 1e-9, 0.0, 128.0, 4000.0)
+    lr = 128 ** -0.5 * min(10 * 4000 ** -1.5, 10 ** -0.5)
+    t = 11
+    lr_t = lr * math.sqrt(1 - 0.98 ** t) / (1 - 0.9 ** t)
+    m_ = g * 0.1
+    v_ = g * g * 0.02
+    ref = p - lr_t * m_ / (v_.sqrt() + 1e-9)
+    _close(pd, ref, 1e-5, "adam p")
+    _close(md, m_, 1e-6, "adam m")
+    assert step.item() == 11
+    assert gd.abs().max().item() == 0.0
+    _close(sh, ref, 1e-2, "adam shadow")
