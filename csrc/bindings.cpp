@@ -5,7 +5,7 @@
 // kernel never sees operands its grid does not assume.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "tdg_attn.h"
 
@@ -92,20 +92,22 @@ void gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tens
   TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0 &&
                   (reinterpret_cast<uintptr_t>(B.data_ptr()) % 16) == 0,
               "gemm: A/B must be 16-byte aligned");
-  // A(m,k): KC -> [M][lda] ; MC -> [K][lda]
+  // A(m,k): KC -> [M][lda] ; MC -> [K][lda]. The kernel reads whole 16-byte
+  // chunks, so the contiguous dimension must be readable up to a multiple of 8.
+  auto r8 = [](int64_t v) { return (v + 7) / 8 * 8; };
   if (a_kc) {
-    TORCH_CHECK(lda >= K, "gemm: lda < K");
-    check_extent(A, M, lda, K, "A");
+    TORCH_CHECK(lda >= r8(K), "gemm: lda < round8(K)");
+    check_extent(A, M, lda, r8(K), "A");
   } else {
-    TORCH_CHECK(lda >= M, "gemm: lda < M");
-    check_extent(A, K, lda, M, "A");
+    TORCH_CHECK(lda >= r8(M), "gemm: lda < round8(M)");
+    check_extent(A, K, lda, r8(M), "A");
   }
   if (b_kc) {
-    TORCH_CHECK(ldb >= K, "gemm: ldb < K");
-    check_extent(B, N, ldb, K, "B");
+    TORCH_CHECK(ldb >= r8(K), "gemm: ldb < round8(K)");
+    check_extent(B, N, ldb, r8(K), "B");
   } else {
-    TORCH_CHECK(ldb >= N, "gemm: ldb < N");
-    check_extent(B, K, ldb, N, "B");
+    TORCH_CHECK(ldb >= r8(N), "gemm: ldb < round8(N)");
+    check_extent(B, K, ldb, r8(N), "B");
   }
   TORCH_CHECK(ldc >= N, "gemm: ldc < N");
   check_extent(C, M, ldc, N, "C");
@@ -130,7 +132,7 @@ void gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tens
     TORCH_CHECK(ws->numel() >= splits * M * ldc, "gemm: workspace too small");
     wptr = ws->data_ptr<float>();
   }
-  c10::hip::HIPGuard g(A.device());
+  c10::DeviceGuard g(A.device());
   const int rc = tdg_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bptr, xptr, (int)M, (int)N,
                           (int)K, (int)lda, (int)ldb, (int)ldc, (int)ldaux, a_kc, b_kc, (int)epi,
                           f32, (float)alpha, (float)beta, (int)tile_cfg, (int)splits, wptr,
@@ -147,7 +149,7 @@ void colsum(const Tensor& X, const Tensor& out, const Tensor& part, int64_t M, i
   TORCH_CHECK(out.numel() >= N, "colsum: out too short");
   TORCH_CHECK(part.numel() >= ((M + rows_per_block - 1) / rows_per_block) * N,
               "colsum: partial buffer too small");
-  c10::hip::HIPGuard g(X.device());
+  c10::DeviceGuard g(X.device());
   tdg_colsum(X.data_ptr(), out.data_ptr<float>(), part.data_ptr<float>(), (int)M, (int)N, (int)ld,
              (int)rows_per_block, (float)beta, stream_of(X));
   check_err(0, "tdg colsum");
@@ -206,7 +208,7 @@ void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   }
   a.scale = (float)scale;
   a.causal = causal;
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   check_err(tdg_attn_fwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_fwd");
 }
 
@@ -247,7 +249,7 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   }
   a.scale = (float)scale;
   a.causal = causal;
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   check_err(tdg_attn_bwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_bwd");
 }
 
@@ -264,7 +266,7 @@ void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
   }
   a.scale = (float)scale;
   a.causal = causal;
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   check_err(tdg_attn_probs(&a, (int)q.size(3), probs.data_ptr<float>(), stream_of(q)),
             "tdg attn_probs");
 }
@@ -304,7 +306,7 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
       check_f32(**t, "mean/rstd");
       TORCH_CHECK((*t)->numel() == M, "ln: mean/rstd shape");
     }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   const int rc = tdg_ln_fwd(x.data_ptr(), s.has_value() ? s->data_ptr() : nullptr,
                             gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
                             hsave.has_value() ? hsave->data_ptr() : nullptr,
@@ -344,8 +346,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
     TORCH_CHECK(dbias->numel() == D && ds.has_value(), "ln_bwd: dbias needs ds");
   }
   check_f32(ws, "ws");
-  TORCH_CHECK(ws.numel() >= 3 * ((M + 63) / 64) * D, "ln_bwd: workspace too small");
-  c10::hip::HIPGuard g(dy.device());
+  TORCH_CHECK(ws.numel() >= 3 * ((M + 31) / 32) * D, "ln_bwd: workspace too small");
+  c10::DeviceGuard g(dy.device());
   const int rc = tdg_ln_bwd(
       dy.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
       gamma.data_ptr<float>(), dh.data_ptr(), ds.has_value() ? ds->data_ptr() : nullptr,
@@ -371,7 +373,7 @@ void embed_fwd(const Tensor& tok, const Tensor& table, const Tensor& pe, const T
   const int64_t D = table.size(1), L = tok.size(1), M = tok.numel();
   TORCH_CHECK(pe.dim() == 2 && pe.size(1) == D && pe.size(0) >= L, "pe table too short");
   TORCH_CHECK(out.numel() == M * D, "out shape");
-  c10::hip::HIPGuard g(tok.device());
+  c10::DeviceGuard g(tok.device());
   const int rc = tdg_embed_fwd(tok.data_ptr(), t64, table.data_ptr(), pe.data_ptr<float>(),
                                out.data_ptr(), (int)M, (int)L, (int)D, (float)scale, (float)p,
                                (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, stream_of(tok));
@@ -389,7 +391,7 @@ void embed_bwd(const Tensor& tok, const Tensor& dout, const Tensor& dtable, doub
   check_contig(dtable, "dtable");
   const int64_t D = dtable.size(1), M = tok.numel();
   TORCH_CHECK(dout.numel() == M * D, "dout shape");
-  c10::hip::HIPGuard g(tok.device());
+  c10::DeviceGuard g(tok.device());
   const int rc = tdg_embed_bwd(tok.data_ptr(), t64, dout.data_ptr(), dtable.data_ptr<float>(),
                                (int)M, (int)D, (float)scale, (float)p, (uint64_t)seed,
                                ctr_ptr(ctr), (uint64_t)site, stream_of(tok));
@@ -401,7 +403,7 @@ void count_tokens(const Tensor& labels, const Tensor& out) {
   TORCH_CHECK(labels.is_contiguous() && labels.is_cuda(), "labels");
   const bool l64 = labels.scalar_type() == at::kLong;
   check_f32(out, "out");
-  c10::hip::HIPGuard g(labels.device());
+  c10::DeviceGuard g(labels.device());
   check_err(tdg_count_tokens(labels.data_ptr(), l64, (int)labels.numel(), out.data_ptr<float>(),
                              stream_of(labels)),
             "tdg count_tokens");
@@ -421,7 +423,7 @@ void xent(const Tensor& logits, int64_t V, const Tensor& labels, const Tensor& n
   check_f32(row_loss, "row_loss");
   check_f32(row_correct, "row_correct");
   TORCH_CHECK(row_loss.numel() == M && row_correct.numel() == M, "xent: row outputs");
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   check_err(tdg_xent(logits.data_ptr(), (int)M, (int)V, (int)ldl, labels.data_ptr(), l64,
                      ntok.data_ptr<float>(), (float)workers, (float)smoothing,
                      row_loss.data_ptr<float>(), row_correct.data_ptr<float>(), write_grad,
@@ -439,7 +441,7 @@ void xent_stats(const Tensor& row_loss, const Tensor& row_correct, const Tensor&
     check_f32(*accum, "accum");
     TORCH_CHECK(accum->numel() >= 4, "accum needs 4 slots");
   }
-  c10::hip::HIPGuard g(row_loss.device());
+  c10::DeviceGuard g(row_loss.device());
   check_err(tdg_xent_stats(row_loss.data_ptr<float>(), row_correct.data_ptr<float>(),
                            (int)row_loss.numel(), ntok.data_ptr<float>(), (float)workers,
                            step_out.has_value() ? step_out->data_ptr<float>() : nullptr,
@@ -464,7 +466,7 @@ void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
     TORCH_CHECK(shadow->numel() == p.numel(), "adam: shadow size");
   }
   TORCH_CHECK(step.scalar_type() == at::kLong && step.is_cuda(), "adam: step int64 GPU");
-  c10::hip::HIPGuard gd(p.device());
+  c10::DeviceGuard gd(p.device());
   check_err(tdg_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                      v.data_ptr<float>(), shadow.has_value() ? shadow->data_ptr() : nullptr,
                      p.numel(), reinterpret_cast<long long*>(step.data_ptr<int64_t>()), (float)beta1, (float)beta2, (float)eps,
@@ -477,7 +479,7 @@ void to_bf16(const Tensor& p, const Tensor& o) {
   check_f32(p, "p");
   check_bf16(o, "o");
   TORCH_CHECK(p.numel() == o.numel() && p.is_contiguous() && o.is_contiguous(), "to_bf16 shape");
-  c10::hip::HIPGuard g(p.device());
+  c10::DeviceGuard g(p.device());
   check_err(tdg_to_bf16(p.data_ptr<float>(), o.data_ptr(), p.numel(), stream_of(p)),
             "tdg to_bf16");
 }

@@ -22,6 +22,9 @@
 // (reference: distributed_training_transformer/transformer_model.py:119-122,
 // 165, 172-174, 333) and their gradients.
 #include "tdg_common.h"
+#include "tdg_reduce.h"
+
+#include <type_traits>
 
 namespace tdg {
 
@@ -44,9 +47,9 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
   if constexpr (KC) {
     const int seg = (byte >> 5) ^ ((row >> 1) & 3);
     return row * (BK * 2) + (seg << 5) + (byte & 31);
-  } else if constexpr (R == 128) {
+  } else if constexpr (R >= 128) {
     const int seg = (byte >> 5) ^ ((row & 3) | (((row >> 3) & 1) << 2));
-    return row * 256 + (seg << 5) + (byte & 31);
+    return row * (R * 2) + (seg << 5) + (byte & 31);
   } else {
     static_assert(R == 64, "MN-contiguous tiles must be 64 or 128 wide");
     const int seg = (byte >> 5) ^ (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
@@ -54,73 +57,100 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
   }
 }
 
-// Staging of one operand tile (R = BM or BN rows/cols, BK deep).
-template <bool KC, int R, int NT>
-struct Stage {
-  static constexpr int CHUNKS = R * BK * 2 / 16;  // 16-byte chunks per tile
-  static constexpr int PER = CHUNKS / NT;
-  static_assert(CHUNKS % NT == 0, "tile/thread mismatch");
-  short8_t v[PER];
-
-  // Global load of tile (mn0, k0). `len` = M or N, ld in elements.
-  __device__ __forceinline__ void load(const bf16_t* __restrict__ X, int ld, int len, int K, int mn0,
-                                       int k0, int tid) {
+// Direct global->LDS staging (global_load_lds_dwordx4) of one operand tile.
+// One wave instruction writes 1 KiB of LDS linearly (wave-uniform base +
+// 16*lane), so the XOR swizzle of the image is applied to the per-lane SOURCE
+// address: lane l fetches the logical 16-byte chunk that belongs at physical
+// position l of the piece. Out-of-range rows/columns are clamped to valid
+// addresses (their outputs are never stored); the K tail of the last tile is
+// zeroed in LDS after it lands (zero_ktail).
+template <bool KC, int R, int NW>
+struct Glds {
+  static constexpr int BYTES = R * BK * 2;
+  static constexpr int P = BYTES / (NW * 1024);  // pieces per wave per tile
+  static_assert(BYTES % (NW * 1024) == 0, "tile must split into 1 KiB pieces per wave");
+  static constexpr int RPP = KC ? 8 : 1024 / (R * 2);  // tile rows per piece
+  static constexpr int CPR = KC ? 8 : R / 8;           // 16-byte chunks per tile row
+  // per piece: element offset of this lane's chunk relative to (mn0, k0)
+  int row[P];   // KC: mn row within tile; MC: k row within tile
+  int col[P];   // KC: k element offset (chunk*8); MC: mn element offset
+  __device__ __forceinline__ void init(int wid, int lane) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = tid + i * NT;
-      int mn, kk;
+    for (int i = 0; i < P; ++i) {
+      const int j = wid * P + i;
+      const int r = j * RPP + lane / CPR;
+      const int pc = lane % CPR;
+      int c;
       if constexpr (KC) {
-        const int row = id >> 3, c = id & 7;
-        mn = mn0 + row;
-        kk = k0 + c * 8;
-        if (mn < len && kk + 8 <= K) {
-          v[i] = *reinterpret_cast<const short8_t*>(X + (size_t)mn * ld + kk);
-        } else {
-          short8_t t = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (mn < len) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (kk + e < K) t[e] = (short)X[(size_t)mn * ld + kk + e];
-          }
-          v[i] = t;
-        }
+        c = (((pc >> 1) ^ ((r >> 1) & 3)) << 1) | (pc & 1);
+      } else if constexpr (R >= 128) {
+        c = (((pc >> 1) ^ ((r & 3) | (((r >> 3) & 1) << 2))) << 1) | (pc & 1);
       } else {
-        constexpr int CPR = R / 8;  // chunks per k-row
-        const int row = id / CPR, c = id % CPR;
-        kk = k0 + row;
-        mn = mn0 + c * 8;
-        if (kk < K && mn + 8 <= len) {
-          v[i] = *reinterpret_cast<const short8_t*>(X + (size_t)kk * ld + mn);
-        } else {
-          short8_t t = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (kk < K) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (mn + e < len) t[e] = (short)X[(size_t)kk * ld + mn + e];
-          }
-          v[i] = t;
-        }
+        c = (((pc >> 1) ^ (((r >> 1) & 1) | (((r >> 3) & 1) << 1))) << 1) | (pc & 1);
       }
+      row[i] = r;
+      col[i] = c * 8;
     }
   }
-
-  __device__ __forceinline__ void store(char* lds, int tid) const {
+  // Issue the tile at (mn0, k0). len = M or N; kend = K bound; ld elements.
+  __device__ __forceinline__ void issue(const bf16_t* __restrict__ X, int ld, int len, int kend,
+                                        int mn0, int k0, char* lds, int wid) const {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int id = tid + i * NT;
-      int row, byte;
+    for (int i = 0; i < P; ++i) {
+      long long off;
       if constexpr (KC) {
-        row = id >> 3;
-        byte = (id & 7) * 16;
+        int mn = mn0 + row[i];
+        mn = mn < len ? mn : len - 1;
+        int k = k0 + col[i];
+        k = k < kend ? k : 0;  // fully past K: any valid chunk (zeroed later)
+        off = (long long)mn * ld + k;
       } else {
-        constexpr int CPR = R / 8;
-        row = id / CPR;
-        byte = (id % CPR) * 16;
+        int k = k0 + row[i];
+        k = k < kend ? k : kend - 1;  // zeroed later
+        int mn = mn0 + col[i];
+        mn = mn < len ? mn : 0;  // fully past len: never stored
+        off = (long long)k * ld + mn;
       }
-      *reinterpret_cast<short8_t*>(lds + lds_off<KC, R>(row, byte)) = v[i];
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(X + off),
+          (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, 0, 0);
+    }
+  }
+  // Zero the k >= kend part of the tile image at k0 (last, partial tile).
+  __device__ __forceinline__ static void zero_ktail(char* lds, int k0, int kend, int tid, int nt) {
+    if constexpr (KC) {
+      for (int id = tid; id < R * 8; id += nt) {
+        const int r = id >> 3, c = id & 7;
+        const int kk = k0 + c * 8;
+        if (kk + 8 <= kend) continue;
+        short8_t* p = reinterpret_cast<short8_t*>(lds + lds_off<KC, R>(r, c * 16));
+        short8_t v = *p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (kk + e >= kend) v[e] = 0;
+        *p = v;
+      }
+    } else {
+      for (int id = tid; id < BK * (R / 8); id += nt) {
+        const int r = id / (R / 8), c = id % (R / 8);
+        if (k0 + r < kend) continue;
+        *reinterpret_cast<short8_t*>(lds + lds_off<KC, R>(r, c * 16)) =
+            short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
   }
 };
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Workgroup barrier that does NOT drain in-flight LDS-DMA (no vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // MFMA operand fragment for 16 rows/cols starting at `base` within the tile,
 // k-step s (32 deep). Lane l holds X(base + (l&15), 32s + 8(l>>4) + j), j<8.
@@ -140,34 +170,54 @@ __device__ __forceinline__ short8_t frag(const char* lds, int base, int s, int l
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+template <int BM, int BN, int WM, int WN, int STAGES, bool A_KC, bool B_KC, int EPI,
+          bool OUT_F32>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
     const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
     int ldb, int ldc, int ldaux, float alpha, float beta, int k_per_split, long long split_stride) {
-  constexpr int NT = WM * WN * 64;
+  constexpr int NW = WM * WN;
+  constexpr int NT = NW * 64;
   constexpr int TM = BM / WM / 16;  // 16x16 subtiles per wave along M
   constexpr int TN = BN / WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int SB = A_BYTES + B_BYTES;  // bytes per pipeline stage
+  using GA = Glds<A_KC, BM, NW>;
+  using GB = Glds<B_KC, BN, NW>;
+  constexpr int PT = GA::P + GB::P;  // LDS-DMA instructions per wave per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
   const int nwg = tiles_m * tiles_n;
+  // XCD-aware raster: xcd_remap gives each XCD a contiguous run of tile ids;
+  // the run walks the SHORT output dimension fastest, so each XCD owns a band
+  // of the larger operand (read from HBM once chip-wide) and re-reads only the
+  // smaller one (L2-resident). Walking the long dimension fastest instead made
+  // every XCD stream the whole large operand.
   const int t = xcd_remap(blockIdx.x, nwg);
-  const int tm = t % tiles_m, tn = t / tiles_m;
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // split-K range
   const int kb = blockIdx.z * k_per_split;
   const int ke = min(K, kb + k_per_split);
   const int nk = cdiv(ke - kb, BK);
+  const bool ktail = ((ke - kb) % BK) != 0;
 
-  constexpr int BUF = A_BYTES + B_BYTES;  // one stage = A tile then B tile
-
-  Stage<A_KC, BM, NT> sa;
-  Stage<B_KC, BN, NT> sb;
+  GA ga;
+  GB gb;
+  ga.init(wid, lane);
+  gb.init(wid, lane);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -175,23 +225,37 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    sa.load(A, lda, M, ke, m0, kb, tid);
-    sb.load(B, ldb, N, ke, n0, kb, tid);
-    sa.store(smem, tid);
-    sb.store(smem + A_BYTES, tid);
-    __syncthreads();
+  // prologue: STAGES-1 tiles in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      ga.issue(A, lda, M, ke, m0, kb + s * BK, smem + s * SB, wid);
+      gb.issue(B, ldb, N, ke, n0, kb + s * BK, smem + s * SB + A_BYTES, wid);
+    }
   }
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(A, lda, M, ke, m0, kb + (kt + 1) * BK, tid);
-      sb.load(B, ldb, N, ke, n0, kb + (kt + 1) * BK, tid);
+    // tile kt landed (this wave's DMA), then everyone's (barrier)
+    if (kt + STAGES - 2 < nk)
+      wait_vmcnt<(STAGES - 2) * PT>();
+    else
+      wait_vmcnt<0>();
+    lds_barrier();
+    char* st = smem + (kt % STAGES) * SB;
+    if (ktail && kt == nk - 1) {
+      GA::zero_ktail(st, kb + kt * BK, ke, tid, NT);
+      GB::zero_ktail(st + A_BYTES, kb + kt * BK, ke, tid, NT);
+      lds_barrier();
     }
-    const char* la = smem + cur * BUF;
-    const char* lb = la + A_BYTES;
+    // refill the slot consumed in iteration kt-1
+    const int nt_ = kt + STAGES - 1;
+    if (nt_ < nk) {
+      char* ns = smem + (nt_ % STAGES) * SB;
+      ga.issue(A, lda, M, ke, m0, kb + nt_ * BK, ns, wid);
+      gb.issue(B, ldb, N, ke, n0, kb + nt_ * BK, ns + A_BYTES, wid);
+    }
+    const char* la = st;
+    const char* lb = st + A_BYTES;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       short8_t af[TM], bfr[TN];
@@ -204,60 +268,96 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (more) {
-      sa.store(smem + (cur ^ 1) * BUF, tid);
-      sb.store(smem + (cur ^ 1) * BUF + A_BYTES, tid);
-    }
-    __syncthreads();
   }
 
-  // ---------------- epilogue: C/D layout col = lane&15, row = 4*(lane>>4) + r
+  // ---------------- epilogue (LDS-staged, 16-byte coalesced stores)
+  // 1) every lane writes its accumulators (alpha, bias, relu applied; C/D
+  //    layout col = lane&15, row = 4*(lane>>4) + r) into a row-major LDS image
+  //    of the wave's sub-tile; 2) the wave reads the image back as 16-byte row
+  //    chunks, applies the elementwise epilogue that needs a second operand
+  //    (ReLU-mask aux, beta*C) with vector loads, and stores 16 bytes per lane.
+  // Split-K partial products take the same path into the f32 slab of split z.
+  using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int ES = sizeof(OutT);
+  constexpr int SROW = WTN * ES + 16;          // padded LDS row (bytes)
+  constexpr int EPC = 16 / ES;                  // elements per 16-byte chunk
+  constexpr int CPR = WTN / EPC;                // chunks per sub-tile row
+  const bool split = gridDim.z > 1;
+  OutT* C = reinterpret_cast<OutT*>(Cv) + (split ? (size_t)blockIdx.z * split_stride : 0);
+  const float a_ = split ? 1.f : alpha;
+  const float b_ = split ? 0.f : beta;
+  lds_barrier();  // all waves done with the pipeline stages
+  char* wimg = smem + wid * (WTM * SROW);
   const int g = lane >> 4, cl = lane & 15;
-  if (gridDim.z > 1) {
-    // split-K partial: raw f32 slab, epilogue applied by the reduce kernel
-    float* C = reinterpret_cast<float*>(Cv) + (size_t)blockIdx.z * split_stride;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * (BN / WN) + 16 * j + cl;
-        if (n >= N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * (BM / WM) + 16 * i + 4 * g + r;
-          if (m < M) C[(size_t)m * ldc + n] = acc[i][j][r];
-        }
-      }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (BN / WN) + 16 * j + cl;
-    if (n >= N) continue;
+    const int n = n0 + wn * WTN + 16 * j + cl;
     float bn = 0.f;
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bn = bias[n];
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+      if (!split) bn = bias[n < N ? n : N - 1];
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + 16 * i + 4 * g + r;
-        if (m >= M) continue;
-        float v = alpha * acc[i][j][r];
+        float v = a_ * acc[i][j][r];
         if constexpr (EPI == EPI_BIAS) v += bn;
-        if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v + bn, 0.f);
+        if constexpr (EPI == EPI_BIAS_RELU) {
+          if (!split) v = fmaxf(v + bn, 0.f);
+        }
+        OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW +
+                                            (16 * j + cl) * ES);
+        if constexpr (OUT_F32) *dst = v;
+        else *dst = f2bf(v);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local image complete
+  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                      (EPI != EPI_DRELU ||
+                       ((ldaux % 8) == 0 && (reinterpret_cast<uintptr_t>(aux) & 15) == 0));
+#pragma unroll
+  for (int t = 0; t < (WTM * CPR) / 64; ++t) {
+    const int id = lane + 64 * t;
+    const int row = id / CPR, ch = id % CPR;
+    const int m = m0 + wm * WTM + row;
+    const int n = n0 + wn * WTN + ch * EPC;
+    if (m >= M || n >= N) continue;
+    OutT vals[EPC];
+    *reinterpret_cast<int4*>(vals) =
+        *reinterpret_cast<const int4*>(wimg + row * SROW + ch * 16);
+    OutT* cp = C + (size_t)m * ldc + n;
+    if (vec_ok && n + EPC <= N) {
+      if constexpr (EPI == EPI_DRELU) {
+        const short8_t x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e)
+          if (!(bf2f((bf16_t)x[e * (8 / EPC)]) > 0.f)) vals[e] = OutT(0);
+      }
+      if (b_ != 0.f) {
+        OutT old[EPC];
+        *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          if constexpr (OUT_F32) vals[e] += b_ * old[e];
+          else vals[e] = f2bf(bf2f(vals[e]) + b_ * bf2f(old[e]));
+        }
+      }
+      *reinterpret_cast<int4*>(cp) = *reinterpret_cast<const int4*>(vals);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        if (n + e >= N) break;
+        OutT v = vals[e];
         if constexpr (EPI == EPI_DRELU) {
-          if (!(bf2f(aux[(size_t)m * ldaux + n]) > 0.f)) v = 0.f;
+          if (!(bf2f(aux[(size_t)m * ldaux + n + e]) > 0.f)) v = OutT(0);
         }
-        const size_t o = (size_t)m * ldc + n;
-        if constexpr (OUT_F32) {
-          float* C = reinterpret_cast<float*>(Cv);
-          if (beta != 0.f) v += beta * C[o];
-          C[o] = v;
-        } else {
-          bf16_t* C = reinterpret_cast<bf16_t*>(Cv);
-          if (beta != 0.f) v += beta * bf2f(C[o]);
-          C[o] = f2bf(v);
+        if (b_ != 0.f) {
+          if constexpr (OUT_F32) v += b_ * cp[e];
+          else v = f2bf(bf2f(v) + b_ * bf2f(cp[e]));
         }
+        cp[e] = v;
       }
     }
   }
@@ -295,39 +395,44 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, void* __restr
 }
 
 // Column sum of a bf16 [M, N] matrix (row stride ld) into f32 out[N]
-// (out = beta*out + sum): the bias gradient. Two-stage, deterministic.
-// Stage 1: block (bx, by) sums rows [by*RB, ..) for 64*8 columns.
-__global__ void colsum_partial_kernel(const bf16_t* __restrict__ X, float* __restrict__ part,
-                                      int M, int N, int ld, int rows_per_block) {
-  // 256 threads: 64 column-groups of 8 columns? keep simple: each thread owns 2 columns
-  const int col = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+// (out = beta*out + sum): the bias gradient. Deterministic two-stage:
+// block (bx, by) sums columns [64bx, 64bx+64) over rows [by*RB, by*RB+RB)
+// with 16-byte loads (8 columns per thread, 32 row lanes), then
+// reduce_partials folds the row chunks.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ X,
+                                                             float* __restrict__ part, int M, int N,
+                                                             int ld, int rows_per_block) {
+  __shared__ float red[32][65];
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int col0 = blockIdx.x * 64 + cg * 8;
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
-  if (col >= N) return;
-  float s0 = 0.f, s1 = 0.f;
-  if (col + 1 < N && (ld % 2) == 0) {
-    for (int r = r0; r < r1; ++r) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(X + (size_t)r * ld + col);
-      s0 += bf2f((bf16_t)(w & 0xffff));
-      s1 += bf2f((bf16_t)(w >> 16));
-    }
-  } else {
-    for (int r = r0; r < r1; ++r) {
-      s0 += bf2f(X[(size_t)r * ld + col]);
-      if (col + 1 < N) s1 += bf2f(X[(size_t)r * ld + col + 1]);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  const bool vec = (col0 + 8 <= N) && (ld % 8 == 0);
+  for (int r = r0 + rl; r < r1; r += 32) {
+    const bf16_t* p = X + (size_t)r * ld + col0;
+    if (vec) {
+      const short8_t v = *reinterpret_cast<const short8_t*>(p);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (col0 + i < N) acc[i] += bf2f(p[i]);
     }
   }
-  part[(size_t)blockIdx.y * N + col] = s0;
-  if (col + 1 < N) part[(size_t)blockIdx.y * N + col + 1] = s1;
-}
-
-__global__ void colsum_final_kernel(const float* __restrict__ part, float* __restrict__ out, int N,
-                                    int nparts, float beta) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * N + n];
-  out[n] = (beta != 0.f ? beta * out[n] : 0.f) + s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rl][cg * 8 + i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) s += red[k][threadIdx.x];
+    const int col = blockIdx.x * 64 + threadIdx.x;
+    if (col < N) part[(size_t)blockIdx.y * N + col] = s;
+  }
 }
 
 }  // namespace tdg
@@ -337,21 +442,31 @@ using namespace tdg;
 
 namespace {
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKc, int EPI, bool F32>
+template <int BM, int BN, int WM, int WN, int ST, bool AK, bool BKc, int EPI, bool F32>
 void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, const bf16_t* aux,
                 int M, int N, int K, int lda, int ldb, int ldc, int ldaux, float alpha, float beta,
                 int splits, float* ws, hipStream_t st) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int lds = 2 * (BM + BN) * BK * 2;
+  const int img = WM * (BM / WM) * ((BN / WN) * (F32 ? 4 : 2) + 16) * WN;
+  const int img32 = WM * (BM / WM) * ((BN / WN) * 4 + 16) * WN;  // split-K slab staging
+  const int lds = std::max(ST * (BM + BN) * BK * 2, std::max(img, splits > 1 ? img32 : 0));
+  static bool attr_set = false;  // >64 KiB dynamic LDS needs the opt-in
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI_NONE, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
   if (splits <= 1) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AK, BKc, EPI, F32>), dim3(tiles, 1, 1),
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>), dim3(tiles, 1, 1),
                        dim3(WM * WN * 64), lds, st, A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
                        ldaux, alpha, beta, K, 0LL);
   } else {
     int kps = cdiv(cdiv(K, splits), BK) * BK;
     splits = cdiv(K, kps);
     const long long stride = (long long)M * ldc;
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AK, BKc, EPI_NONE, true>),
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI_NONE, true>),
                        dim3(tiles, 1, splits), dim3(WM * WN * 64), lds, st, A, B, (void*)ws, bias,
                        aux, M, N, K, lda, ldb, ldc, ldaux, 1.f, 0.f, kps, stride);
     const long long total = (long long)M * N;
@@ -365,24 +480,30 @@ template <bool AK, bool BKc, int EPI, bool F32>
 void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const float* bias,
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st) {
+#define TDG_CFG(ID, BM_, BN_, WM_, WN_, ST_)                                                  \
+  case ID:                                                                                    \
+    launch_cfg<BM_, BN_, WM_, WN_, ST_, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, \
+                                                          ldc, ldaux, alpha, beta, splits, ws,   \
+                                                          st);                                   \
+    break;
+  // Tile table (BM, BN, waves M x N, pipeline stages). LDS = ST*(BM+BN)*128 B;
+  // the table keeps >= 2 waves per SIMD resident (1 is latency-bound).
   switch (tile_cfg) {
-    case 0:
-      launch_cfg<128, 128, 2, 2, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                    ldaux, alpha, beta, splits, ws, st);
-      break;
-    case 1:
-      launch_cfg<128, 64, 2, 2, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                   ldaux, alpha, beta, splits, ws, st);
-      break;
-    case 2:
-      launch_cfg<64, 128, 2, 2, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                   ldaux, alpha, beta, splits, ws, st);
-      break;
+    TDG_CFG(0, 128, 128, 2, 2, 2)
+    TDG_CFG(1, 128, 64, 2, 2, 3)
+    TDG_CFG(2, 64, 128, 2, 2, 3)
+    TDG_CFG(3, 64, 64, 2, 2, 4)
+    TDG_CFG(4, 128, 128, 2, 4, 3)
+    TDG_CFG(5, 256, 128, 4, 2, 2)
+    TDG_CFG(6, 128, 256, 2, 4, 2)
+    TDG_CFG(7, 64, 128, 2, 2, 2)
+    TDG_CFG(9, 256, 128, 4, 2, 3)
+    TDG_CFG(10, 128, 256, 2, 4, 3)
+    TDG_CFG(11, 128, 128, 2, 2, 4)
     default:
-      launch_cfg<64, 64, 2, 2, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                  ldaux, alpha, beta, splits, ws, st);
-      break;
+      TDG_CFG(8, 64, 64, 2, 2, 2)
   }
+#undef TDG_CFG
 }
 
 template <bool AK, bool BKc>
@@ -432,9 +553,8 @@ extern "C" int tdg_gemm(const void* A, const void* B, void* C, const float* bias
 extern "C" void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld,
                            int rows_per_block, float beta, hipStream_t st) {
   const int nparts = cdiv(M, rows_per_block);
-  dim3 grid(cdiv(cdiv(N, 2), 256), nparts);
+  dim3 grid(cdiv(N, 64), nparts);
   hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(256), 0, st, (const bf16_t*)X, part, M, N,
                      ld, rows_per_block);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 256)), dim3(256), 0, st, part, out, N,
-                     nparts, beta);
+  launch_reduce_partials(part, out, N, nparts, beta, st);
 }

@@ -12,6 +12,7 @@
 // 219-248). One wave per row; each lane owns D/64 contiguous elements
 // (vectorised 4..32-byte accesses), so D in {128, 256, 512, 1024}.
 #include "tdg_common.h"
+#include "tdg_reduce.h"
 
 namespace tdg {
 
@@ -217,16 +218,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[col] (+)= sum_p part[p, col] for up to 3 partial arrays.
-__global__ void colpart_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                      int D, int nparts, int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= D) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * D + col];
-  out[col] = accumulate ? out[col] + s : s;
-}
-
 }  // namespace tdg
 
 using namespace tdg;
@@ -247,7 +238,7 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
               int accumulate, hipStream_t st) {
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
-  const int rpb = 64;
+  const int rpb = 32;
   const int nb = cdiv(M, rpb);
   float* pg = ws;
   float* pb = ws + (size_t)nb * D;
@@ -255,13 +246,10 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
   hipLaunchKernelGGL(ln_bwd_kernel<D>, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                      (const bf16_t*)dres, pg, pb, ps, M, rpb, p, thresh, seed, ctr, site);
-  hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, pg, dgamma, D,
-                     nb, accumulate);
-  hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, pb, dbeta, D,
-                     nb, accumulate);
-  if (dbias)
-    hipLaunchKernelGGL(colpart_reduce_kernel, dim3(cdiv(D, 256)), dim3(256), 0, st, ps, dbias, D,
-                       nb, accumulate);
+  const float beta = accumulate ? 1.f : 0.f;
+  launch_reduce_partials(pg, dgamma, D, nb, beta, st);
+  launch_reduce_partials(pb, dbeta, D, nb, beta, st);
+  if (dbias) launch_reduce_partials(ps, dbias, D, nb, beta, st);
 }
 }  // namespace
 
@@ -277,7 +265,7 @@ extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, cons
   }
 }
 
-// ws must hold 3 * ceil(M/64) * D floats.
+// ws must hold 3 * ceil(M/32) * D floats.
 extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                           const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,

@@ -37,7 +37,8 @@ def reset_workspace() -> None:
 
 # ------------------------------------------------------------------ GEMM
 # tile configs (see csrc/kernels/gemm.hip): 0=128x128, 1=128x64, 2=64x128, 3=64x64
-_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128), 5: (256, 128),
+          6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (256, 128), 10: (128, 256), 11: (128, 128)}
 _CFG_OVERRIDE: Dict[Tuple[int, int, int, bool, bool], Tuple[int, int]] = {}
 
 
@@ -46,40 +47,81 @@ def set_gemm_config(M: int, N: int, K: int, a_kc: bool, b_kc: bool, cfg: int, sp
 
 
 def choose_gemm(M: int, N: int, K: int, a_kc: bool = True, b_kc: bool = True) -> Tuple[int, int]:
-    """Pick (tile config, split-K). Aim for >= 2 workgroups per CU so the
-    256 CUs (8 XCDs) are filled; split K when output tiles are too few
-    (weight-gradient GEMMs: small output, K = tokens)."""
+    """Heuristic (tile config, split-K) when no autotuned entry exists.
+    Measured on MI355X (scripts/bench_gemm.py, profiles/gemm_bench.txt): the
+    64x128 / 64x64 4-wave tiles win on these skinny training shapes; weight
+    gradients (K = tokens, small output) need split-K to fill 256 CUs."""
     o = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
     if o is not None:
         return o
-    target = 2 * NUM_CU
-    for cfg in (0, 1, 2, 3):
-        bm, bn = _TILES[cfg]
-        if cfg == 1 and M < N:
+    if not a_kc and not b_kc:  # weight gradient: split K (= tokens)
+        t64 = math.ceil(M / 64) * math.ceil(N / 64)
+        splits = 1
+        while t64 * splits < 2 * NUM_CU and K // (splits * 2) >= 512:
+            splits *= 2
+        return 8, splits
+    if math.ceil(M / 64) * math.ceil(N / 128) >= NUM_CU:
+        return 7, 1
+    return 8, 1
+
+
+_TUNED: Dict[tuple, Tuple[int, int]] = {}
+AUTOTUNE = True
+_CANDIDATES = [(0, 1), (2, 1), (7, 1), (8, 1), (4, 1), (10, 1)]
+
+
+def _autotune(key, run) -> Tuple[int, int]:
+    """Time the candidate tile configs once for this problem (3 reps each, HIP
+    events on the current stream) and keep the fastest."""
+    M, N, K, a_kc, b_kc = key[:5]
+    cands = list(_CANDIDATES)
+    if not a_kc and not b_kc:
+        cands = [(c, s) for c in (0, 7, 8) for s in (1, 2, 4, 8) if K // s >= 256]
+    best = None
+    for cfg in cands:
+        try:
+            run(cfg)  # warm-up (also surfaces unsupported configs)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(3):
+                run(cfg)
+            ev[1].record()
+            ev[1].synchronize()
+            t = ev[0].elapsed_time(ev[1])
+        except RuntimeError:
             continue
-        if cfg == 2 and N < M:
-            continue
-        tiles = math.ceil(M / bm) * math.ceil(N / bn)
-        if tiles >= target:
-            return cfg, 1
-    bm, bn = _TILES[3]
-    tiles = math.ceil(M / bm) * math.ceil(N / bn)
-    splits = 1
-    if tiles < NUM_CU and K >= 1024:
-        splits = min(max(1, target // tiles), K // 256)
-        splits = max(1, splits)
-    return 3, splits
+        if best is None or t < best[1]:
+            best = (cfg, t)
+    return best[0]
 
 
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
          ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    tile, splits = cfg if cfg is not None else choose_gemm(M, N, K, a_kc, b_kc)
-    ws = None
-    if splits > 1:
-        ws = workspace("splitk", splits * M * ldc, A.device)
-    C().gemm(A, B, Cout, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha, beta,
-             tile, splits, ws)
+    def run(c):
+        tile, splits = c
+        ws = workspace("splitk", splits * M * ldc, A.device) if splits > 1 else None
+        C().gemm(A, B, Cout, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha,
+                 beta, tile, splits, ws)
+
+    if cfg is None:
+        key = (M, N, K, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0)
+        cfg = _TUNED.get(key)
+        if cfg is None:
+            cfg = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
+        if cfg is None:
+            if (AUTOTUNE and beta == 0.0 and A.is_cuda
+                    and not torch.cuda.is_current_stream_capturing()):
+                cfg = _autotune(key, run)
+                _TUNED[key] = cfg
+            else:
+                cfg = choose_gemm(M, N, K, a_kc, b_kc)
+    run(cfg)
     return Cout
+
+
+def tuned_table() -> Dict[str, str]:
+    return {f"{k[0]}x{k[1]}x{k[2]} a_kc={k[3]} b_kc={k[4]} epi={k[5]}": f"cfg{v[0]} split{v[1]}"
+            for k, v in _TUNED.items()}
 
 
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
@@ -164,7 +206,7 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
     dh = torch.empty_like(dy)
     need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
     ds = torch.empty_like(dy) if need_ds else None
-    ws = workspace("ln_bwd", 3 * math.ceil(M / 64) * D, dy.device)
+    ws = workspace("ln_bwd", 3 * math.ceil(M / 32) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
                accumulate)
     if ds is None:

@@ -5,7 +5,7 @@ import math
 import pytest
 import torch
 
-from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk
 from tensorflow_distributed_on_gke_amd.ops import philox
 
 pytestmark = pytest.mark.gpu
@@ -39,7 +39,7 @@ def test_gemm_forward_bias_relu(M, N, K, cfg):
     b = _rand(N, seed=3)
     ref = torch.relu(x.float() @ w.float().t() + b)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    K.gemm(x.to(DEV), w.to(DEV), out, M, N, K, K, K, N, True, True, K.EPI_BIAS_RELU,
+    kk.gemm(x.to(DEV), w.to(DEV), out, M, N, K, K, K, N, True, True, kk.EPI_BIAS_RELU,
            bias=b.to(DEV), cfg=(cfg, 1))
     _close(out, ref, 1e-2, "gemm fwd")
 
@@ -50,7 +50,7 @@ def test_gemm_identity_asymmetric():
     a = torch.eye(n, dtype=torch.bfloat16)
     bmat = _bf(torch.arange(n * n, dtype=torch.float32).view(n, n) % 251)
     out = torch.empty(n, n, dtype=torch.float32, device=DEV)
-    K.gemm(a.to(DEV), bmat.to(DEV), out, n, n, n, n, n, n, True, True, K.EPI_NONE, cfg=(0, 1))
+    kk.gemm(a.to(DEV), bmat.to(DEV), out, n, n, n, n, n, n, True, True, kk.EPI_NONE, cfg=(0, 1))
     torch.testing.assert_close(out.cpu(), bmat.float().t())
 
 
@@ -62,7 +62,7 @@ def test_gemm_dgrad_drelu(M, N, K, cfg):
     h = _bf(_rand(M, K, seed=6))
     ref = (dy.float() @ w.float()) * (h.float() > 0)
     out = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
-    K.gemm(dy.to(DEV), w.to(DEV), out, M, K, N, N, K, K, True, False, K.EPI_DRELU, aux=h.to(DEV),
+    kk.gemm(dy.to(DEV), w.to(DEV), out, M, K, N, N, K, K, True, False, kk.EPI_DRELU, aux=h.to(DEV),
            ldaux=K, cfg=(cfg, 1))
     _close(out, ref, 1e-2, "gemm dgrad")
 
@@ -92,18 +92,18 @@ def test_linear_wrappers_padded_vocab():
     x = _bf(_rand(M, d, seed=9)).to(DEV)
     w = _bf(_rand(V, d, scale=0.3, seed=10)).to(DEV)
     b = _rand(V, seed=11).to(DEV)
-    lg = K.linear_fwd(x, w, b, ldc=Vp)
+    lg = kk.linear_fwd(x, w, b, ldc=Vp)
     ref = x.float() @ w.float().t() + b
     _close(lg[:, :V], ref, 1e-2, "vocab fwd")
     dl = _bf(_rand(M, Vp, seed=12)).to(DEV)
     dl[:, V:] = 0
-    dx = K.linear_dgrad(dl, w, V)
+    dx = kk.linear_dgrad(dl, w, V)
     _close(dx, dl[:, :V].float() @ w.float(), 1e-2, "vocab dgrad")
     dw = torch.empty(V, d, dtype=torch.float32, device=DEV)
-    K.linear_wgrad(dl, x, V, dw)
+    kk.linear_wgrad(dl, x, V, dw)
     _close(dw, dl[:, :V].float().t() @ x.float(), 2e-3, "vocab wgrad")
     db = torch.empty(V, dtype=torch.float32, device=DEV)
-    K.colsum(dl, V, db)
+    kk.colsum(dl, V, db)
     _close(db, dl[:, :V].float().sum(0), 1e-3, "colsum")
 
 
@@ -138,14 +138,14 @@ def test_attention_fwd_bwd(hd, causal, Lq, Lk):
     scale = 1 / math.sqrt(hd)
     qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
     ref, _ = _ref_attn(qr, kr, vr, kv_len, causal, scale)
-    out, lse = K.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), kv_len.to(DEV), scale, causal)
+    out, lse = kk.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), kv_len.to(DEV), scale, causal)
     _close(out, ref.detach(), 2e-2, "attn fwd")
     dout = _bf(torch.randn(B, Lq, H, hd))
     ref.backward(dout.float())
     dq = torch.empty_like(q, device=DEV)
     dk = torch.empty_like(k, device=DEV)
     dv = torch.empty_like(v, device=DEV)
-    K.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), out, dout.to(DEV), lse, dq, dk, dv, kv_len.to(DEV),
+    kk.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), out, dout.to(DEV), lse, dq, dk, dv, kv_len.to(DEV),
                scale, causal)
     _close(dv, vr.grad, 3e-2, "attn dv")
     _close(dk, kr.grad, 3e-2, "attn dk")
@@ -157,7 +157,7 @@ def test_attention_strided_fused_qkv():
     B, L, H, hd = 2, 96, 8, 64
     qkv = _bf(torch.randn(B, L, 3, H, hd)).to(DEV)
     kv_len = torch.tensor([96, 50], dtype=torch.int32, device=DEV)
-    out, _ = K.attn_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], kv_len, 0.125, True)
+    out, _ = kk.attn_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], kv_len, 0.125, True)
     c = qkv.cpu()
     ref, _ = _ref_attn(c[:, :, 0], c[:, :, 1], c[:, :, 2], kv_len.cpu(), True, 0.125)
     _close(out, ref, 2e-2, "strided attn")
@@ -168,7 +168,7 @@ def test_attention_probs():
     q = _bf(torch.randn(B, Lq, H, hd))
     k = _bf(torch.randn(B, Lk, H, hd))
     kv_len = torch.tensor([17, 9], dtype=torch.int32)
-    pr = K.attn_probs(q.to(DEV), k.to(DEV), kv_len.to(DEV), 0.125, False)
+    pr = kk.attn_probs(q.to(DEV), k.to(DEV), kv_len.to(DEV), 0.125, False)
     _, ref = _ref_attn(q, k, k, kv_len, False, 0.125)
     _close(pr, ref, 1e-3, "probs")
 
@@ -184,7 +184,7 @@ def test_add_ln_fwd_bwd(D, p):
     s = _bf(torch.randn(M, D))
     gamma = torch.rand(D) + 0.5
     beta = torch.randn(D)
-    y, h, mean, rstd = K.ln_fwd(x.to(DEV), s.to(DEV), gamma.to(DEV), beta.to(DEV), p, seed,
+    y, h, mean, rstd = kk.ln_fwd(x.to(DEV), s.to(DEV), gamma.to(DEV), beta.to(DEV), p, seed,
                                 ctr.to(DEV), site)
     keep = philox.keep_mask(seed, philox.rng_offset(5, site), M * D, p).view(M, D).float() if p > 0 else torch.ones(M, D)
     ks = keep / (1 - p)
@@ -200,7 +200,7 @@ def test_add_ln_fwd_bwd(D, p):
     dg = torch.empty(D, device=DEV)
     db = torch.empty(D, device=DEV)
     dbias = torch.empty(D, device=DEV)
-    dh, ds = K.ln_bwd(dy.to(DEV), h, mean, rstd, gamma.to(DEV), dg, db, dbias, p, seed, ctr.to(DEV), site)
+    dh, ds = kk.ln_bwd(dy.to(DEV), h, mean, rstd, gamma.to(DEV), dg, db, dbias, p, seed, ctr.to(DEV), site)
     _close(dh, xr.grad, 3e-2, "ln dh")
     _close(ds, sr.grad, 3e-2, "ln ds")
     _close(dg, gr.grad, 2e-2, "ln dgamma")
@@ -217,14 +217,14 @@ def test_embed_fwd_bwd(p):
     table = _bf(torch.randn(V, D) * 0.05)
     pe = positional_encoding(64, D)
     ctr = torch.tensor([3], dtype=torch.int64)
-    out = K.embed_fwd(tok.to(DEV), table.to(DEV), pe.to(DEV), math.sqrt(D), p, 77, ctr.to(DEV), 2)
+    out = kk.embed_fwd(tok.to(DEV), table.to(DEV), pe.to(DEV), math.sqrt(D), p, 77, ctr.to(DEV), 2)
     ks = (philox.keep_mask(77, philox.rng_offset(3, 2), B * L * D, p).view(B, L, D).float() / (1 - p)
           if p > 0 else torch.ones(B, L, D))
     ref = (table.float()[tok] * math.sqrt(D) + pe[:L]) * ks
     _close(out, ref, 1e-2, "embed fwd")
     dout = _bf(torch.randn(B, L, D))
     dt = torch.zeros(V, D, device=DEV)
-    K.embed_bwd(tok.to(DEV), dout.to(DEV), dt, math.sqrt(D), p, 77, ctr.to(DEV), 2)
+    kk.embed_bwd(tok.to(DEV), dout.to(DEV), dt, math.sqrt(D), p, 77, ctr.to(DEV), 2)
     refg = torch.zeros(V, D).index_add_(0, tok.view(-1), (dout.float() * ks * math.sqrt(D)).view(-1, D))
     _close(dt, refg, 1e-4, "embed bwd")
 
@@ -238,13 +238,13 @@ def test_xent(smoothing):
     lab[::7] = 0
     ntok = torch.zeros(1, device=DEV)
     lgd = lg.clone().to(DEV)
-    K.count_tokens(lab.to(DEV), ntok)
+    kk.count_tokens(lab.to(DEV), ntok)
     rl = torch.empty(M, device=DEV)
     rc = torch.empty(M, device=DEV)
-    K.xent(lgd, V, lab.to(DEV), ntok, 2.0, smoothing, rl, rc, True)
+    kk.xent(lgd, V, lab.to(DEV), ntok, 2.0, smoothing, rl, rc, True)
     so = torch.empty(2, device=DEV)
     acc = torch.zeros(4, device=DEV)
-    K.xent_stats(rl, rc, ntok, 2.0, so, acc)
+    kk.xent_stats(rl, rc, ntok, 2.0, so, acc)
     x = lg.float()[:, :V].requires_grad_()
     mask = (lab != 0).float()
     n = mask.sum()
@@ -272,7 +272,7 @@ def test_adam_keras_semantics():
     pd, gd, md, vd = (t.clone().to(DEV) for t in (p, g, m, v))
     sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
     step = torch.tensor([10], dtype=torch.int64, device=DEV)
-    K.adam(pd, gd, md, vd, sh, step, 0.9, 0.98, 1e-9, 0.0, 128.0, 4000.0)
+    kk.adam(pd, gd, md, vd, sh, step, 0.9, 0.98, 1e-9, 0.0, 128.0, 4000.0)
     lr = 128 ** -0.5 * min(10 * 4000 ** -1.5, 10 ** -0.5)
     t = 11
     lr_t = lr * math.sqrt(1 - 0.98 ** t) / (1 - 0.9 ** t)
