@@ -27,6 +27,31 @@ static __global__ __launch_bounds__(256) void reduce_partials_kernel(const float
   }
 }
 
+// Up to 3 independent (partials, out) reductions in one launch (blockIdx.y).
+struct ReduceSet {
+  const float* part[3];
+  float* out[3];
+};
+static __global__ __launch_bounds__(256) void reduce_partials3_kernel(ReduceSet rs, int N, int P,
+                                                                      float beta) {
+  __shared__ float red[4][64];
+  const float* part = rs.part[blockIdx.y];
+  float* out = rs.out[blockIdx.y];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (col < N) {
+#pragma unroll 8
+    for (int p = g; p < P; p += 4) s += part[(size_t)p * N + col];
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
+  }
+}
+
 static inline void launch_reduce_partials(const float* part, float* out, int N, int P, float beta,
                                    hipStream_t st) {
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(cdiv(N, 64)), dim3(256), 0, st, part, out, N, P,

@@ -225,49 +225,78 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: STAGES-1 tiles in flight
+  // Software pipeline. LDS: STAGES tiles in flight (LDS-DMA). Registers:
+  // MFMA fragments one 32-deep k-step ahead (fa0/fb0 = step 0, fa1/fb1 =
+  // step 1 of a 64-deep tile), so every ds_read is issued before the MFMAs
+  // that hide its latency, and the single barrier per tile sits between the
+  // two MFMA groups. The slot refilled after that barrier is the one of the
+  // tile whose fragments are already all in registers, so all STAGES slots
+  // hold live prefetches.
+  static_assert(BK == 64, "two 32-deep k-steps per tile");
+  const int abase = wm * (BM / WM), bbase = wn * (BN / WN);
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) {
+  for (int s = 0; s < STAGES; ++s) {
     if (s < nk) {
       ga.issue(A, lda, M, ke, m0, kb + s * BK, smem + s * SB, wid);
       gb.issue(B, ldb, N, ke, n0, kb + s * BK, smem + s * SB + A_BYTES, wid);
     }
   }
-
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's DMA), then everyone's (barrier)
-    if (kt + STAGES - 2 < nk)
-      wait_vmcnt<(STAGES - 2) * PT>();
+  short8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  if (nk > 0) {
+    if (nk >= STAGES)
+      wait_vmcnt<(STAGES - 1) * PT>();
     else
       wait_vmcnt<0>();
     lds_barrier();
-    char* st = smem + (kt % STAGES) * SB;
-    if (ktail && kt == nk - 1) {
-      GA::zero_ktail(st, kb + kt * BK, ke, tid, NT);
-      GB::zero_ktail(st + A_BYTES, kb + kt * BK, ke, tid, NT);
+    if (ktail && nk == 1) {
+      GA::zero_ktail(smem, kb, ke, tid, NT);
+      GB::zero_ktail(smem + A_BYTES, kb, ke, tid, NT);
       lds_barrier();
     }
-    // refill the slot consumed in iteration kt-1
-    const int nt_ = kt + STAGES - 1;
-    if (nt_ < nk) {
-      char* ns = smem + (nt_ % STAGES) * SB;
-      ga.issue(A, lda, M, ke, m0, kb + nt_ * BK, ns, wid);
-      gb.issue(B, ldb, N, ke, n0, kb + nt_ * BK, ns + A_BYTES, wid);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa0[i] = frag<A_KC, BM>(smem, abase + 16 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb0[j] = frag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, 0, lane);
+  }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt % STAGES) * SB;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa1[i] = frag<A_KC, BM>(st, abase + 16 * i, 1, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb1[j] = frag<B_KC, BN>(st + A_BYTES, bbase + 16 * j, 1, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+    if (kt + 1 < nk) {
+      // tile kt+1 landed (this wave's DMA), then everyone's; everyone is done
+      // reading tile kt (its fragments are in registers)
+      if (kt + STAGES - 1 < nk)
+        wait_vmcnt<(STAGES - 2) * PT>();
+      else
+        wait_vmcnt<0>();
+      lds_barrier();
+      const char* nx = smem + ((kt + 1) % STAGES) * SB;
+      if (ktail && kt + 1 == nk - 1) {
+        GA::zero_ktail(const_cast<char*>(nx), kb + (kt + 1) * BK, ke, tid, NT);
+        GB::zero_ktail(const_cast<char*>(nx) + A_BYTES, kb + (kt + 1) * BK, ke, tid, NT);
+        lds_barrier();
+      }
+      if (kt + STAGES < nk) {
+        char* ns = smem + (kt % STAGES) * SB;
+        ga.issue(A, lda, M, ke, m0, kb + (kt + STAGES) * BK, ns, wid);
+        gb.issue(B, ldb, N, ke, n0, kb + (kt + STAGES) * BK, ns + A_BYTES, wid);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa0[i] = frag<A_KC, BM>(nx, abase + 16 * i, 0, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb0[j] = frag<B_KC, BN>(nx + A_BYTES, bbase + 16 * j, 0, lane);
     }
-    const char* la = st;
-    const char* lb = st + A_BYTES;
 #pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
-      short8_t af[TM], bfr[TN];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<A_KC, BM>(la, wm * (BM / WM) + 16 * i, s, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag<B_KC, BN>(lb, wn * (BN / WN) + 16 * j, s, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-    }
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
   }
 
   // ---------------- epilogue (LDS-staged, 16-byte coalesced stores)

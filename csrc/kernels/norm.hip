@@ -247,9 +247,9 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
                      (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                      (const bf16_t*)dres, pg, pb, ps, M, rpb, p, thresh, seed, ctr, site);
   const float beta = accumulate ? 1.f : 0.f;
-  launch_reduce_partials(pg, dgamma, D, nb, beta, st);
-  launch_reduce_partials(pb, dbeta, D, nb, beta, st);
-  if (dbias) launch_reduce_partials(ps, dbias, D, nb, beta, st);
+  ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
+  hipLaunchKernelGGL(reduce_partials3_kernel, dim3(cdiv(D, 64), dbias ? 3 : 2), dim3(256), 0, st,
+                     rs, D, nb, beta);
 }
 }  // namespace
 

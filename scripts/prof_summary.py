@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace --stats CSV directory: per-kernel total
-time, calls, average, and share of GPU time."""
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel time over the LAST
+N training steps only (steps delimited by the Adam kernel, so autotuning and
+warm-up dispatches are excluded), as ms per step."""
 import csv
 import glob
 import os
@@ -8,27 +9,30 @@ import sys
 from collections import defaultdict
 
 
-def main(d):
-    stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
-    if stats:
-        rows = list(csv.DictReader(open(stats[0])))
-        tot = sum(float(r["TotalDurationNs"]) for r in rows)
-        print(f"# {stats[0]}\n# total kernel time {tot/1e6:.3f} ms")
-        print(f"{'pct':>6} {'total_ms':>9} {'calls':>6} {'avg_us':>8}  kernel")
-        for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:45]:
-            t = float(r["TotalDurationNs"])
-            print(f"{100*t/tot:6.2f} {t/1e6:9.3f} {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:8.2f}  {r['Name'][:110]}")
-        return
+def main(d, nsteps=5):
     traces = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = list(csv.DictReader(open(traces[0])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    if len(ends) > nsteps:
+        lo, hi = ends[-nsteps - 1] + 1, ends[-1] + 1
+    else:
+        lo, hi = 0, len(rows)
+    sel = rows[lo:hi]
+    n = max(1, min(nsteps, len(ends) - 1))
     agg = defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(traces[0])):
-        n = r["Kernel_Name"]
-        agg[n][0] += 1
-        agg[n][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for r in sel:
+        name = r["Kernel_Name"]
+        agg[name][0] += 1
+        agg[name][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     tot = sum(v[1] for v in agg.values())
-    for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
-        print(f"{100*t/tot:6.2f} {t/1e6:9.3f} {c:6d} {t/c/1e3:8.2f}  {n[:110]}")
+    wall = int(sel[-1]["End_Timestamp"]) - int(sel[0]["Start_Timestamp"])
+    print(f"# {traces[0]}\n# last {n} steps: kernel busy {tot/1e6/n:.3f} ms/step, "
+          f"wall {wall/1e6/n:.3f} ms/step, {len(sel)//n} dispatches/step")
+    print(f"{'pct':>6} {'ms/step':>8} {'calls/st':>8} {'avg_us':>8}  kernel")
+    for name, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
+        print(f"{100*t/tot:6.2f} {t/1e6/n:8.3f} {c/n:8.1f} {t/c/1e3:8.2f}  {name[:100]}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 5)

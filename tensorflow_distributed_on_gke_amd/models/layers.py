@@ -1,20 +1,31 @@
-"""Fused layer-level autograd ops of the encoder-decoder Transformer.
+"""Fused block-level autograd ops of the encoder-decoder Transformer.
 
-Each op is a coarse `torch.autograd.Function` with a hand-written backward that
-sequences the gfx950 kernels (GEMM with fused epilogues, flash attention,
-fused dropout+residual+LayerNorm, fused embedding) and writes parameter
+Every post-LN sublayer of the reference is ONE `torch.autograd.Function` with a
+hand-written backward that sequences the gfx950 kernels and writes parameter
 gradients straight into the flat f32 gradient buffer, notifying the
-data-parallel engine as each one becomes final (so its bucket's all-reduce can
-start while backward continues).
+data-parallel engine as each becomes final (its bucket's all-reduce can start
+while backward continues):
+
+  SelfAttnBlockFn : y = LN(x + dropout(MHA(x, x, x)))          (encoder / decoder block 1)
+  CrossAttnBlockFn: y = LN(x + dropout(MHA(enc, enc, x)))      (decoder block 2)
+  FFNBlockFn      : y = LN(x + dropout(W2 relu(W1 x + b1) + b2))
+  CrossKVFn       : K|V projections of the encoder output for ALL decoder
+                    layers as one GEMM (N = layers*2*d)
+  EmbedFn         : dropout(emb[tok] * sqrt(d) + PE)
+
+Fusions this buys over per-op autograd: the residual gradient is added inside
+the dgrad GEMM epilogue (beta = 1 onto the LayerNorm input gradient) instead
+of an autograd add; the sublayer's output-bias gradient comes out of the
+LayerNorm backward's column reduction; ReLU backward is the dgrad epilogue of
+the second FFN GEMM; the encoder-output gradient of all cross attentions is
+produced by one dgrad GEMM.
 
 On CPU tensors the same ops run a plain-PyTorch f32 reference with identical
-semantics (including the Philox dropout masks): that is the CPU test path and
-the BASELINE "tiny on CPU" configuration; on GPU tensors only the HIP kernels
-run.
+semantics (including the Philox dropout masks): the CPU test path and the
+BASELINE "tiny on CPU" configuration. On GPU tensors only the HIP kernels run.
 
-Semantics follow the reference model
-(reference: distributed_training_transformer/transformer_model.py):
-  MultiHeadAttention :112-166  (separate Q/K/V Dense; here fused [3d,d] / [2d,d])
+Reference semantics (distributed_training_transformer/transformer_model.py):
+  MultiHeadAttention :112-166  (separate Q/K/V Dense; here fused [3d,d] / [L*2d,d])
   FFN                :169-175  (Dense(ff, relu) -> Dense(d))
   post-LN sublayer   :187-204, :219-248  (LN(x + dropout(sublayer(x))), eps 1e-6)
   embedding          :270-279, :301-308  (emb * sqrt(d) + PE, dropout)
@@ -22,7 +33,7 @@ Semantics follow the reference model
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
@@ -30,6 +41,8 @@ import torch
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.ops import philox
+
+LN_EPS = 1e-6
 
 
 @dataclass
@@ -48,12 +61,21 @@ class RunCtx:
         return self.dropout if self.training else 0.0
 
     def cpu_offset(self, site: int) -> int:
-        c = int(self.ctr.item()) if self.ctr is not None else 0
-        return philox.rng_offset(c, site) if self.ctr is not None else site
+        if self.ctr is None:
+            return site
+        return philox.rng_offset(int(self.ctr.item()), site)
+
+
+@dataclass
+class KVGrad:
+    """Side channel collecting every decoder layer's d(K|V) into one buffer so
+    the cross-K/V projection backward is a single GEMM pair."""
+
+    buf: Optional[torch.Tensor] = None
 
 
 def _keep_scale(rt: RunCtx, site: int, shape, device) -> Optional[torch.Tensor]:
-    """CPU reference dropout multiplier (keep/(1-p)) with the device RNG stream."""
+    """CPU reference dropout multiplier (keep/(1-p)) drawn from the device RNG stream."""
     p = rt.p
     if p <= 0:
         return None
@@ -77,6 +99,50 @@ def _write_grad(p: Param, g: torch.Tensor, rt: RunCtx) -> None:
         p.grad.add_(g.to(p.grad.dtype))
     else:
         p.grad.copy_(g.to(p.grad.dtype))
+
+
+# =============================================================================== LN helpers
+def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
+    """Returns (y, saved) for y = LN(x + dropout(s))."""
+    if x.is_cuda:
+        y, h, mean, rstd = K.ln_fwd(x.contiguous(), s.contiguous(), gamma.master, beta.master,
+                                    rt.p, rt.seed, rt.ctr, site)
+        return y, (h, mean, rstd, None)
+    ks = _keep_scale(rt, site, s.shape, s.device)
+    h = x + (s * ks if ks is not None else s)
+    mean = h.mean(-1, keepdim=True)
+    rstd = torch.rsqrt(((h - mean) ** 2).mean(-1, keepdim=True) + LN_EPS)
+    return (h - mean) * rstd * gamma.master + beta.master, (h, mean, rstd, ks)
+
+
+def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt: RunCtx):
+    """Returns (dh, ds): dh = dL/d(residual input) (fresh, writable), ds =
+    dL/d(sublayer output). Also writes dgamma, dbeta and the sublayer's output
+    bias gradient (sum of ds over rows)."""
+    h, mean, rstd, ks = saved
+    if dy.is_cuda:
+        dh, ds = K.ln_bwd(dy.contiguous(), h, mean, rstd, gamma.master, gamma.grad, beta.grad,
+                          sub_bias.grad, rt.p, rt.seed, rt.ctr, site, want_ds=True,
+                          accumulate=rt.accumulate)
+    else:
+        xhat = (h - mean) * rstd
+        D = h.shape[-1]
+        g = dy * gamma.master
+        dh = rstd * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))
+        ds = dh * ks if ks is not None else dh
+        _write_grad(gamma, (dy * xhat).reshape(-1, D).sum(0), rt)
+        _write_grad(beta, dy.reshape(-1, D).sum(0), rt)
+        _write_grad(sub_bias, ds.reshape(-1, D).sum(0), rt)
+    _ready(rt, gamma, beta, sub_bias)
+    return dh, ds
+
+
+def _dgrad_into(dy2: torch.Tensor, w: Param, N: int, dx: torch.Tensor) -> torch.Tensor:
+    """dx += dy2 @ w (the residual gradient already sits in dx)."""
+    if dy2.is_cuda:
+        return K.linear_dgrad(dy2, w.compute, N, out=dx.view(dy2.shape[0], -1), beta=1.0)
+    dx.view(dy2.shape[0], -1).add_(dy2 @ w.master)
+    return dx
 
 
 # =============================================================================== embedding
@@ -110,52 +176,6 @@ class EmbedFn(torch.autograd.Function):
         return None, None, None, None, None, None
 
 
-# =============================================================================== residual + LN
-class AddLNFn(torch.autograd.Function):
-    """y = LayerNorm(x + dropout(s)); optionally also produces the bias grad of
-    the sublayer that produced `s` (sum of ds over rows)."""
-
-    @staticmethod
-    def forward(ctx, x, s, gamma: Param, beta: Param, site: int, rt: RunCtx,
-                sub_bias: Optional[Param]):
-        ctx.gamma, ctx.beta, ctx.site, ctx.rt, ctx.sub_bias = gamma, beta, site, rt, sub_bias
-        p = rt.p
-        if x.is_cuda:
-            y, h, mean, rstd = K.ln_fwd(x.contiguous(), s.contiguous(), gamma.master, beta.master,
-                                        p, rt.seed, rt.ctr, site)
-            ctx.save_for_backward(h, mean, rstd)
-            return y
-        ks = _keep_scale(rt, site, s.shape, s.device)
-        h = x + (s * ks if ks is not None else s)
-        mean = h.mean(-1, keepdim=True)
-        var = ((h - mean) ** 2).mean(-1, keepdim=True)
-        rstd = torch.rsqrt(var + 1e-6)
-        ctx.ks = ks
-        ctx.save_for_backward(h, mean, rstd)
-        return (h - mean) * rstd * gamma.master + beta.master
-
-    @staticmethod
-    def backward(ctx, dy):
-        h, mean, rstd = ctx.saved_tensors
-        gamma, beta, rt, sb = ctx.gamma, ctx.beta, ctx.rt, ctx.sub_bias
-        if dy.is_cuda:
-            dh, ds = K.ln_bwd(dy.contiguous(), h, mean, rstd, gamma.master, gamma.grad, beta.grad,
-                              sb.grad if sb is not None else None, rt.p, rt.seed, rt.ctr, ctx.site,
-                              want_ds=True, accumulate=rt.accumulate)
-        else:
-            xhat = (h - mean) * rstd
-            D = h.shape[-1]
-            g = dy * gamma.master
-            dh = rstd * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))
-            ds = dh * ctx.ks if ctx.ks is not None else dh
-            _write_grad(gamma, (dy * xhat).reshape(-1, D).sum(0), rt)
-            _write_grad(beta, dy.reshape(-1, D).sum(0), rt)
-            if sb is not None:
-                _write_grad(sb, ds.reshape(-1, D).sum(0), rt)
-        _ready(rt, gamma, beta, *([sb] if sb is not None else []))
-        return dh, ds, None, None, None, None, None
-
-
 # =============================================================================== attention (CPU reference core)
 def _ref_attn_fwd(q, k, v, kv_len, causal, scale):
     """q [B,Lq,H,hd] ... -> out [B,Lq,H,hd], probs [B,H,Lq,Lk]. Masked logits
@@ -183,208 +203,237 @@ def _ref_attn_bwd(q, k, v, p, dout, scale):
     return dq, dk, dv
 
 
-# =============================================================================== multi-head attention
-class SelfMHAFn(torch.autograd.Function):
-    """out = Dense_o(SDPA(Dense_q x, Dense_k x, Dense_v x)) with fused QKV."""
+def attention_probs(q, k, kv_len, causal: bool, scale: float) -> torch.Tensor:
+    """Attention weights [B,H,Lq,Lk] (f32), the maps the reference returns."""
+    if q.is_cuda:
+        return K.attn_probs(q, k, kv_len, scale, causal)
+    return _ref_attn_fwd(q, k, k, kv_len, causal, scale)[1]
 
+
+# =============================================================================== self-attention block
+class SelfAttnBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wqkv: Param, bqkv: Param, wo: Param, bo: Param, heads: int,
-                kv_len, causal: bool, rt: RunCtx, fused_bo_grad: bool):
+    def forward(ctx, x, wqkv: Param, bqkv: Param, wo: Param, bo: Param, gamma: Param,
+                beta: Param, heads: int, kv_len, causal: bool, site: int, rt: RunCtx):
         B, L, d = x.shape
         hd = d // heads
         scale = 1.0 / math.sqrt(hd)
-        ctx.p = (wqkv, bqkv, wo, bo)
-        ctx.meta = (heads, causal, scale, rt, fused_bo_grad)
+        ctx.p = (wqkv, bqkv, wo, bo, gamma, beta)
+        ctx.meta = (heads, causal, scale, site, rt)
         x2 = x.reshape(B * L, d)
         if x.is_cuda:
             qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
-            o, lse = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
-            out = K.linear_fwd(o.view(B * L, d), wo.compute, bo.master)
-            ctx.save_for_backward(x2, qkv, o, lse, kv_len)
-            return out.view(B, L, d)
-        qkv = x2 @ wqkv.master.t() + bqkv.master
-        q5 = qkv.view(B, L, 3, heads, hd)
-        o, pr = _ref_attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, causal, scale)
-        out = o.reshape(B * L, d) @ wo.master.t() + bo.master
-        ctx.save_for_backward(x2, qkv, o, pr, kv_len)
-        return out.view(B, L, d)
+            o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
+            s = K.linear_fwd(o.view(B * L, d), wo.compute, bo.master)
+        else:
+            qkv = x2 @ wqkv.master.t() + bqkv.master
+            q5 = qkv.view(B, L, 3, heads, hd)
+            o, aux = _ref_attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, causal, scale)
+            s = o.reshape(B * L, d) @ wo.master.t() + bo.master
+        y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
+        ctx.save_for_backward(x2, qkv, o, aux, kv_len)
+        return y
 
     @staticmethod
-    def backward(ctx, dout):
-        wqkv, bqkv, wo, bo = ctx.p
-        heads, causal, scale, rt, fused_bo = ctx.meta
+    def backward(ctx, dy):
+        wqkv, bqkv, wo, bo, gamma, beta = ctx.p
+        heads, causal, scale, site, rt = ctx.meta
         x2, qkv, o, aux, kv_len = ctx.saved_tensors
-        B, L, d = dout.shape
+        B, L, d = dy.shape
         M = B * L
         hd = d // heads
-        dout2 = dout.reshape(M, d)
-        beta = _beta(rt)
-        if dout.is_cuda:
-            dout2 = dout2.contiguous()
-            o2 = o.view(M, d)
-            K.linear_wgrad(dout2, o2, d, wo.grad, beta)
-            if not fused_bo:
-                K.colsum(dout2, d, bo.grad, beta)
-            _ready(rt, wo, *([] if fused_bo else [bo]))
-            do = K.linear_dgrad(dout2, wo.compute, d)
-            dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dout.device)
-            q5 = qkv.view(B, L, 3, heads, hd)
+        bt = _beta(rt)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
+        ds2 = ds.reshape(M, d)
+        q5 = qkv.view(B, L, 3, heads, hd)
+        if dy.is_cuda:
+            K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
+            _ready(rt, wo)
+            do = K.linear_dgrad(ds2, wo.compute, d)
+            dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
             g5 = dqkv.view(B, L, 3, heads, hd)
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
-            K.linear_wgrad(dqkv, x2, 3 * d, wqkv.grad, beta)
-            K.colsum(dqkv, 3 * d, bqkv.grad, beta)
-            _ready(rt, wqkv, bqkv)
-            dx = K.linear_dgrad(dqkv, wqkv.compute, 3 * d)
-            return dx.view(B, L, d), None, None, None, None, None, None, None, None, None
-        o2 = o.reshape(M, d)
-        _write_grad(wo, dout2.t() @ o2, rt)
-        if not fused_bo:
-            _write_grad(bo, dout2.sum(0), rt)
-        do = (dout2 @ wo.master).view(B, L, heads, hd)
-        q5 = qkv.view(B, L, 3, heads, hd)
-        dq, dk, dv = _ref_attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], aux, do, scale)
-        dqkv = torch.stack([dq, dk, dv], dim=2).reshape(M, 3 * d)
-        _write_grad(wqkv, dqkv.t() @ x2, rt)
-        _write_grad(bqkv, dqkv.sum(0), rt)
-        _ready(rt, wo, *([] if fused_bo else [bo]), wqkv, bqkv)
-        dx = dqkv @ wqkv.master
-        return dx.view(B, L, d), None, None, None, None, None, None, None, None, None
+            K.linear_wgrad(dqkv, x2, 3 * d, wqkv.grad, bt)
+            K.colsum(dqkv, 3 * d, bqkv.grad, bt)
+        else:
+            _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
+            _ready(rt, wo)
+            do = (ds2 @ wo.master).view(B, L, heads, hd)
+            dq, dk, dv = _ref_attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], aux, do, scale)
+            dqkv = torch.stack([dq, dk, dv], dim=2).reshape(M, 3 * d)
+            _write_grad(wqkv, dqkv.t() @ x2, rt)
+            _write_grad(bqkv, dqkv.sum(0), rt)
+        _ready(rt, wqkv, bqkv)
+        dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
+        return (dx.view(B, L, d),) + (None,) * 11
 
 
-class CrossMHAFn(torch.autograd.Function):
+# =============================================================================== cross-attention
+class CrossKVFn(torch.autograd.Function):
+    """kv_all[B, S, layers*2*d] = enc @ Wkv_all^T + b: the K and V projections
+    of the encoder output for every decoder layer in one GEMM."""
+
+    @staticmethod
+    def forward(ctx, enc, wkv: Param, bkv: Param, kvh: KVGrad, rt: RunCtx):
+        B, S, d = enc.shape
+        e2 = enc.reshape(B * S, d)
+        ctx.p = (wkv, bkv)
+        ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
+        ctx.save_for_backward(e2)
+        if enc.is_cuda:
+            kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
+        else:
+            kv = e2 @ wkv.master.t() + bkv.master
+        return kv.view(B, S, -1)
+
+    @staticmethod
+    def backward(ctx, dkv_in):
+        wkv, bkv = ctx.p
+        rt = ctx.rt
+        B, S, d = ctx.shape
+        (e2,) = ctx.saved_tensors
+        # filled slice-by-slice by every CrossAttnBlockFn.backward (layer 0
+        # also hands it to autograd, which delivers it here as dkv_in)
+        dkv = (dkv_in if dkv_in is not None else ctx.kvh.buf).reshape(B * S, -1)
+        ctx.kvh.buf = None
+        N = wkv.shape[0]
+        bt = _beta(rt)
+        if e2.is_cuda:
+            K.linear_wgrad(dkv, e2, N, wkv.grad, bt)
+            K.colsum(dkv, N, bkv.grad, bt)
+            _ready(rt, wkv, bkv)
+            denc = K.linear_dgrad(dkv, wkv.compute, N)
+        else:
+            _write_grad(wkv, dkv.t() @ e2, rt)
+            _write_grad(bkv, dkv.sum(0), rt)
+            _ready(rt, wkv, bkv)
+            denc = dkv @ wkv.master
+        return denc.view(B, S, d), None, None, None, None
+
+
+class CrossAttnBlockFn(torch.autograd.Function):
     """Decoder block 2: Q from the decoder stream, K = V = encoder output
     (reference call order mha2(enc, enc, out1) -> values, keys, query)."""
 
     @staticmethod
-    def forward(ctx, x, enc, wq: Param, bq: Param, wkv: Param, bkv: Param, wo: Param, bo: Param,
-                heads: int, kv_len, rt: RunCtx, fused_bo_grad: bool):
+    def forward(ctx, x, kv_all, layer: int, kvh: KVGrad, wq: Param, bq: Param, wo: Param,
+                bo: Param, gamma: Param, beta: Param, heads: int, kv_len, site: int, rt: RunCtx):
         B, T, d = x.shape
-        S = enc.shape[1]
+        S = kv_all.shape[1]
         hd = d // heads
         scale = 1.0 / math.sqrt(hd)
-        ctx.p = (wq, bq, wkv, bkv, wo, bo)
-        ctx.meta = (heads, scale, rt, fused_bo_grad)
+        ctx.p = (wq, bq, wo, bo, gamma, beta)
+        ctx.meta = (heads, scale, site, rt, layer, kvh)
         x2 = x.reshape(B * T, d)
-        e2 = enc.reshape(B * S, d)
+        kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd) \
+            if kv_all.is_contiguous() else None
+        if kv5 is None:
+            raise ValueError("kv_all must be contiguous")
         if x.is_cuda:
             q = K.linear_fwd(x2, wq.compute, bq.master)
-            kv = K.linear_fwd(e2, wkv.compute, bkv.master)
-            kv5 = kv.view(B, S, 2, heads, hd)
-            o, lse = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
+            o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
                                 False)
-            out = K.linear_fwd(o.view(B * T, d), wo.compute, bo.master)
-            ctx.save_for_backward(x2, e2, q, kv, o, lse, kv_len)
-            return out.view(B, T, d)
-        q = x2 @ wq.master.t() + bq.master
-        kv = e2 @ wkv.master.t() + bkv.master
-        kv5 = kv.view(B, S, 2, heads, hd)
-        o, pr = _ref_attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, False,
-                              scale)
-        out = o.reshape(B * T, d) @ wo.master.t() + bo.master
-        ctx.save_for_backward(x2, e2, q, kv, o, pr, kv_len)
-        return out.view(B, T, d)
-
-    @staticmethod
-    def backward(ctx, dout):
-        wq, bq, wkv, bkv, wo, bo = ctx.p
-        heads, scale, rt, fused_bo = ctx.meta
-        x2, e2, q, kv, o, aux, kv_len = ctx.saved_tensors
-        B, T, d = dout.shape
-        S = e2.shape[0] // B
-        hd = d // heads
-        beta = _beta(rt)
-        dout2 = dout.reshape(B * T, d)
-        if dout.is_cuda:
-            dout2 = dout2.contiguous()
-            K.linear_wgrad(dout2, o.view(B * T, d), d, wo.grad, beta)
-            if not fused_bo:
-                K.colsum(dout2, d, bo.grad, beta)
-            _ready(rt, wo, *([] if fused_bo else [bo]))
-            do = K.linear_dgrad(dout2, wo.compute, d)
-            dq = torch.empty(B * T, d, dtype=torch.bfloat16, device=dout.device)
-            dkv = torch.empty(B * S, 2 * d, dtype=torch.bfloat16, device=dout.device)
-            kv5 = kv.view(B, S, 2, heads, hd)
-            g5 = dkv.view(B, S, 2, heads, hd)
-            K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
-                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
-                       g5[:, :, 1], kv_len, scale, False)
-            K.linear_wgrad(dkv, e2, 2 * d, wkv.grad, beta)
-            K.colsum(dkv, 2 * d, bkv.grad, beta)
-            K.linear_wgrad(dq, x2, d, wq.grad, beta)
-            K.colsum(dq, d, bq.grad, beta)
-            _ready(rt, wkv, bkv, wq, bq)
-            denc = K.linear_dgrad(dkv, wkv.compute, 2 * d)
-            dx = K.linear_dgrad(dq, wq.compute, d)
-            return (dx.view(B, T, d), denc.view(B, S, d)) + (None,) * 10
-        o2 = o.reshape(B * T, d)
-        _write_grad(wo, dout2.t() @ o2, rt)
-        if not fused_bo:
-            _write_grad(bo, dout2.sum(0), rt)
-        do = (dout2 @ wo.master).view(B, T, heads, hd)
-        kv5 = kv.view(B, S, 2, heads, hd)
-        dqh, dk, dv = _ref_attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], aux, do,
-                                    scale)
-        dq = dqh.reshape(B * T, d)
-        dkv = torch.stack([dk, dv], dim=2).reshape(B * S, 2 * d)
-        _write_grad(wkv, dkv.t() @ e2, rt)
-        _write_grad(bkv, dkv.sum(0), rt)
-        _write_grad(wq, dq.t() @ x2, rt)
-        _write_grad(bq, dq.sum(0), rt)
-        _ready(rt, wo, *([] if fused_bo else [bo]), wkv, bkv, wq, bq)
-        denc = dkv @ wkv.master
-        dx = dq @ wq.master
-        return (dx.view(B, T, d), denc.view(B, S, d)) + (None,) * 10
-
-
-# =============================================================================== feed-forward
-class FFNFn(torch.autograd.Function):
-    """Dense(ff, relu) -> Dense(d); ReLU backward fused into the dgrad GEMM."""
-
-    @staticmethod
-    def forward(ctx, x, w1: Param, b1: Param, w2: Param, b2: Param, rt: RunCtx,
-                fused_b2_grad: bool):
-        B, L, d = x.shape
-        x2 = x.reshape(B * L, d)
-        ctx.p = (w1, b1, w2, b2)
-        ctx.meta = (rt, fused_b2_grad)
-        if x.is_cuda:
-            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
-            y = K.linear_fwd(h, w2.compute, b2.master)
+            s = K.linear_fwd(o.view(B * T, d), wo.compute, bo.master)
         else:
-            h = torch.relu(x2 @ w1.master.t() + b1.master)
-            y = h @ w2.master.t() + b2.master
-        ctx.save_for_backward(x2, h)
-        return y.view(B, L, d)
+            q = x2 @ wq.master.t() + bq.master
+            o, aux = _ref_attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len,
+                                   False, scale)
+            s = o.reshape(B * T, d) @ wo.master.t() + bo.master
+        y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
+        ctx.save_for_backward(x2, kv_all, q, o, aux, kv_len)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        w1, b1, w2, b2 = ctx.p
-        rt, fused_b2 = ctx.meta
+        wq, bq, wo, bo, gamma, beta = ctx.p
+        heads, scale, site, rt, layer, kvh = ctx.meta
+        x2, kv_all, q, o, aux, kv_len = ctx.saved_tensors
+        B, T, d = dy.shape
+        S = kv_all.shape[1]
+        hd = d // heads
+        bt = _beta(rt)
+        M = B * T
+        if kvh.buf is None:
+            kvh.buf = torch.empty(B * S, kv_all.shape[2], dtype=kv_all.dtype, device=dy.device)
+        dkv_all = kvh.buf.view(B, S, -1)
+        kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+        g5 = dkv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
+        ds2 = ds.reshape(M, d)
+        if dy.is_cuda:
+            K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
+            _ready(rt, wo)
+            do = K.linear_dgrad(ds2, wo.compute, d)
+            dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
+            K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
+                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
+                       g5[:, :, 1], kv_len, scale, False)
+            K.linear_wgrad(dq, x2, d, wq.grad, bt)
+            K.colsum(dq, d, bq.grad, bt)
+        else:
+            _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
+            _ready(rt, wo)
+            do = (ds2 @ wo.master).view(B, T, heads, hd)
+            dqh, dk, dv = _ref_attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], aux,
+                                        do, scale)
+            g5[:, :, 0] = dk
+            g5[:, :, 1] = dv
+            dq = dqh.reshape(M, d)
+            _write_grad(wq, dq.t() @ x2, rt)
+            _write_grad(bq, dq.sum(0), rt)
+        _ready(rt, wq, bq)
+        dx = _dgrad_into(dq, wq, d, dh)
+        # Only layer 0 hands the (by then complete) shared buffer to autograd;
+        # the other layers contribute through the side channel, so no adds.
+        dkv_ret = dkv_all if layer == 0 else None
+        return (dx.view(B, T, d), dkv_ret) + (None,) * 12
+
+
+# =============================================================================== feed-forward block
+class FFNBlockFn(torch.autograd.Function):
+    """y = LN(x + dropout(Dense(d)(Dense(ff, relu)(x))))."""
+
+    @staticmethod
+    def forward(ctx, x, w1: Param, b1: Param, w2: Param, b2: Param, gamma: Param, beta: Param,
+                site: int, rt: RunCtx):
+        B, L, d = x.shape
+        x2 = x.reshape(B * L, d)
+        ctx.p = (w1, b1, w2, b2, gamma, beta)
+        ctx.meta = (site, rt)
+        if x.is_cuda:
+            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
+            f = K.linear_fwd(h, w2.compute, b2.master)
+        else:
+            h = torch.relu(x2 @ w1.master.t() + b1.master)
+            f = h @ w2.master.t() + b2.master
+        y, ctx.ln = _ln_fwd(x, f.view(B, L, d), gamma, beta, site, rt)
+        ctx.save_for_backward(x2, h)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        w1, b1, w2, b2, gamma, beta = ctx.p
+        site, rt = ctx.meta
         x2, h = ctx.saved_tensors
         B, L, d = dy.shape
         ff = h.shape[1]
-        beta = _beta(rt)
-        dy2 = dy.reshape(B * L, d)
+        bt = _beta(rt)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt)
+        ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
-            dy2 = dy2.contiguous()
-            K.linear_wgrad(dy2, h, d, w2.grad, beta)
-            if not fused_b2:
-                K.colsum(dy2, d, b2.grad, beta)
-            _ready(rt, w2, *([] if fused_b2 else [b2]))
-            dpre = K.linear_dgrad(dy2, w2.compute, d, relu_aux=h)
-            K.linear_wgrad(dpre, x2, ff, w1.grad, beta)
-            K.colsum(dpre, ff, b1.grad, beta)
-            _ready(rt, w1, b1)
-            dx = K.linear_dgrad(dpre, w1.compute, ff)
-            return dx.view(B, L, d), None, None, None, None, None, None
-        _write_grad(w2, dy2.t() @ h, rt)
-        if not fused_b2:
-            _write_grad(b2, dy2.sum(0), rt)
-        dpre = (dy2 @ w2.master) * (h > 0).to(dy2.dtype)
-        _write_grad(w1, dpre.t() @ x2, rt)
-        _write_grad(b1, dpre.sum(0), rt)
-        _ready(rt, w2, *([] if fused_b2 else [b2]), w1, b1)
-        dx = dpre @ w1.master
-        return dx.view(B, L, d), None, None, None, None, None, None
+            K.linear_wgrad(ds2, h, d, w2.grad, bt)
+            _ready(rt, w2)
+            dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
+            K.linear_wgrad(dpre, x2, ff, w1.grad, bt)
+            K.colsum(dpre, ff, b1.grad, bt)
+        else:
+            _write_grad(w2, ds2.t() @ h, rt)
+            _ready(rt, w2)
+            dpre = (ds2 @ w2.master) * (h > 0).to(ds2.dtype)
+            _write_grad(w1, dpre.t() @ x2, rt)
+            _write_grad(b1, dpre.sum(0), rt)
+        _ready(rt, w1, b1)
+        dx = _dgrad_into(dpre, w1, ff, dh)
+        return (dx.view(B, L, d),) + (None,) * 8

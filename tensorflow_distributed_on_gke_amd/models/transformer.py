@@ -20,8 +20,9 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from tensorflow_distributed_on_gke_amd.models.layers import (AddLNFn, CrossMHAFn, EmbedFn, FFNFn,
-                                                              RunCtx, SelfMHAFn)
+from tensorflow_distributed_on_gke_amd.models.layers import (CrossAttnBlockFn, CrossKVFn, EmbedFn,
+                                                              FFNBlockFn, KVGrad, RunCtx,
+                                                              SelfAttnBlockFn)
 from tensorflow_distributed_on_gke_amd.models.params import (ParamStore, TFSlot, const,
                                                               glorot_blocks, glorot_uniform,
                                                               uniform)
@@ -81,7 +82,8 @@ def _var(key: str) -> str:
 
 
 class _Dense:
-    """Helper to register a Dense layer (or a fused stack of them)."""
+    """Registers a Dense layer, or a fused stack of several Dense layers that
+    read the same input (their [out, in] kernels stacked along `out`)."""
 
     def __init__(self, store: ParamStore, name: str, tf_prefixes: List[str], d_in: int, d_out: int):
         k = len(tf_prefixes)
@@ -101,6 +103,8 @@ class _LN:
 
 
 class EncoderLayer:
+    """reference: transformer_model.py:178-204"""
+
     def __init__(self, store: ParamStore, i: int, cfg: ModelConfig, sites):
         d, ff = cfg.d_model, cfg.d_ff
         pre = f"encoder/encoder_layers/{i}"
@@ -116,24 +120,26 @@ class EncoderLayer:
         self.heads = cfg.heads
 
     def __call__(self, x, src_len, rt: RunCtx):
-        a = SelfMHAFn.apply(x, self.qkv.w, self.qkv.b, self.o.w, self.o.b, self.heads, src_len,
-                            False, rt, True)
-        x = AddLNFn.apply(x, a, self.ln1.gamma, self.ln1.beta, self.site1, rt, self.o.b)
-        f = FFNFn.apply(x, self.ff1.w, self.ff1.b, self.ff2.w, self.ff2.b, rt, True)
-        return AddLNFn.apply(x, f, self.ln2.gamma, self.ln2.beta, self.site2, rt, self.ff2.b)
+        x = SelfAttnBlockFn.apply(x, self.qkv.w, self.qkv.b, self.o.w, self.o.b, self.ln1.gamma,
+                                  self.ln1.beta, self.heads, src_len, False, self.site1, rt)
+        return FFNBlockFn.apply(x, self.ff1.w, self.ff1.b, self.ff2.w, self.ff2.b, self.ln2.gamma,
+                                self.ln2.beta, self.site2, rt)
 
 
 class DecoderLayer:
+    """reference: transformer_model.py:207-248 (the cross-attention K/V
+    projections of all layers live in Transformer.cross_kv)"""
+
     def __init__(self, store: ParamStore, i: int, cfg: ModelConfig, sites):
         d, ff = cfg.d_model, cfg.d_ff
         pre = f"decoder/decoder_layers/{i}"
         m1, m2 = pre + "/mha1", pre + "/mha2"
+        self.index = i
         self.qkv1 = _Dense(store, m1 + "/qkv", [m1 + "/query_generator_weights", m1 + "/key_generator_weights",
                                                 m1 + "/value_generator_weights"], d, d)
         self.o1 = _Dense(store, m1 + "/dense", [m1 + "/dense"], d, d)
         self.ln1 = _LN(store, pre + "/layernorm1", d)
         self.q2 = _Dense(store, m2 + "/query_generator_weights", [m2 + "/query_generator_weights"], d, d)
-        self.kv2 = _Dense(store, m2 + "/kv", [m2 + "/key_generator_weights", m2 + "/value_generator_weights"], d, d)
         self.o2 = _Dense(store, m2 + "/dense", [m2 + "/dense"], d, d)
         self.ln2 = _LN(store, pre + "/layernorm2", d)
         self.ff1 = _Dense(store, pre + "/ffn/layer_with_weights-0", [pre + "/ffn/layer_with_weights-0"], d, ff)
@@ -142,15 +148,14 @@ class DecoderLayer:
         self.site1, self.site2, self.site3 = next(sites), next(sites), next(sites)
         self.heads = cfg.heads
 
-    def __call__(self, x, enc, src_len, tgt_len, rt: RunCtx):
-        a = SelfMHAFn.apply(x, self.qkv1.w, self.qkv1.b, self.o1.w, self.o1.b, self.heads, tgt_len,
-                            True, rt, True)
-        x = AddLNFn.apply(x, a, self.ln1.gamma, self.ln1.beta, self.site1, rt, self.o1.b)
-        c = CrossMHAFn.apply(x, enc, self.q2.w, self.q2.b, self.kv2.w, self.kv2.b, self.o2.w,
-                             self.o2.b, self.heads, src_len, rt, True)
-        x = AddLNFn.apply(x, c, self.ln2.gamma, self.ln2.beta, self.site2, rt, self.o2.b)
-        f = FFNFn.apply(x, self.ff1.w, self.ff1.b, self.ff2.w, self.ff2.b, rt, True)
-        return AddLNFn.apply(x, f, self.ln3.gamma, self.ln3.beta, self.site3, rt, self.ff2.b)
+    def __call__(self, x, kv_all, kvh: KVGrad, src_len, tgt_len, rt: RunCtx):
+        x = SelfAttnBlockFn.apply(x, self.qkv1.w, self.qkv1.b, self.o1.w, self.o1.b, self.ln1.gamma,
+                                  self.ln1.beta, self.heads, tgt_len, True, self.site1, rt)
+        x = CrossAttnBlockFn.apply(x, kv_all, self.index, kvh, self.q2.w, self.q2.b, self.o2.w,
+                                   self.o2.b, self.ln2.gamma, self.ln2.beta, self.heads, src_len,
+                                   self.site2, rt)
+        return FFNBlockFn.apply(x, self.ff1.w, self.ff1.b, self.ff2.w, self.ff2.b, self.ln3.gamma,
+                                self.ln3.beta, self.site3, rt)
 
 
 def seq_lengths(tok: torch.Tensor) -> torch.Tensor:
@@ -173,6 +178,14 @@ class Transformer:
                              [TFSlot(_var("encoder/embedding/embeddings"), 0, cfg.src_vocab, False)])
         self.enc_site = next(sites)
         self.enc_layers = [EncoderLayer(S, i, cfg, sites) for i in range(cfg.layers)]
+        # K|V projections of the encoder output for every decoder layer,
+        # stacked [layers*2*d, d] so the forward is one GEMM (reference: each
+        # decoder_layers/{i}/mha2/{key,value}_generator_weights Dense)
+        kv_prefixes = []
+        for i in range(cfg.layers):
+            m2 = f"decoder/decoder_layers/{i}/mha2"
+            kv_prefixes += [m2 + "/key_generator_weights", m2 + "/value_generator_weights"]
+        self.cross_kv = _Dense(S, "decoder/cross_kv_all", kv_prefixes, d, d)
         self.dec_emb = S.add("decoder/embedding/embeddings", (cfg.tgt_vocab, d), uniform(-0.05, 0.05),
                              [TFSlot(_var("decoder/embedding/embeddings"), 0, cfg.tgt_vocab, False)])
         self.dec_site = next(sites)
@@ -210,9 +223,11 @@ class Transformer:
     def decode(self, tgt_in: torch.Tensor, enc: torch.Tensor, src_len, tgt_len, rt: RunCtx) -> torch.Tensor:
         if tgt_in.shape[1] > self.cfg.max_tgt_len:
             raise ValueError(f"target length {tgt_in.shape[1]} > positional table {self.cfg.max_tgt_len}")
+        kvh = KVGrad()
+        kv_all = CrossKVFn.apply(enc, self.cross_kv.w, self.cross_kv.b, kvh, rt)
         x = EmbedFn.apply(self.store.anchor, tgt_in.contiguous(), self.dec_emb, self.pe_tgt, self.dec_site, rt)
         for layer in self.dec_layers:
-            x = layer(x, enc, src_len, tgt_len, rt)
+            x = layer(x, kv_all, kvh, src_len, tgt_len, rt)
         return x
 
     def features(self, src, tgt_in, rt: RunCtx):

@@ -70,13 +70,16 @@ AUTOTUNE = True
 _CANDIDATES = [(0, 1), (2, 1), (7, 1), (8, 1), (4, 1), (10, 1)]
 
 
-def _autotune(key, run) -> Tuple[int, int]:
+def _autotune(key, run, blas_ok=False) -> Tuple[int, int]:
     """Time the candidate tile configs once for this problem (3 reps each, HIP
-    events on the current stream) and keep the fastest."""
+    events on the current stream) and keep the fastest. Plain GEMMs also try
+    the library (hipBLASLt) path."""
     M, N, K, a_kc, b_kc = key[:5]
     cands = list(_CANDIDATES)
     if not a_kc and not b_kc:
         cands = [(c, s) for c in (0, 7, 8) for s in (1, 2, 4, 8) if K // s >= 256]
+    if blas_ok:
+        cands.append(BLAS)
     best = None
     for cfg in cands:
         try:
@@ -95,33 +98,72 @@ def _autotune(key, run) -> Tuple[int, int]:
     return best[0]
 
 
+BLAS = (-1, 1)  # "config" meaning: plain library GEMM (hipBLASLt via torch)
+ALLOW_BLAS = True
+
+
+def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N) -> bool:
+    """Plain GEMMs only (no fused epilogue): dgrad (KC x MC, bf16 out) and
+    wgrad (MC x MC, f32 out) may go to hipBLASLt if it is faster."""
+    if not ALLOW_BLAS or epi != EPI_NONE or alpha != 1.0 or beta != 0.0 or ldc != N:
+        return False
+    return (a_kc and not b_kc and Cout.dtype == torch.bfloat16) or \
+        (not a_kc and not b_kc and Cout.dtype == torch.float32)
+
+
+def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc):
+    a = A.as_strided((M, K), (lda, 1)) if a_kc else A.as_strided((K, M), (lda, 1)).t()
+    b = B.as_strided((K, N), (ldb, 1))
+    c = Cout.as_strided((M, N), (N, 1))
+    if Cout.dtype == torch.bfloat16:
+        torch.mm(a, b, out=c)
+    else:
+        torch.mm(a, b, out_dtype=torch.float32, out=c)
+
+
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
          ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    def run(c):
+    blas_ok = _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N)
+
+    def run(c, out=Cout):
+        if c == BLAS:
+            if not blas_ok:
+                raise RuntimeError("library GEMM not applicable")
+            _blas(A, B, out, M, N, K, lda, ldb, a_kc)
+            return
         tile, splits = c
         ws = workspace("splitk", splits * M * ldc, A.device) if splits > 1 else None
-        C().gemm(A, B, Cout, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha,
+        C().gemm(A, B, out, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha,
                  beta, tile, splits, ws)
 
     if cfg is None:
-        key = (M, N, K, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0)
-        cfg = _TUNED.get(key)
-        if cfg is None:
-            cfg = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
-        if cfg is None:
-            if (AUTOTUNE and beta == 0.0 and A.is_cuda
-                    and not torch.cuda.is_current_stream_capturing()):
-                cfg = _autotune(key, run)
-                _TUNED[key] = cfg
+        key = (M, N, K, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0, beta != 0.0)
+        ent = _TUNED.get(key)
+        if ent is None:
+            o = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
+            if o is not None:
+                ent = (o, o)
+        if ent is None and AUTOTUNE and A.is_cuda and not torch.cuda.is_current_stream_capturing():
+            if beta != 0.0:
+                # accumulate into C: tune on a scratch copy so C is untouched
+                scratch = workspace("tune_c", Cout.numel(), A.device, Cout.dtype)[: Cout.numel()]
+                scratch = scratch.view_as(Cout)
+                best = _autotune(key, lambda c: run(c, scratch), False)
             else:
-                cfg = choose_gemm(M, N, K, a_kc, b_kc)
+                best = _autotune(key, run, blas_ok)
+            ent = (best, best)
+            _TUNED[key] = ent
+        if ent is None:
+            cfg = choose_gemm(M, N, K, a_kc, b_kc)
+        else:
+            cfg = ent[0]
     run(cfg)
     return Cout
 
 
 def tuned_table() -> Dict[str, str]:
-    return {f"{k[0]}x{k[1]}x{k[2]} a_kc={k[3]} b_kc={k[4]} epi={k[5]}": f"cfg{v[0]} split{v[1]}"
-            for k, v in _TUNED.items()}
+    return {f"{k[0]}x{k[1]}x{k[2]} a_kc={k[3]} b_kc={k[4]} epi={k[5]}":
+            ("hipblaslt" if v == BLAS else f"cfg{v[0]} split{v[1]}") for k, v in _TUNED.items()}
 
 
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
