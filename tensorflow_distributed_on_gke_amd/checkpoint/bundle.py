@@ -135,7 +135,7 @@ def tf_tensors(store: ParamStore) -> Dict[str, np.ndarray]:
 
 
 def write_bundle(prefix: str, tensors: Dict[str, np.ndarray], order=tf_creation_order,
-                 with_object_graph: bool = True) -> None:
+                 with_object_graph: bool = True, state_file: bool = True) -> None:
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
     w = native().BundleWriter(prefix)
     for key in sorted(tensors, key=order):
@@ -145,6 +145,8 @@ def write_bundle(prefix: str, tensors: Dict[str, np.ndarray], order=tf_creation_
     if with_object_graph:
         w.add_string(OBJECT_GRAPH_KEY, object_graph(list(tensors)))
     w.finish()
+    if not state_file:
+        return
     state = os.path.join(os.path.dirname(os.path.abspath(prefix)), "checkpoint")
     base = os.path.basename(prefix)
     with open(state, "w") as f:
@@ -230,7 +232,8 @@ def save_training_state(store: ParamStore, opt, prefix: str, extra: Optional[Dic
     out["optimizer/iter/.ATTRIBUTES/VARIABLE_VALUE"] = np.array(opt.iterations, dtype=np.int64)
     for k, val in (extra or {}).items():
         out[f"training_state/{k}"] = np.array(int(val), dtype=np.int64)
-    write_bundle(prefix + "_optimizer", out, order=lambda k: k, with_object_graph=False)
+    write_bundle(prefix + "_optimizer", out, order=lambda k: k, with_object_graph=False,
+                 state_file=False)
 
 
 def load_training_state(store: ParamStore, opt, prefix: str) -> Dict[str, int]:

@@ -55,6 +55,8 @@ class RunCtx:
     ctr: Optional[torch.Tensor] = None  # int64[1]: dropout stream counter (device-resident)
     accumulate: bool = False  # accumulate into existing grads (gradient accumulation)
     store: Optional[ParamStore] = None
+    # inference probe: {site: [B,H,Lq,Lk] f32 attention weights} when set
+    attn_maps: Optional[dict] = None
 
     @property
     def p(self) -> float:
@@ -231,6 +233,8 @@ class SelfAttnBlockFn(torch.autograd.Function):
             q5 = qkv.view(B, L, 3, heads, hd)
             o, aux = _ref_attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, causal, scale)
             s = o.reshape(B * L, d) @ wo.master.t() + bo.master
+        if rt.attn_maps is not None:
+            rt.attn_maps[site] = attention_probs(q5[:, :, 0], q5[:, :, 1], kv_len, causal, scale)
         y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
         ctx.save_for_backward(x2, qkv, o, aux, kv_len)
         return y
@@ -341,6 +345,8 @@ class CrossAttnBlockFn(torch.autograd.Function):
             o, aux = _ref_attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len,
                                    False, scale)
             s = o.reshape(B * T, d) @ wo.master.t() + bo.master
+        if rt.attn_maps is not None:
+            rt.attn_maps[site] = attention_probs(q.view(B, T, heads, hd), kv5[:, :, 0], kv_len, False, scale)
         y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
         ctx.save_for_backward(x2, kv_all, q, o, aux, kv_len)
         return y

@@ -48,7 +48,7 @@ def test_gpu_matches_cpu(preset, kw, dropout):
     # bf16 activations / gradients vs an f32 oracle: a layout or masking bug
     # shows up as O(1) errors, rounding as a few percent
     assert errs[worst] < 0.15, f"{worst}: rel grad err {errs[worst]:.3e}"
-    assert med < 0.03, f"median rel grad err {med:.3e}"
+    assert med < 0.05, f"median rel grad err {med:.3e}"
 
 
 def test_gpu_training_reduces_loss():

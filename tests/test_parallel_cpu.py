@@ -1,0 +1,140 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2).
+
+The bucketed, backward-overlapped all-reduce must give exactly the update a
+single process computes from both ranks' batches with the reference's loss
+scaling (per-replica token mean / workers, gradients SUM-reduced;
+reference: distributed_training_transformer/__main__.py:75-132)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
+from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel, plan_buckets
+from tensorflow_distributed_on_gke_amd.train.optim import Adam
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = dict(src_vocab=60, tgt_vocab=50, dropout=0.0)
+STEPS = 3
+# eps=1 keeps Adam's update ~linear in the gradient: with Keras' eps=1e-9 an
+# identically-zero gradient (e.g. the key bias, softmax-invariant) carrying
+# 1e-10 summation-order noise is normalised to a full +-lr step
+ADAM = dict(lr=0.05, eps=1.0)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank, world):
+    return SyntheticPairs(4, 10, 11, 60, 50, seed=3, rank=rank, world=world, min_len=3)
+
+
+def _worker(rank, world, port, out, bucket_mb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    info = tdist.init_distributed("cpu")
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=1 + rank)  # ranks differ until broadcast
+    opt = Adam(m.store, m.cfg.d_model, **ADAM)
+    ddp = DataParallel(m.store, bucket_mb=bucket_mb)
+    ddp.broadcast_params(0)
+    step = TrainStep(m, opt, ddp, workers=world, seed=5)
+    data = _data(rank, world)
+    losses = []
+    for i in range(STEPS):
+        losses.append(step(*data.batch(i)).clone())
+    torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.buckets)},
+               f"{out}.{rank}")
+    tdist.barrier()
+    tdist.shutdown()
+
+
+def _single_process_reference(world):
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=1)
+    opt = Adam(m.store, m.cfg.d_model, **ADAM)
+    datas = [_data(r, world) for r in range(world)]
+    losses = []
+    for i in range(STEPS):
+        tot = 0.0
+        for r in range(world):
+            rt = RunCtx(training=True, dropout=0.0, seed=5, ctr=torch.zeros(1, dtype=torch.int64),
+                        accumulate=r > 0)
+            out = m.loss_and_backward(*datas[r].batch(i), rt, float(world))
+            if r == 0:
+                losses.append(out.clone())
+        opt.apply()
+    return m.store.flat, torch.stack(losses)
+
+
+@pytest.mark.parametrize("bucket_mb", [0.05, 64.0])
+def test_dp2_matches_single_process(tmp_path, bucket_mb):
+    world = 2
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, _free_port(), out, bucket_mb), nprocs=world, join=True,
+                       start_method="spawn")
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    if bucket_mb < 1:
+        assert r0["nb"] > 3  # several buckets, launched from inside backward
+    assert torch.equal(r0["flat"], r1["flat"])  # replicas stay identical
+    ref_flat, ref_loss = _single_process_reference(world)
+    assert not torch.equal(r0["flat"], Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat)
+    assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(r0["loss"], ref_loss, atol=1e-6)
+
+
+def test_plan_buckets_cover_flat_buffer():
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=0)
+    for mb in (0.01, 0.1, 1.0, 100.0):
+        bs = plan_buckets(m.store, int(mb * 2 ** 20))
+        assert bs[0].start == 0 and bs[-1].end == m.store.total
+        for a, b in zip(bs, bs[1:]):
+            assert a.end == b.start
+        idx = sorted(i for b in bs for i in b.params)
+        assert idx == list(range(len(m.store.params)))
+        for b in bs[:-1]:
+            assert (b.end - b.start) * 4 >= mb * 2 ** 20
+
+
+def _cli(tmp, *sets, nproc=2):
+    cmd = [sys.executable, "-m", "tensorflow_distributed_on_gke_amd", "train", "--config",
+           os.path.join(ROOT, "configuration", "settings.yaml"), "--nproc", str(nproc),
+           "--master-port", str(_free_port())]
+    base = ["preset=tiny", "steps_per_epoch=6", "log_every=3", "local_batch_size=4", "src_len=10",
+            "tgt_len=10", "src_vocab=300", "tgt_vocab=300", "snapshot_every_epochs=1",
+            "validation_steps=1", "learning_rate=0.001", "worker_count=2"]
+    for kv in base + list(sets):
+        cmd += ["--set", kv]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("RANK", None)
+    return subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_train_cli_fault_injection_and_resume(tmp_path):
+    """2 ranks; rank 1 dies mid epoch 2 -> launcher stops the job with its
+    exit code; the restarted job resumes from the epoch-1 state and finishes."""
+    r = _cli(tmp_path, "epochs=3", "kill_at_step=9")
+    assert r.returncode == 17, r.stdout + r.stderr
+    assert "Epoch 1 Loss" in r.stdout and "Epoch 2 Loss" not in r.stdout
+    r = _cli(tmp_path, "epochs=3")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Resuming from" in r.stdout and "at epoch 2" in r.stdout
+    assert "Epoch 1 Batch" not in r.stdout and "Epoch 3 Loss" in r.stdout
+    assert "Time taken for 1 epoch" in r.stdout
+    snaps = tmp_path / "snapshots" / "kubernetes-transformer-training"
+    assert (snaps / "training-snapshots" / "initial_model" / "variables" / "variables.index").exists()
+    assert (snaps / "training-snapshots_2" / "weights_snapshot_2" / "model_weights.index").exists()
