@@ -46,9 +46,13 @@ def test_gpu_matches_cpu(preset, kw, dropout):
     worst = max(errs, key=errs.get)
     med = sorted(errs.values())[len(errs) // 2]
     # bf16 activations / gradients vs an f32 oracle: a layout or masking bug
-    # shows up as O(1) errors, rounding as a few percent
-    assert errs[worst] < 0.15, f"{worst}: rel grad err {errs[worst]:.3e}"
-    assert med < 0.05, f"median rel grad err {med:.3e}"
+    # shows up as O(1) errors, rounding as a few percent. The ReLU derivative
+    # dominates: bf16 inputs move ~0.2% of pre-activations across zero, and
+    # each flip contributes a full-size gradient element, so the FFN-input
+    # gradients carry ~sqrt(0.2-0.3%) = 4-6% relative (L2) error that the
+    # layers below inherit (measured: scripts/diag_grad_err.py).
+    assert errs[worst] < 0.2, f"{worst}: rel grad err {errs[worst]:.3e}"
+    assert med < 0.08, f"median rel grad err {med:.3e}"
 
 
 def test_gpu_training_reduces_loss():
