@@ -70,6 +70,8 @@ class Settings:
     bucket_mb: float = 64.0
     hip_graph: bool = False
     idle_after_train: bool = False  # reference __main__.py:183-186 keeps the pod alive
+    check_replicas_every: int = 0  # debug: assert bitwise-identical replicas every N steps
+    metrics_file: Optional[str] = None  # JSONL metrics sink (rank 0)
     kill_at_step: int = -1  # fault injection (tests): global step at which to exit
     kill_rank: int = -1  # rank that exits (-1: the last rank)
     loss_mode: str = "replica_mean"  # reference per-replica token mean / workers

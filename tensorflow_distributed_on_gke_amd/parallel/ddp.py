@@ -127,6 +127,22 @@ class DataParallel:
                 view.copy_(buf)
         self.reset()
 
+    def verify_replicas(self) -> None:
+        """Debug check (race / divergence detection): every rank's weights must
+        be bitwise identical after a synchronous step. Compares an exact
+        checksum (sum of the int32 bit patterns, int64) across ranks."""
+        if self.world <= 1:
+            return
+        bits = self.store.flat.detach().view(torch.int32)
+        local = torch.stack([bits.sum(dtype=torch.int64), (bits.to(torch.int64) * 2654435761).sum()])
+        allv = [torch.zeros_like(local) for _ in range(self.world)]
+        dist.all_gather(allv, local, group=self.group)
+        ref = allv[0]
+        bad = [r for r, v in enumerate(allv) if not torch.equal(v, ref)]
+        if bad:
+            raise RuntimeError(f"replica divergence: ranks {bad} differ from rank 0 "
+                               f"({[tuple(v.tolist()) for v in allv]})")
+
     def allreduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
             dist.all_reduce(t, group=self.group)

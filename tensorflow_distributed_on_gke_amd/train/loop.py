@@ -43,6 +43,7 @@ from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+from tensorflow_distributed_on_gke_amd.utils.profiling import MetricsWriter, StepTimer, summarize
 
 RESUME_DIR = "resume"
 RESUME_PREFIX = "model_weights"
@@ -96,6 +97,8 @@ class Trainer:
         self.start_epoch = 0
         self.uploader: Optional[ModelUploader] = None
         self.global_step = 0
+        self.timer = StepTimer(info.device)
+        self.metrics = MetricsWriter(s.metrics_file if info.chief else None)
 
     # ------------------------------------------------------------------ state
     @property
@@ -185,8 +188,13 @@ class Trainer:
                 if s.hip_graph and info.device.type == "cuda" and not captured:
                     self.step_fn.capture(src, tgt)
                     captured = True
+                self.timer.start()
                 self.step_fn(src, tgt)
+                self.timer.stop()
                 self.global_step += 1
+                if self.ddp is not None and s.check_replicas_every > 0 and \
+                        self.global_step % s.check_replicas_every == 0:
+                    self.ddp.verify_replicas()
                 if s.kill_at_step >= 0 and self.global_step == s.kill_at_step and \
                         info.rank == (s.kill_rank % info.world):
                     self.log(f"fault injection: rank {info.rank} exiting at step {self.global_step}")
@@ -195,9 +203,13 @@ class Trainer:
                 if batch % s.log_every == 0:
                     a = self._reduce(self.step_fn.accum)
                     n = max(float(a[2]) / info.world, 1.0)
+                    st = summarize(self.timer.drain())
                     if info.chief:
                         self.log(f"Epoch {epoch + 1} Batch {batch} Loss {float(a[0]) / n:.4f} "
                                  f"Accuracy {float(a[1]) / (n * info.world):.4f}")
+                        self.metrics.write(kind="train", epoch=epoch + 1, batch=batch, step=self.global_step,
+                                           loss=float(a[0]) / n, accuracy=float(a[1]) / (n * info.world),
+                                           **st)
             a = self._reduce(self.step_fn.accum)
             n = max(float(a[2]) / info.world, 1.0)
             train_loss = float(a[0]) / n
@@ -215,6 +227,8 @@ class Trainer:
             st = EpochStats(epoch + 1, train_loss, train_acc, val["loss"], val["acc"], dt,
                             tok_per_step * steps / max(train_time, 1e-9))
             self.history.append(st)
+            self.timer.drain()
+            self.metrics.write(kind="epoch", **st.__dict__)
             if info.chief:
                 self.log(f"Epoch {epoch + 1} Loss {train_loss:.4f} Accuracy {train_acc:.4f} "
                          f"Test Loss {val['loss']:.4f} Test Accuracy {val['acc']:.4f}")

@@ -57,7 +57,18 @@ def _worker(rank, world, port, out, bucket_mb):
     losses = []
     for i in range(STEPS):
         losses.append(step(*data.batch(i)).clone())
-    torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.buckets)},
+        ddp.verify_replicas()
+    saved = m.store.flat[0].clone()
+    if rank == 1:  # a diverged replica is detected
+        m.store.flat[0] += 1.0
+    try:
+        ddp.verify_replicas()
+        diverged = False
+    except RuntimeError:
+        diverged = True
+    m.store.flat[0] = saved
+    torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.buckets),
+                "diverged": diverged},
                f"{out}.{rank}")
     tdist.barrier()
     tdist.shutdown()
@@ -91,6 +102,7 @@ def test_dp2_matches_single_process(tmp_path, bucket_mb):
     if bucket_mb < 1:
         assert r0["nb"] > 3  # several buckets, launched from inside backward
     assert torch.equal(r0["flat"], r1["flat"])  # replicas stay identical
+    assert r0["diverged"] and r1["diverged"]
     ref_flat, ref_loss = _single_process_reference(world)
     assert not torch.equal(r0["flat"], Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat)
     assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
@@ -116,7 +128,7 @@ def _cli(tmp, *sets, nproc=2):
            "--master-port", str(_free_port())]
     base = ["preset=tiny", "steps_per_epoch=6", "log_every=3", "local_batch_size=4", "src_len=10",
             "tgt_len=10", "src_vocab=300", "tgt_vocab=300", "snapshot_every_epochs=1",
-            "validation_steps=1", "learning_rate=0.001", "worker_count=2"]
+            "validation_steps=1", "learning_rate=0.001", "worker_count=2", "check_replicas_every=2"]
     for kv in base + list(sets):
         cmd += ["--set", kv]
     env = dict(os.environ, PYTHONPATH=ROOT)
