@@ -24,6 +24,8 @@
 #include "tdg_common.h"
 #include "tdg_attn.h"
 
+#include <cstdlib>
+
 namespace tdg {
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -43,14 +45,15 @@ struct ATile {
     return row * RB + (seg << 5) + (byte & 31);
   }
   // Stage 64 rows (row0..row0+63, rows >= nrows zero) of a [L, ...] tensor.
+  template <int NT = 256>
   __device__ static __forceinline__ void load(char* lds, const bf16_t* __restrict__ base,
                                               long long sl, int row0, int nrows, int tid) {
     constexpr int CPR = HD / 8;
     constexpr int TOTAL = 64 * CPR;
 #pragma unroll
-    for (int i = 0; i < (TOTAL + 255) / 256; ++i) {
-      const int id = tid + i * 256;
-      if (TOTAL % 256 != 0 && id >= TOTAL) break;
+    for (int i = 0; i < (TOTAL + NT - 1) / NT; ++i) {
+      const int id = tid + i * NT;
+      if (TOTAL % NT != 0 && id >= TOTAL) break;
       const int row = id / CPR, c = id % CPR;
       short8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
       if (row0 + row < nrows)
@@ -96,19 +99,22 @@ __device__ __forceinline__ short8_t gfrag(const bf16_t* __restrict__ rowp, bool 
 
 
 // ============================================================================ forward
-template <int HD>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+// NWV waves per workgroup, 16 query rows per wave (NWV = 8 covers a whole
+// <= 128-query sequence, so K/V are read from HBM once per (batch, head)).
+template <int HD, int NWV>
+__global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   using T = ATile<HD>;
+  constexpr int QBW = 16 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
   char* ldsV = smem + T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QB;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
   const int qrow = q0 + 16 * w + cl;
   const bool qvalid = qrow < a.Lq;
   int klim = a.Lk;
   if (a.kv_len) klim = min(klim, a.kv_len[b]);
-  if (a.causal) klim = min(klim, q0 + QB);
+  if (a.causal) klim = min(klim, q0 + QBW);
 
   const bf16_t* qp = a.q + b * a.q_sb + (long long)min(qrow, a.Lq - 1) * a.q_sl + h * a.q_sh;
   short8_t qf[T::KS];
@@ -125,8 +131,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
 
   for (int k0 = 0; k0 < klim; k0 += KB) {
-    T::load(ldsK, kb, a.k_sl, k0, a.Lk, tid);
-    T::load(ldsV, vb, a.v_sl, k0, a.Lk, tid);
+    T::template load<NWV * 64>(ldsK, kb, a.k_sl, k0, a.Lk, tid);
+    T::template load<NWV * 64>(ldsV, vb, a.v_sl, k0, a.Lk, tid);
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -383,6 +389,191 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ fused backward, short sequences
+// Lq, Lk <= 128: one workgroup (8 waves) per (batch, head) computes dQ, dK
+// and dV together, with delta = rowsum(dO*O) computed in the prologue.
+// Phase 1 (key rows on lanes, wave w owns keys 16w..16w+15): S^T and dP^T
+// from the Q / dO tiles in LDS and the wave's K / V fragments in registers,
+// P recomputed from the forward log-sum-exp, dS = P (dP - delta); dV^T and
+// dK^T accumulate over all queries. dS is then written as bf16 into the LDS
+// the Q / dO tiles used: a [key][query] image whose transposing read is
+// exactly the B-operand layout of phase 2. Phase 2 (query rows on lanes,
+// wave w owns queries 16w..16w+15): dQ^T = K^T dS^T.
+// Versus the three-kernel path (delta, dK/dV, dQ): every tile is read from
+// HBM once and there is one launch instead of three.
+template <int HD>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 4 : 2))) void attn_bwd_fused_kernel(AttnArgs a) {
+  using T = ATile<HD>;
+  using TS = ATile<128>;  // dS image: 128 key rows x 128 queries (bf16)
+  constexpr int R = 128;
+  constexpr int TB = R * T::RB;  // bytes of one 128-row tile image
+  constexpr int SB = R * TS::RB;  // dS image bytes (32 KiB)
+  constexpr int ALIAS = 2 * TB >= SB;  // dS fits over Q + dO
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ldsQ = smem;
+  char* ldsO = smem + TB;
+  char* ldsK = smem + 2 * TB;
+  char* ldsS = ALIAS ? smem : smem + 3 * TB;
+  float* ldsL = reinterpret_cast<float*>(smem + (ALIAS ? 3 * TB : 3 * TB + SB));
+  float* ldsD = ldsL + R;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  int klim = a.Lk;
+  if (a.kv_len) klim = min(klim, a.kv_len[b]);
+  const float c = a.scale * LOG2E;
+
+  // ---- prologue: Q, dO, K tiles -> LDS; lse, delta -> LDS
+  const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
+  const bf16_t* kbp = a.k + b * a.k_sb + h * a.k_sh;
+  {
+    constexpr int CPR = HD / 8;
+    constexpr int TOTAL = R * CPR;
+#pragma unroll
+    for (int i = 0; i < (TOTAL + 511) / 512; ++i) {
+      const int id = tid + i * 512;
+      if (TOTAL % 512 != 0 && id >= TOTAL) break;
+      const int row = id / CPR, cc = id % CPR;
+      short8_t vq = {0, 0, 0, 0, 0, 0, 0, 0}, vo = vq, vk = vq;
+      if (row < a.Lq) {
+        vq = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
+        vo = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
+      }
+      if (row < a.Lk) vk = *reinterpret_cast<const short8_t*>(kbp + (long long)row * a.k_sl + cc * 8);
+      *reinterpret_cast<short8_t*>(ldsQ + T::off(row, cc * 16)) = vq;
+      *reinterpret_cast<short8_t*>(ldsO + T::off(row, cc * 16)) = vo;
+      *reinterpret_cast<short8_t*>(ldsK + T::off(row, cc * 16)) = vk;
+    }
+    // delta[q] = sum_d dO[q][d] * O[q][d]: 4 threads per row
+    const int row = tid >> 2, part = tid & 3;
+    float d = 0.f;
+    if (row < a.Lq) {
+      const bf16_t* op = a.o + b * a.o_sb + (long long)row * a.o_sl + h * a.o_sh;
+      const bf16_t* dp = ob + (long long)row * a.do_sl;
+#pragma unroll
+      for (int e0 = part * 8; e0 < HD; e0 += 32) {
+        const short8_t x = *reinterpret_cast<const short8_t*>(op + e0);
+        const short8_t y = *reinterpret_cast<const short8_t*>(dp + e0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)x[e]) * bf2f((bf16_t)y[e]);
+      }
+    }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    if (part == 0) {
+      ldsD[row] = row < a.Lq ? d : 0.f;
+      ldsL[row] = row < a.Lq ? a.lse[((long long)b * a.H + h) * a.Lq + row] : INFINITY;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 1: this wave's 16 keys against all queries
+  const int key = 16 * w + cl;
+  const bool kvalid = key < klim;
+  const bool active = 16 * w < klim;  // wave-uniform
+  f32x4 dk[T::DT], dv[T::DT];
+#pragma unroll
+  for (int i = 0; i < T::DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // P and dS of [q = 16t + 4g + r][key], packed to bf16 pairs as produced
+  uint32_t pk[8][2], dk2[8][2];
+  if (active) {
+    short8_t kf[T::KS], vf[T::KS];
+    const int krow = min(key, a.Lk - 1);
+    const bf16_t* kp = kbp + (long long)krow * a.k_sl;
+    const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      kf[ks] = gfrag<HD>(kp, key < a.Lk, ks, lane);
+      vf[ks] = gfrag<HD>(vp, key < a.Lk, ks, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
+      const bool live = 16 * t < a.Lq && (!a.causal || 16 * t + 15 >= 16 * w);  // uniform
+      if (live) {
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          sv = mfma16(T::frag_row(ldsQ, 16 * t, ks, lane), kf[ks], sv);
+          dpv = mfma16(T::frag_row(ldsO, 16 * t, ks, lane), vf[ks], dpv);
+        }
+      }
+      float pv[4], dv4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 16 * t + 4 * g + r;
+        const bool ok = live && kvalid && q < a.Lq && (!a.causal || key <= q);
+        pv[r] = ok ? exp2f(sv[r] * c - ldsL[q]) : 0.f;
+        dv4[r] = pv[r] * (dpv[r] - ldsD[q]);
+      }
+      pk[t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
+      pk[t][1] = (uint32_t)f2bf(pv[2]) | ((uint32_t)f2bf(pv[3]) << 16);
+      dk2[t][0] = (uint32_t)f2bf(dv4[0]) | ((uint32_t)f2bf(dv4[1]) << 16);
+      dk2[t][1] = (uint32_t)f2bf(dv4[2]) | ((uint32_t)f2bf(dv4[3]) << 16);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      if (32 * s2 >= a.Lq) break;
+      const short8_t pf = __builtin_bit_cast(
+          short8_t, make_uint4(pk[2 * s2][0], pk[2 * s2][1], pk[2 * s2 + 1][0], pk[2 * s2 + 1][1]));
+      const short8_t dsf = __builtin_bit_cast(
+          short8_t, make_uint4(dk2[2 * s2][0], dk2[2 * s2][1], dk2[2 * s2 + 1][0], dk2[2 * s2 + 1][1]));
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) {
+        dv[dt] = mfma16(T::frag_tr(ldsO, s2, dt, lane), pf, dv[dt]);
+        dk[dt] = mfma16(T::frag_tr(ldsQ, s2, dt, lane), dsf, dk[dt]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) dk2[t][0] = dk2[t][1] = 0u;
+  }
+  __syncthreads();  // everyone done with Q / dO (the dS image aliases them)
+  // dS^T image: row = key, bytes (16t + 4g) * 2 .. +8 = queries 16t+4g .. +3
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    *reinterpret_cast<uint2*>(ldsS + TS::off(key, (16 * t + 4 * g) * 2)) = make_uint2(dk2[t][0], dk2[t][1]);
+  // dK, dV out (key rows on lanes)
+  if (key < a.Lk) {
+    bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key * a.dk_sl + h * a.dk_sh;
+    bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key * a.dv_sl + h * a.dv_sh;
+    const float sc = a.scale;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      uint32_t lo = (uint32_t)f2bf(dk[dt][0] * sc) | ((uint32_t)f2bf(dk[dt][1] * sc) << 16);
+      uint32_t hi = (uint32_t)f2bf(dk[dt][2] * sc) | ((uint32_t)f2bf(dk[dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+      lo = (uint32_t)f2bf(dv[dt][0]) | ((uint32_t)f2bf(dv[dt][1]) << 16);
+      hi = (uint32_t)f2bf(dv[dt][2]) | ((uint32_t)f2bf(dv[dt][3]) << 16);
+      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: dQ for queries 16w .. 16w+15 (query on lanes)
+  const int qrow = 16 * w + cl;
+  if (16 * w >= a.Lq) return;
+  f32x4 dq[T::DT];
+#pragma unroll
+  for (int i = 0; i < T::DT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    if (32 * s2 >= klim) break;
+    const short8_t dsf = TS::frag_tr(ldsS, s2, w, lane);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) dq[dt] = mfma16(T::frag_tr(ldsK, s2, dt, lane), dsf, dq[dt]);
+  }
+  if (qrow >= a.Lq) return;
+  bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow * a.dq_sl + h * a.dq_sh;
+  const float sc = a.scale;
+#pragma unroll
+  for (int dt = 0; dt < T::DT; ++dt) {
+    const uint32_t lo = (uint32_t)f2bf(dq[dt][0] * sc) | ((uint32_t)f2bf(dq[dt][1] * sc) << 16);
+    const uint32_t hi = (uint32_t)f2bf(dq[dt][2] * sc) | ((uint32_t)f2bf(dq[dt][3] * sc) << 16);
+    *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+  }
+}
+
 // ============================================================================ probabilities (inference maps)
 // One wave per (b, h, q) row: emits the full softmax row [Lk] in f32, the
 // attention_weights the reference returns (transformer_model.py:104-109,
@@ -431,14 +622,42 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 using namespace tdg;
 
 namespace {
+bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v != nullptr && v[0] != '\0' && v[0] != '0';
+}
+
 template <int HD>
 int fwd_hd(const AttnArgs& a, hipStream_t st) {
-  dim3 grid(cdiv(a.Lq, QB), a.H, a.B);
-  hipLaunchKernelGGL(attn_fwd_kernel<HD>, grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
+  if (a.Lq > 64) {
+    dim3 grid(cdiv(a.Lq, 128), a.H, a.B);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8>), grid, dim3(512), 2 * ATile<HD>::BYTES, st, a);
+  } else {
+    dim3 grid(cdiv(a.Lq, 64), a.H, a.B);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 4>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
+  }
   return 0;
 }
 template <int HD>
+constexpr int fused_bwd_lds() {
+  constexpr int TB = 128 * HD * 2, SB = 128 * 256;
+  return (2 * TB >= SB ? 3 * TB : 3 * TB + SB) + 2 * 128 * 4;
+}
+
+template <int HD>
 int bwd_hd(const AttnArgs& a, hipStream_t st) {
+  static const bool split_only = getenv_flag("TDG_ATTN_BWD_SPLIT");
+  if (a.Lq <= 128 && a.Lk <= 128 && !split_only) {
+    constexpr int lds = fused_bwd_lds<HD>();
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<HD>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(attn_bwd_fused_kernel<HD>, dim3(a.B * a.H), dim3(512), lds, st, a);
+    return 0;
+  }
   const long long rows = (long long)a.B * a.H * a.Lq;
   hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
                      a);

@@ -141,6 +141,16 @@ struct Glds {
   }
 };
 
+#ifndef TDG_GEMM_PRIO
+#define TDG_GEMM_PRIO 1
+#endif
+__device__ __forceinline__ void prio_hi() {
+  if (TDG_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void prio_lo() {
+  if (TDG_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -265,10 +275,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     for (int i = 0; i < TM; ++i) fa1[i] = frag<A_KC, BM>(st, abase + 16 * i, 1, lane);
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb1[j] = frag<B_KC, BN>(st + A_BYTES, bbase + 16 * j, 1, lane);
+    prio_hi();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+    prio_lo();
     if (kt + 1 < nk) {
       // tile kt+1 landed (this wave's DMA), then everyone's; everyone is done
       // reading tile kt (its fragments are in registers)
@@ -293,10 +305,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb0[j] = frag<B_KC, BN>(nx + A_BYTES, bbase + 16 * j, 0, lane);
     }
+    prio_hi();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
+    prio_lo();
   }
 
   // ---------------- epilogue (LDS-staged, 16-byte coalesced stores)

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Attention fwd / bwd timing on the Transformer-base shape (B=64, H=8,
+L=128, hd=64), HIP-graph replay of 20 calls (set TDG_ATTN_BWD_SPLIT=1 for
+the three-kernel backward)."""
+import os, sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+
+def graph_time(fn, n=20):
+    fn(); torch.cuda.synchronize()
+    s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay(); torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(); g.replay(); b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / n * 1e3
+
+B, H, L, hd = 64, 8, 128, 64
+for causal in (False, True):
+    q, k, v, do = (torch.randn(B, L, H, hd, device="cuda").bfloat16() for _ in range(4))
+    kv = torch.full((B,), L, dtype=torch.int32, device="cuda")
+    o, lse = kk.attn_fwd(q, k, v, kv, 0.125, causal)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    tf = graph_time(lambda: kk.attn_fwd(q, k, v, kv, 0.125, causal))
+    tb = graph_time(lambda: kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, causal))
+    print(f"causal={causal} split={os.environ.get('TDG_ATTN_BWD_SPLIT', '0')}: fwd {tf:.2f} us  bwd {tb:.2f} us", flush=True)
