@@ -346,7 +346,7 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
     TORCH_CHECK(dbias->numel() == D && ds.has_value(), "ln_bwd: dbias needs ds");
   }
   check_f32(ws, "ws");
-  TORCH_CHECK(ws.numel() >= 3 * ((M + 31) / 32) * D, "ln_bwd: workspace too small");
+  TORCH_CHECK(ws.numel() >= 3 * ((M + 7) / 8) * D, "ln_bwd: workspace too small");
   c10::DeviceGuard g(dy.device());
   const int rc = tdg_ln_bwd(
       dy.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),

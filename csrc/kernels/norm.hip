@@ -107,7 +107,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   // round h to bf16 first so that forward and backward see the same h
   if (hsave) {
     h.store_bf(hsave + base);
-    h.load_bf(hsave + base);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h.v[i] = bf2f(f2bf(h.v[i]));
   }
   float sum = 0.f;
 #pragma unroll
@@ -134,16 +135,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
-// rows_per_block rows per 256-thread block (4 waves); partial column sums to
-// part_g / part_b / part_s [gridDim.x, D].
-template <int D>
+// RPW rows per wave, 4 waves (4*RPW rows) per 256-thread block; all loads of
+// a wave's rows are issued before any of them is used (one memory latency per
+// wave instead of one per row). Partial column sums go to part_g / part_b /
+// part_s [gridDim.x, D].
+template <int D, int RPW>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const float* __restrict__ gamma, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ ds_out,
     const bf16_t* __restrict__ dres_in, float* __restrict__ part_g, float* __restrict__ part_b,
-    float* __restrict__ part_s, int M, int rows_per_block, float p, uint32_t thresh,
-    uint64_t seed, const long long* ctr, uint64_t site) {
+    float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
+    const long long* ctr, uint64_t site) {
   constexpr int VEC = D / 64;
   __shared__ float red[3][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -153,23 +156,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   float gm[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) gm[i] = gamma[lane * VEC + i];
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(M, r0 + rows_per_block);
+  const int r0 = blockIdx.x * (4 * RPW) + w * RPW;
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  for (int row = r0 + w; row < r1; row += 4) {
+  RowVec<VEC> g[RPW], h[RPW], e[RPW];
+  float mean[RPW], rstd[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int row = min(r0 + k, M - 1);
     const size_t base = (size_t)row * D + lane * VEC;
-    RowVec<VEC> g, h;
-    g.load_bf(dy + base);
-    h.load_bf(hsave + base);
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    g[k].load_bf(dy + base);
+    h[k].load_bf(hsave + base);
+    if (dres_in) e[k].load_bf(dres_in + base);
+    mean[k] = mean_in[row];
+    rstd[k] = rstd_in[row];
+  }
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int row = r0 + k;
+    if (row >= M) break;
+    const size_t base = (size_t)row * D + lane * VEC;
     float sg = 0.f, sgx = 0.f;
     float xh[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      xh[i] = (h.v[i] - mean) * rstd;
-      ag[i] += g.v[i] * xh[i];
-      ab[i] += g.v[i];
-      const float gg = g.v[i] * gm[i];
+      xh[i] = (h[k].v[i] - mean[k]) * rstd[k];
+      ag[i] += g[k].v[i] * xh[i];
+      ab[i] += g[k].v[i];
+      const float gg = g[k].v[i] * gm[i];
       sg += gg;
       sgx += gg * xh[i];
     }
@@ -177,7 +190,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     sgx = wave_sum(sgx) * (1.f / D);
     RowVec<VEC> dh;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) dh.v[i] = rstd * (g.v[i] * gm[i] - sg - xh[i] * sgx);
+    for (int i = 0; i < VEC; ++i) dh.v[i] = rstd[k] * (g[k].v[i] * gm[i] - sg - xh[i] * sgx);
     RowVec<VEC> ds = dh;
     if (p > 0.f) {
       const uint32_t km = keep_bits<VEC>(seed, ctr, site, base, thresh);
@@ -190,10 +203,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
     }
     if (dres_in) {  // fused accumulation of the residual branch's other gradient
-      RowVec<VEC> e;
-      e.load_bf(dres_in + base);
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) dh.v[i] += e.v[i];
+      for (int i = 0; i < VEC; ++i) dh.v[i] += e[k].v[i];
     }
     dh.store_bf(dh_out + base);
   }
@@ -238,14 +249,15 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
               int accumulate, hipStream_t st) {
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
-  const int rpb = 32;
+  constexpr int RPW = D >= 1024 ? 2 : 4;
+  const int rpb = 4 * RPW;
   const int nb = cdiv(M, rpb);
   float* pg = ws;
   float* pb = ws + (size_t)nb * D;
   float* ps = dbias ? ws + 2 * (size_t)nb * D : nullptr;
-  hipLaunchKernelGGL(ln_bwd_kernel<D>, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
+  hipLaunchKernelGGL((ln_bwd_kernel<D, RPW>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
-                     (const bf16_t*)dres, pg, pb, ps, M, rpb, p, thresh, seed, ctr, site);
+                     (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site);
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
   hipLaunchKernelGGL(reduce_partials3_kernel, dim3(cdiv(D, 64), dbias ? 3 : 2), dim3(256), 0, st,
@@ -265,7 +277,7 @@ extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, cons
   }
 }
 
-// ws must hold 3 * ceil(M/32) * D floats.
+// ws must hold 3 * ceil(M/8) * D floats.
 extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                           const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,

@@ -248,7 +248,7 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
     dh = torch.empty_like(dy)
     need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
     ds = torch.empty_like(dy) if need_ds else None
-    ws = workspace("ln_bwd", 3 * math.ceil(M / 32) * D, dy.device)
+    ws = workspace("ln_bwd", 3 * math.ceil(M / 8) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
                accumulate)
     if ds is None:
