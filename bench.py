@@ -48,6 +48,7 @@ def main() -> None:
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     args = ap.parse_args()
 
     info = tdist.init_distributed()
@@ -127,6 +128,9 @@ def main() -> None:
                 "last_loss": round(loss, 4),
             },
         }), flush=True)
+    if args.save_tuned and info.rank == 0:
+        from tensorflow_distributed_on_gke_amd.ops import kernels as _kk
+        _kk.save_tuned(args.save_tuned)
     tdist.shutdown()
 
 

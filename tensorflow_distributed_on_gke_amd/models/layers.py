@@ -40,6 +40,7 @@ import torch
 
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.ops.streams import offload
 from tensorflow_distributed_on_gke_amd.ops import philox
 
 LN_EPS = 1e-6
@@ -168,8 +169,11 @@ class EmbedFn(torch.autograd.Function):
         (tok,) = ctx.saved_tensors
         table, rt = ctx.table, ctx.rt
         if dout.is_cuda:
-            K.embed_bwd(tok, dout.contiguous(), table.grad, ctx.scale, rt.p, rt.seed, rt.ctr,
-                        ctx.site)
+            dc = dout.contiguous()
+            with offload(tok, dc):
+                K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site)
+                _ready(rt, table)
+            return None, None, None, None, None, None
         else:
             g = dout * ctx.ks if ctx.ks is not None else dout
             g = (g * ctx.scale).reshape(-1, table.shape[1])
@@ -252,15 +256,20 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ds2 = ds.reshape(M, d)
         q5 = qkv.view(B, L, 3, heads, hd)
         if dy.is_cuda:
-            K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
-            _ready(rt, wo)
+            with offload(ds2, o):
+                K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
+                _ready(rt, wo)
             do = K.linear_dgrad(ds2, wo.compute, d)
             dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
             g5 = dqkv.view(B, L, 3, heads, hd)
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
-            K.linear_wgrad(dqkv, x2, 3 * d, wqkv.grad, bt)
-            K.colsum(dqkv, 3 * d, bqkv.grad, bt)
+            with offload(dqkv, x2):
+                K.linear_wgrad(dqkv, x2, 3 * d, wqkv.grad, bt)
+                K.colsum(dqkv, 3 * d, bqkv.grad, bt)
+                _ready(rt, wqkv, bqkv)
+            dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
+            return (dx.view(B, L, d),) + (None,) * 11
         else:
             _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
             _ready(rt, wo)
@@ -305,9 +314,10 @@ class CrossKVFn(torch.autograd.Function):
         N = wkv.shape[0]
         bt = _beta(rt)
         if e2.is_cuda:
-            K.linear_wgrad(dkv, e2, N, wkv.grad, bt)
-            K.colsum(dkv, N, bkv.grad, bt)
-            _ready(rt, wkv, bkv)
+            with offload(dkv, e2):
+                K.linear_wgrad(dkv, e2, N, wkv.grad, bt)
+                K.colsum(dkv, N, bkv.grad, bt)
+                _ready(rt, wkv, bkv)
             denc = K.linear_dgrad(dkv, wkv.compute, N)
         else:
             _write_grad(wkv, dkv.t() @ e2, rt)
@@ -369,15 +379,18 @@ class CrossAttnBlockFn(torch.autograd.Function):
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:
-            K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
-            _ready(rt, wo)
+            with offload(ds2, o):
+                K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
+                _ready(rt, wo)
             do = K.linear_dgrad(ds2, wo.compute, d)
             dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
             K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
                        do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
                        g5[:, :, 1], kv_len, scale, False)
-            K.linear_wgrad(dq, x2, d, wq.grad, bt)
-            K.colsum(dq, d, bq.grad, bt)
+            with offload(dq, x2):
+                K.linear_wgrad(dq, x2, d, wq.grad, bt)
+                K.colsum(dq, d, bq.grad, bt)
+                _ready(rt, wq, bq)
         else:
             _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
             _ready(rt, wo)
@@ -429,11 +442,16 @@ class FFNBlockFn(torch.autograd.Function):
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
-            K.linear_wgrad(ds2, h, d, w2.grad, bt)
-            _ready(rt, w2)
+            with offload(ds2, h):
+                K.linear_wgrad(ds2, h, d, w2.grad, bt)
+                _ready(rt, w2)
             dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
-            K.linear_wgrad(dpre, x2, ff, w1.grad, bt)
-            K.colsum(dpre, ff, b1.grad, bt)
+            with offload(dpre, x2):
+                K.linear_wgrad(dpre, x2, ff, w1.grad, bt)
+                K.colsum(dpre, ff, b1.grad, bt)
+                _ready(rt, w1, b1)
+            dx = _dgrad_into(dpre, w1, ff, dh)
+            return (dx.view(B, L, d),) + (None,) * 8
         else:
             _write_grad(w2, ds2.t() @ h, rt)
             _ready(rt, w2)

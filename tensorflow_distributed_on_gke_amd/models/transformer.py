@@ -27,6 +27,7 @@ from tensorflow_distributed_on_gke_amd.models.params import (ParamStore, TFSlot,
                                                               glorot_blocks, glorot_uniform,
                                                               uniform)
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.ops.streams import join, offload
 
 PAD_ID = 0
 
@@ -288,11 +289,13 @@ class Transformer:
                 return step_out
             beta = 1.0 if rt.accumulate else 0.0
             dl = logits  # now holds dlogits (pad columns zeroed)
-            K.linear_wgrad(dl, dec2.contiguous(), cfg.tgt_vocab, self.final.w.grad, beta)
-            K.colsum(dl, cfg.tgt_vocab, self.final.b.grad, beta)
-            if rt.store is not None:
-                rt.store.grad_ready(self.final.w)
-                rt.store.grad_ready(self.final.b)
+            d2c = dec2.contiguous()
+            with offload(dl, d2c):  # off the critical path (ops/streams.py)
+                K.linear_wgrad(dl, d2c, cfg.tgt_vocab, self.final.w.grad, beta)
+                K.colsum(dl, cfg.tgt_vocab, self.final.b.grad, beta)
+                if rt.store is not None:
+                    rt.store.grad_ready(self.final.w)
+                    rt.store.grad_ready(self.final.b)
             ddec = K.linear_dgrad(dl, self.final.w.compute, cfg.tgt_vocab)
         else:
             lg = self.project(dec.detach())
@@ -329,4 +332,6 @@ class Transformer:
                 rt.store.grad_ready(fb)
             ddec = dl @ fw.master
         dec.backward(ddec.view(B, T, cfg.d_model).to(dec.dtype))
+        if dev.type == "cuda":
+            join(dev)  # weight gradients are final when this returns
         return step_out

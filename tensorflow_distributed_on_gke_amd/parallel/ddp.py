@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
+from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
 
 
 @dataclass
@@ -94,6 +95,12 @@ class DataParallel:
             b.work = None
 
     def _launch(self, b: Bucket) -> None:
+        # gradients come from both the compute stream and the weight-gradient
+        # side stream: collect on the side stream after it caught up
+        with on_side(self.store.flat_grad.device):
+            self._launch_now(b)
+
+    def _launch_now(self, b: Bucket) -> None:
         view = self.store.flat_grad[b.start:b.end]
         if self.comm_dtype is not None and self.comm_dtype != view.dtype:
             buf = self._comm_bufs.get(b.start)
@@ -114,6 +121,7 @@ class DataParallel:
     def finish(self) -> None:
         """Launch any bucket not yet reduced and make the current stream wait
         for all of them (device-side wait; no host sync)."""
+        join(self.store.flat_grad.device)
         if self.world <= 1:
             self.reset()
             return

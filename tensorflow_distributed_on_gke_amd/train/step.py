@@ -19,6 +19,7 @@ import torch
 from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
+from tensorflow_distributed_on_gke_amd.ops.streams import join
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 
@@ -45,6 +46,8 @@ class TrainStep:
                                      step_out=self.last)
         if self.ddp is not None:
             self.ddp.finish()
+        else:
+            join(self.model.device)  # weight gradients from the side stream
         self.opt.apply()
         return self.last
 
