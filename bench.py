@@ -46,6 +46,8 @@ def main() -> None:
     ap.add_argument("--local-batch", type=int, default=64)
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce dtype (bf16 halves xGMI bytes)")
     ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
@@ -59,7 +61,8 @@ def main() -> None:
     cfg = model_config(args.preset, max_src_len=max(1000, args.seq_len), max_tgt_len=max(1000, args.seq_len))
     model = Transformer(cfg).build(dev, seed=args.seed)
     opt = Adam(model.store, cfg.d_model)
-    ddp = DataParallel(model.store, bucket_mb=args.bucket_mb) if world > 1 else None
+    comm = torch.bfloat16 if args.grad_comm == "bf16" else None
+    ddp = DataParallel(model.store, bucket_mb=args.bucket_mb, comm_dtype=comm) if world > 1 else None
     if ddp is not None:
         ddp.broadcast_params(0)
     step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17)
@@ -116,7 +119,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
-            "data": "synthetic (random-init weights, synthetic pt/en token pairs, full-length 128)",
+            "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
                 "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "
                          f"heads={cfg.heads}, d_ff={cfg.d_ff}, vocab {cfg.src_vocab}/{cfg.tgt_vocab})",
@@ -125,6 +128,8 @@ def main() -> None:
                 "seq_len": S,
                 "parallelism": f"dp{world}",
                 "hip_graph": bool(use_graph),
+                "grad_comm": args.grad_comm,
+                "bucket_mb": args.bucket_mb,
                 "last_loss": round(loss, 4),
             },
         }), flush=True)

@@ -35,6 +35,9 @@ int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe
 int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, int M, int D,
                   float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
                   hipStream_t st);
+int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable, long long* acc,
+                      int M, int D, long long V, float scale, float p, uint64_t seed,
+                      const long long* ctr, uint64_t site, float beta, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
 int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64, const float* ntok,
              float workers, float smoothing, float* row_loss, float* row_correct, int write_grad,
@@ -398,6 +401,29 @@ void embed_bwd(const Tensor& tok, const Tensor& dout, const Tensor& dtable, doub
   check_err(rc, "tdg embed_bwd");
 }
 
+// Deterministic: acc is an all-zero int64 [V, D] scratch (left all-zero).
+void embed_bwd_det(const Tensor& tok, const Tensor& dout, const Tensor& dtable, const Tensor& acc,
+                   double scale, double p, int64_t seed, const optional<Tensor>& ctr, int64_t site,
+                   bool accumulate) {
+  TORCH_CHECK(tok.is_contiguous() && tok.is_cuda(), "tok");
+  const bool t64 = tok.scalar_type() == at::kLong;
+  TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
+  check_bf16(dout, "dout");
+  check_contig(dout, "dout");
+  check_f32(dtable, "dtable");
+  check_contig(dtable, "dtable");
+  TORCH_CHECK(acc.scalar_type() == at::kLong && acc.is_cuda() && acc.is_contiguous(), "acc int64");
+  TORCH_CHECK(acc.numel() >= dtable.numel(), "acc too small");
+  const int64_t D = dtable.size(1), M = tok.numel(), V = dtable.size(0);
+  TORCH_CHECK(dout.numel() == M * D, "dout shape");
+  c10::DeviceGuard g(tok.device());
+  const int rc = tdg_embed_bwd_det(tok.data_ptr(), t64, dout.data_ptr(), dtable.data_ptr<float>(),
+                                   reinterpret_cast<long long*>(acc.data_ptr<int64_t>()), (int)M, (int)D, (long long)V,
+                                   (float)scale, (float)p, (uint64_t)seed, ctr_ptr(ctr),
+                                   (uint64_t)site, accumulate ? 1.f : 0.f, stream_of(tok));
+  check_err(rc, "tdg embed_bwd_det");
+}
+
 // ---------------------------------------------------------------- loss
 void count_tokens(const Tensor& labels, const Tensor& out) {
   TORCH_CHECK(labels.is_contiguous() && labels.is_cuda(), "labels");
@@ -497,6 +523,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd_det", &embed_bwd_det);
   m.def("count_tokens", &count_tokens);
   m.def("xent", &xent);
   m.def("xent_stats", &xent_stats);

@@ -8,6 +8,8 @@
 // stays L2-resident.
 #include "tdg_common.h"
 
+#include <algorithm>
+
 namespace tdg {
 
 // out[row, :] = drop(table[tok[row]] * scale + pe[row % L])
@@ -64,6 +66,61 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
   }
 }
 
+// Deterministic variant: contributions are added as 2^-32 fixed-point int64,
+// so the sum is independent of the order the atomics land in (integer
+// addition is associative); embed_acc_convert turns the accumulator into the
+// f32 gradient and re-zeroes it. Resolution 2.3e-10, range +-2^31.
+constexpr float FX_SCALE = 4294967296.f;  // 2^32
+
+template <int D, typename TT>
+__global__ __launch_bounds__(256) void embed_bwd_fx_kernel(
+    const TT* __restrict__ tok, const bf16_t* __restrict__ dout, unsigned long long* __restrict__ acc,
+    int M, float scale, float p, uint32_t thresh, uint64_t seed, const long long* ctr,
+    uint64_t site) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const long long t = (long long)tok[row];
+  const size_t rbase = (size_t)row * D;
+  const float sc = p > 0.f ? scale / (1.f - p) : scale;
+#pragma unroll
+  for (int c = 0; c < D / 64; ++c) {
+    const int col = c * 64 + lane;
+    float g = bf2f(dout[rbase + col]) * sc;
+    if (p > 0.f && !dropout_keep(seed, ctr, site, rbase + col, thresh)) g = 0.f;
+    const long long fx = (long long)rintf(g * FX_SCALE);
+    if (fx != 0) atomicAdd(acc + t * D + col, (unsigned long long)fx);
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_acc_convert_kernel(long long* __restrict__ acc,
+                                                                float* __restrict__ out,
+                                                                long long n, float beta) {
+  const long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  for (long long i = i0; i < n; i += (long long)gridDim.x * blockDim.x * 2) {
+    if (i + 1 < n) {
+      const long long a0 = acc[i], a1 = acc[i + 1];
+      float2 o;
+      if (beta != 0.f) {
+        o = *reinterpret_cast<float2*>(out + i);
+        o.x = beta * o.x + (float)a0 * (1.f / FX_SCALE);
+        o.y = beta * o.y + (float)a1 * (1.f / FX_SCALE);
+      } else {
+        o = make_float2((float)a0 * (1.f / FX_SCALE), (float)a1 * (1.f / FX_SCALE));
+      }
+      *reinterpret_cast<float2*>(out + i) = o;
+      if (a0 != 0 || a1 != 0) {
+        acc[i] = 0;
+        acc[i + 1] = 0;
+      }
+    } else {
+      const float v = (float)acc[i] * (1.f / FX_SCALE);
+      out[i] = beta != 0.f ? beta * out[i] + v : v;
+      acc[i] = 0;
+    }
+  }
+}
+
 }  // namespace tdg
 
 using namespace tdg;
@@ -83,6 +140,13 @@ void bwd_d(const void* tok, const void* dout, float* dtable, int M, float scale,
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
   hipLaunchKernelGGL((embed_bwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
                      (const TT*)tok, (const bf16_t*)dout, dtable, M, scale, p, thresh, seed, ctr, site);
+}
+template <int D, typename TT>
+void bwd_fx_d(const void* tok, const void* dout, unsigned long long* acc, int M, float scale, float p,
+              uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
+  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  hipLaunchKernelGGL((embed_bwd_fx_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
+                     (const TT*)tok, (const bf16_t*)dout, acc, M, scale, p, thresh, seed, ctr, site);
 }
 }  // namespace
 
@@ -113,4 +177,34 @@ extern "C" int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float
   } else {
     TDG_D_SWITCH(bwd_d, int, tok, dout, dtable, M, scale, p, seed, ctr, site, st)
   }
+}
+
+// Deterministic embedding backward: fixed-point accumulation into acc
+// ([V, D] int64, all-zero on entry and on exit), then dtable = beta*dtable + acc.
+extern "C" int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable,
+                                 long long* acc, int M, int D, long long V, float scale, float p,
+                                 uint64_t seed, const long long* ctr, uint64_t site, float beta,
+                                 hipStream_t st) {
+  unsigned long long* a = reinterpret_cast<unsigned long long*>(acc);
+  int rc = -1;
+  if (tok64) {
+    switch (D) {
+      case 128: bwd_fx_d<128, long long>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 256: bwd_fx_d<256, long long>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 512: bwd_fx_d<512, long long>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 1024: bwd_fx_d<1024, long long>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+    }
+  } else {
+    switch (D) {
+      case 128: bwd_fx_d<128, int>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 256: bwd_fx_d<256, int>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 512: bwd_fx_d<512, int>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+      case 1024: bwd_fx_d<1024, int>(tok, dout, a, M, scale, p, seed, ctr, site, st); rc = 0; break;
+    }
+  }
+  if (rc) return rc;
+  const long long n = V * D;
+  const int blocks = (int)std::min<long long>(4096, (n / 2 + 255) / 256 + 1);
+  hipLaunchKernelGGL(embed_acc_convert_kernel, dim3(blocks), dim3(256), 0, st, acc, dtable, n, beta);
+  return 0;
 }

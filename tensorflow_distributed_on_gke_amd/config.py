@@ -68,6 +68,7 @@ class Settings:
     # --- runtime
     dtype: str = "bf16"
     bucket_mb: float = 64.0
+    grad_comm_dtype: str = "fp32"  # fp32 | bf16 (gradient all-reduce payload)
     hip_graph: bool = False
     idle_after_train: bool = False  # reference __main__.py:183-186 keeps the pod alive
     check_replicas_every: int = 0  # debug: assert bitwise-identical replicas every N steps

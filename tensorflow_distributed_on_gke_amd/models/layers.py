@@ -171,7 +171,8 @@ class EmbedFn(torch.autograd.Function):
         if dout.is_cuda:
             dc = dout.contiguous()
             with offload(tok, dc):
-                K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site)
+                K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site,
+                            accumulate=rt.accumulate)
                 _ready(rt, table)
             return None, None, None, None, None, None
         else:

@@ -22,7 +22,7 @@ NUM_CU = 256
 _WS: Dict[Tuple[int, int, str], torch.Tensor] = {}
 
 
-def workspace(name: str, numel: int, device, dtype=torch.float32) -> torch.Tensor:
+def workspace(name: str, numel: int, device, dtype=torch.float32, zero: bool = False) -> torch.Tensor:
     """Named scratch buffer, one per (device, stream): a buffer is only ever
     used by kernels of one stream, so growing it (which frees the old one to
     the caching allocator, in that stream's pool) cannot race a kernel of
@@ -32,7 +32,7 @@ def workspace(name: str, numel: int, device, dtype=torch.float32) -> torch.Tenso
     key = (dev.index or 0, sid, name)
     t = _WS.get(key)
     if t is None or t.numel() < numel or t.dtype != dtype:
-        t = torch.empty(max(numel, 1), dtype=dtype, device=dev)
+        t = (torch.zeros if zero else torch.empty)(max(numel, 1), dtype=dtype, device=dev)
         _WS[key] = t
     return t
 
@@ -309,8 +309,18 @@ def embed_fwd(tok, table, pe, scale, p, seed, ctr, site):
     return out
 
 
-def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site):
-    C().embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site)
+DETERMINISTIC_EMBED = os.environ.get("TDG_DETERMINISTIC", "1") != "0"
+
+
+def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False):
+    """dtable (=|+=) scatter-add of the embedding gradient. Default: the
+    deterministic fixed-point path (bitwise reproducible); TDG_DETERMINISTIC=0
+    uses plain f32 atomics (dtable must then be zero unless accumulating)."""
+    if DETERMINISTIC_EMBED:
+        acc = workspace("embed_fx", dtable.numel(), dtable.device, torch.int64, zero=True)
+        C().embed_bwd_det(tok, dout, dtable, acc, scale, p, seed, ctr, site, accumulate)
+    else:
+        C().embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site)
 
 
 def count_tokens(labels, out):

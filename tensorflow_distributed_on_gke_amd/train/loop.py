@@ -86,7 +86,9 @@ class Trainer:
         self.model = build_model(s, info.device)
         self.opt = Adam(self.model.store, self.model.cfg.d_model, warmup=s.warmup_steps, beta1=s.beta1,
                         beta2=s.beta2, eps=s.epsilon, lr=s.learning_rate)
-        self.ddp = DataParallel(self.model.store, bucket_mb=s.bucket_mb) if info.world > 1 else None
+        comm = torch.bfloat16 if s.grad_comm_dtype == "bf16" else None
+        self.ddp = (DataParallel(self.model.store, bucket_mb=s.bucket_mb, comm_dtype=comm)
+                    if info.world > 1 else None)
         self.step_fn = TrainStep(self.model, self.opt, self.ddp, workers=info.world, seed=s.seed + 17)
         self.train_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab, s.tgt_vocab,
                                          seed=s.seed, rank=info.rank, world=info.world, min_len=s.min_len,

@@ -227,6 +227,12 @@ def test_embed_fwd_bwd(p):
     kk.embed_bwd(tok.to(DEV), dout.to(DEV), dt, math.sqrt(D), p, 77, ctr.to(DEV), 2)
     refg = torch.zeros(V, D).index_add_(0, tok.view(-1), (dout.float() * ks * math.sqrt(D)).view(-1, D))
     _close(dt, refg, 1e-4, "embed bwd")
+    # deterministic path: bitwise identical across calls (and accumulate mode)
+    dt2 = torch.full((V, D), 7.0, device=DEV)
+    kk.embed_bwd(tok.to(DEV), dout.to(DEV), dt2, math.sqrt(D), p, 77, ctr.to(DEV), 2)
+    assert torch.equal(dt, dt2)
+    kk.embed_bwd(tok.to(DEV), dout.to(DEV), dt2, math.sqrt(D), p, 77, ctr.to(DEV), 2, accumulate=True)
+    _close(dt2, 2 * refg, 1e-4, "embed bwd accumulate")
 
 
 # --------------------------------------------------------------------------- cross-entropy

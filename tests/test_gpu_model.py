@@ -71,3 +71,22 @@ def test_gpu_training_reduces_loss():
         opt.apply()
         losses.append(out[0].item())
     assert losses[-1] < 0.75 * losses[0], losses[::20]
+
+
+def test_gpu_backward_bitwise_deterministic():
+    """Same weights, batch and dropout stream -> bitwise-identical gradients
+    (no order-dependent atomics anywhere in backward)."""
+    cfg = model_config("tiny", src_vocab=300, tgt_vocab=250, dropout=0.1)
+    m = Transformer(cfg).build("cuda", seed=3)
+    src, tgt = _batch(8, 40, 33, cfg.src_vocab, cfg.tgt_vocab, seed=9)
+    src, tgt = src.cuda(), tgt.cuda()
+    grads = []
+    for _ in range(3):
+        rt = RunCtx(training=True, dropout=0.1, seed=5, ctr=torch.tensor([4], dtype=torch.int64, device="cuda"),
+                    store=m.store)
+        m.store.flat_grad.zero_()
+        out = m.loss_and_backward(src, tgt, rt, workers=1.0)
+        torch.cuda.synchronize()
+        grads.append((out.clone(), m.store.flat_grad.clone()))
+    assert torch.equal(grads[1][0], grads[2][0])
+    assert torch.equal(grads[1][1], grads[2][1])

@@ -40,7 +40,7 @@ def _data(rank, world):
     return SyntheticPairs(4, 10, 11, 60, 50, seed=3, rank=rank, world=world, min_len=3)
 
 
-def _worker(rank, world, port, out, bucket_mb):
+def _worker(rank, world, port, out, bucket_mb, comm=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
@@ -50,7 +50,7 @@ def _worker(rank, world, port, out, bucket_mb):
     info = tdist.init_distributed("cpu")
     m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=1 + rank)  # ranks differ until broadcast
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
-    ddp = DataParallel(m.store, bucket_mb=bucket_mb)
+    ddp = DataParallel(m.store, bucket_mb=bucket_mb, comm_dtype=comm)
     ddp.broadcast_params(0)
     step = TrainStep(m, opt, ddp, workers=world, seed=5)
     data = _data(rank, world)
@@ -107,6 +107,21 @@ def test_dp2_matches_single_process(tmp_path, bucket_mb):
     assert not torch.equal(r0["flat"], Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat)
     assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
     assert torch.allclose(r0["loss"], ref_loss, atol=1e-6)
+
+
+def test_dp2_bf16_gradient_comm(tmp_path):
+    world = 2
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, _free_port(), out, 0.05, torch.bfloat16), nprocs=world,
+                       join=True, start_method="spawn")
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    assert torch.equal(r0["flat"], r1["flat"])
+    ref_flat, _ = _single_process_reference(world)
+    init = Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat
+    # bf16 gradients: the update matches the f32 one to bf16 precision
+    rel = (r0["flat"] - ref_flat).norm() / (ref_flat - init).norm()
+    assert rel < 2e-2, rel
 
 
 def test_plan_buckets_cover_flat_buffer():

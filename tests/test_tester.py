@@ -44,6 +44,12 @@ def _check(dev, tol=0.0):
         n = single.shape[1]
         if tol == 0.0:
             assert torch.equal(single[0], out[i, :n].cpu())
+    # KV-cache incremental decode == full re-forward decode
+    src_t = tester.src_tok.tokenize(sents)
+    full = tester.greedy(src_t, max_length=12).cpu()
+    cached = tester.greedy_cached(src_t, max_length=12).cpu()
+    n = min(full.shape[1], cached.shape[1])
+    assert (full[:, :n] != cached[:, :n]).float().mean().item() <= tol
     text, tokens, attn = tester(sents[0], max_length=8)
     assert isinstance(text, str) and tokens[0] == "[START]"
     L = len(tokens) - 1 if tokens[-1] != "[END]" else len(tokens) - 1
