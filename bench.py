@@ -50,6 +50,8 @@ def main() -> None:
                     help="gradient all-reduce dtype (bf16 halves xGMI bytes)")
     ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: FFN forward GEMMs in e4m3 with delayed scaling (BASELINE config 5)")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     args = ap.parse_args()
 
@@ -65,7 +67,11 @@ def main() -> None:
     ddp = DataParallel(model.store, bucket_mb=args.bucket_mb, comm_dtype=comm) if world > 1 else None
     if ddp is not None:
         ddp.broadcast_params(0)
-    step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17)
+    fp8_state = None
+    if args.dtype == "fp8":
+        from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
+        fp8_state = Fp8State(model)
+    step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17, fp8_state=fp8_state)
 
     S = T = args.seq_len
     data = SyntheticPairs(batch=args.local_batch, src_len=S, tgt_len=T + 1, src_vocab=cfg.src_vocab,
@@ -118,7 +124,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if args.dtype == "bf16" else "fp8 (e4m3 FFN forward GEMMs, bf16 elsewhere)",
             "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
                 "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "

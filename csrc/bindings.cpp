@@ -24,7 +24,8 @@ int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
-               const long long* ctr, uint64_t site, float eps, hipStream_t st);
+               const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
+               unsigned* amax8, hipStream_t st);
 int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
@@ -39,6 +40,13 @@ int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtabl
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
+int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
+                 const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
+                 int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
+int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale, unsigned* amax,
+                  hipStream_t st);
+int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2, hipStream_t st);
+int tdg_fp8_dequant(const void* x8, float* y, long long n, float inv_scale, hipStream_t st);
 int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64, const float* ntok,
              float workers, float smoothing, float* row_loss, float* row_correct, int write_grad,
              hipStream_t st);
@@ -274,6 +282,16 @@ void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
             "tdg attn_probs");
 }
 
+void check_f8(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.element_size() == 1, n, " must be a 1-byte (fp8 e4m3) GPU tensor");
+}
+unsigned* amax_ptr(const optional<Tensor>& t) {
+  if (!t.has_value()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->element_size() == 4 && t->numel() >= 64,
+              "amax must be a 64-word GPU tensor (one fp8 slot)");
+  return reinterpret_cast<unsigned*>(t->data_ptr());
+}
+
 // ---------------------------------------------------------------- layernorm
 const long long* ctr_ptr(const optional<Tensor>& c) {
   if (!c.has_value()) return nullptr;
@@ -285,7 +303,8 @@ const long long* ctr_ptr(const optional<Tensor>& c) {
 void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, const Tensor& beta,
             const Tensor& y, const optional<Tensor>& hsave, const optional<Tensor>& mean,
             const optional<Tensor>& rstd, double p, int64_t seed, const optional<Tensor>& ctr,
-            int64_t site, double eps) {
+            int64_t site, double eps, const optional<Tensor>& y8, const optional<Tensor>& s8,
+            const optional<Tensor>& amax8) {
   check_bf16(x, "x");
   check_contig(x, "x");
   const int64_t D = x.size(-1), M = x.numel() / D;
@@ -309,6 +328,11 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
       check_f32(**t, "mean/rstd");
       TORCH_CHECK((*t)->numel() == M, "ln: mean/rstd shape");
     }
+  if (y8.has_value()) {
+    check_f8(*y8, "y8");
+    TORCH_CHECK(y8->numel() == x.numel() && y8->is_contiguous() && s8.has_value(), "ln: y8");
+    check_f32(*s8, "s8");
+  }
   c10::DeviceGuard g(x.device());
   const int rc = tdg_ln_fwd(x.data_ptr(), s.has_value() ? s->data_ptr() : nullptr,
                             gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
@@ -316,7 +340,8 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
                             mean.has_value() ? mean->data_ptr<float>() : nullptr,
                             rstd.has_value() ? rstd->data_ptr<float>() : nullptr, (int)M, (int)D,
                             (float)p, (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, (float)eps,
-                            stream_of(x));
+                            y8 ? y8->data_ptr() : nullptr, s8 ? s8->data_ptr<float>() : nullptr,
+                            amax_ptr(amax8), stream_of(x));
   check_err(rc, "tdg ln_fwd");
 }
 
@@ -424,6 +449,65 @@ void embed_bwd_det(const Tensor& tok, const Tensor& dout, const Tensor& dtable, 
   check_err(rc, "tdg embed_bwd_det");
 }
 
+// ---------------------------------------------------------------- fp8
+void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
+              const Tensor& sa, const Tensor& sb, const optional<Tensor>& C8,
+              const optional<Tensor>& sc8, const optional<Tensor>& amax, int64_t M, int64_t N,
+              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldc8, int64_t epi,
+              int64_t cfg) {
+  check_f8(A, "A8");
+  check_f8(B, "B8");
+  check_bf16(C, "C");
+  check_f32(sa, "sa");
+  check_f32(sb, "sb");
+  TORCH_CHECK(K % 128 == 0 && lda % 16 == 0 && ldb % 16 == 0, "gemm_fp8: K % 128, ld % 16");
+  TORCH_CHECK(A.numel() >= (M - 1) * lda + K && B.numel() >= (N - 1) * ldb + K, "gemm_fp8: A/B extent");
+  TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc % 8 == 0, "gemm_fp8: C extent / ldc");
+  if (bias.has_value()) check_f32(*bias, "bias");
+  TORCH_CHECK(epi == 0 || bias.has_value(), "gemm_fp8: epilogue needs bias");
+  if (C8.has_value()) {
+    check_f8(*C8, "C8");
+    TORCH_CHECK(sc8.has_value() && C8->numel() >= (M - 1) * ldc8 + N && ldc8 % 8 == 0, "gemm_fp8: C8");
+  }
+  c10::DeviceGuard g(A.device());
+  const int rc = tdg_gemm_fp8(A.data_ptr(), B.data_ptr(), C.data_ptr(),
+                              bias ? bias->data_ptr<float>() : nullptr, sa.data_ptr<float>(),
+                              sb.data_ptr<float>(), C8 ? C8->data_ptr() : nullptr,
+                              sc8 ? sc8->data_ptr<float>() : nullptr, amax_ptr(amax), (int)M,
+                              (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)ldc8, (int)epi,
+                              (int)cfg, stream_of(A));
+  check_err(rc, "tdg gemm_fp8");
+}
+
+void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
+               const optional<Tensor>& amax) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  check_f8(y8, "y8");
+  TORCH_CHECK(y8.numel() >= x.numel() && y8.is_contiguous(), "fp8_quant: y8");
+  check_f32(scale, "scale");
+  c10::DeviceGuard g(x.device());
+  check_err(tdg_fp8_quant(x.data_ptr(), y8.data_ptr(), x.numel(), scale.data_ptr<float>(),
+                          amax_ptr(amax), stream_of(x)), "tdg fp8_quant");
+}
+
+void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow2) {
+  check_f32(scale, "scale");
+  TORCH_CHECK(amax.numel() == 64 * scale.numel(), "fp8_scale_update: amax is [n, 64]");
+  c10::DeviceGuard g(scale.device());
+  check_err(tdg_fp8_scale_update(scale.data_ptr<float>(), amax_ptr(amax), (int)scale.numel(),
+                                 (float)margin_pow2, stream_of(scale)), "tdg fp8_scale_update");
+}
+
+void fp8_dequant(const Tensor& x8, const Tensor& y, double inv_scale) {
+  check_f8(x8, "x8");
+  check_f32(y, "y");
+  TORCH_CHECK(y.numel() == x8.numel(), "fp8_dequant: sizes");
+  c10::DeviceGuard g(x8.device());
+  check_err(tdg_fp8_dequant(x8.data_ptr(), y.data_ptr<float>(), x8.numel(), (float)inv_scale,
+                            stream_of(x8)), "tdg fp8_dequant");
+}
+
 // ---------------------------------------------------------------- loss
 void count_tokens(const Tensor& labels, const Tensor& out) {
   TORCH_CHECK(labels.is_contiguous() && labels.is_cuda(), "labels");
@@ -515,6 +599,10 @@ void to_bf16(const Tensor& p, const Tensor& o) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
+  m.def("gemm_fp8", &gemm_fp8);
+  m.def("fp8_quant", &fp8_quant);
+  m.def("fp8_scale_update", &fp8_scale_update);
+  m.def("fp8_dequant", &fp8_dequant);
   m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

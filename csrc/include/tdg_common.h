@@ -142,6 +142,21 @@ __device__ __forceinline__ short8_t pack8(float a0, float a1, float a2, float a3
 // XCD-aware bijective block remap (blocks b and b+8 share an XCD under the
 // observed round-robin dispatch): give each XCD a contiguous chunk of tiles so
 // neighbouring tiles share that XCD's L2. Speed-only; any placement is correct.
+// OCP e4m3 (gfx950 native fp8): saturating pack of two floats into the low
+// (HI=false) or high 16 bits of `old`; amax as the bit pattern of |v| (non-
+// negative floats order like their bits), spread over AMAX_SPREAD words.
+constexpr float E4M3_MAX = 448.f;
+constexpr int AMAX_SPREAD = 64;
+template <bool HI>
+__device__ __forceinline__ int pack2_e4m3(float a, float b, int old) {
+  a = fminf(fmaxf(a, -E4M3_MAX), E4M3_MAX);
+  b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+}
+__device__ __forceinline__ void atomic_amax(unsigned* p, float v) {
+  atomicMax(p, __float_as_uint(fabsf(v)));
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   constexpr int NX = 8;
   if (nwg <= NX) return bid;

@@ -1,0 +1,401 @@
+// FP8 (OCP e4m3) forward GEMM and quantization for gfx950.
+//
+//   C[m,n] = act( (sum_k A8[m,k] * B8[n,k]) / (sa * sb) + bias[n] )      (bf16 out)
+//   optional C8 = e4m3(C * sc8), amax(C) -> amax_out   (fp8 copy for the next GEMM)
+//
+// A8 = e4m3(A * sa) and B8 = e4m3(B * sb) are per-tensor scaled copies of the
+// bf16 activations / weights; the scales live in device memory (delayed
+// scaling: each producer records the amax of what it quantised, and
+// fp8_scale_update turns last step's amax into this step's scale), so a
+// captured HIP graph stays valid across steps.
+//
+// MFMA: v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 block scales -- the
+// per-tensor scales are applied in the epilogue. Lane l holds
+// A[row l&15][k 32(l>>4) .. +31] and B[k 32(l>>4) .. +31][col l&15] (verified
+// with exact integer data: scripts/probes/fp8_mfma_layout.hip); C/D layout as
+// every 16x16 MFMA on gfx950 (col l&15, row 4(l>>4)+r). One instruction per
+// 128-deep K tile = twice the bf16 16x16x32 rate per clock, and half the bytes
+// staged through LDS.
+//
+// Staging is the bf16 kernel's (csrc/kernels/gemm.hip): LDS-DMA
+// (global_load_lds_dwordx4) into 128-byte-row images with the same 32-byte
+// XOR swizzle, STAGES tiles in flight, counted vmcnt + raw s_barrier.
+//
+// Replaces (in the fp8 configuration, BASELINE config 5) the forward Dense
+// MatMuls of the reference (distributed_training_transformer/
+// transformer_model.py:119-122, 165, 172-174); backward stays bf16.
+#include "tdg_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace tdg {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// E4M3_MAX, AMAX_SPREAD, pack2_e4m3, atomic_amax: tdg_common.h (each amax slot
+// is AMAX_SPREAD words; producers pick one by block id so the atomics of a
+// large grid do not serialise on one address)
+constexpr int BK8 = 128;  // K elements (= bytes) per tile row
+
+namespace f8 {
+
+__device__ __forceinline__ int lds_off(int row, int byte) {
+  const int seg = (byte >> 5) ^ ((row >> 1) & 3);
+  return row * BK8 + (seg << 5) + (byte & 31);
+}
+
+// global -> LDS staging of an R x 128-byte K-contiguous tile (as Glds<KC> in gemm.hip)
+template <int R, int NW>
+struct Stage {
+  static constexpr int BYTES = R * BK8;
+  static constexpr int P = BYTES / (NW * 1024);
+  static_assert(BYTES % (NW * 1024) == 0, "tile must split into 1 KiB pieces per wave");
+  int row[P], col[P];
+  __device__ __forceinline__ void init(int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int j = wid * P + i;
+      const int r = j * 8 + lane / 8;
+      const int pc = lane % 8;
+      const int c = (((pc >> 1) ^ ((r >> 1) & 3)) << 1) | (pc & 1);
+      row[i] = r;
+      col[i] = c * 16;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ X, int ld, int len, int mn0,
+                                        int k0, char* lds, int wid) const {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      int mn = mn0 + row[i];
+      mn = mn < len ? mn : len - 1;
+      const long long off = (long long)mn * ld + k0 + col[i];
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(X + off),
+          (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// 32-byte operand fragment: row base + (lane&15), bytes 32(lane>>4) .. +31
+__device__ __forceinline__ i32x8 frag(const char* lds, int base, int lane) {
+  const int row = base + (lane & 15);
+  const int g = lane >> 4;
+  const int4 lo = *reinterpret_cast<const int4*>(lds + lds_off(row, 32 * g));
+  const int4 hi = *reinterpret_cast<const int4*>(lds + lds_off(row, 32 * g + 16));
+  return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+using tdg::atomic_amax;
+using tdg::pack2_e4m3;
+
+}  // namespace f8
+
+enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2 };
+
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
+    uint8_t* __restrict__ C8, const float* __restrict__ sc8, unsigned* __restrict__ amax_out,
+    int M, int N, int K, int lda, int ldb, int ldc, int ldc8) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_BYTES = BM * BK8, B_BYTES = BN * BK8, SB = A_BYTES + B_BYTES;
+  using GA = f8::Stage<BM, NW>;
+  using GB = f8::Stage<BN, NW>;
+  constexpr int PT = GA::P + GB::P;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / BK8;  // host guarantees K % 128 == 0
+
+  GA ga;
+  GB gb;
+  ga.init(wid, lane);
+  gb.init(wid, lane);
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES; ++s)
+    if (s < nk) {
+      ga.issue(A, lda, M, m0, s * BK8, smem + s * SB, wid);
+      gb.issue(B, ldb, N, n0, s * BK8, smem + s * SB + A_BYTES, wid);
+    }
+  if (nk >= STAGES) f8::wait_vmcnt<(STAGES - 1) * PT>();
+  else f8::wait_vmcnt<0>();
+  f8::lds_barrier();
+  const int abase = wm * (BM / WM), bbase = wn * (BN / WN);
+  i32x8 fa[TM], fb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa[i] = f8::frag(smem, abase + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb[j] = f8::frag(smem + A_BYTES, bbase + 16 * j, lane);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0,
+                                                                     0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
+    if (kt + 1 < nk) {
+      if (kt + STAGES - 1 < nk) f8::wait_vmcnt<(STAGES - 2) * PT>();
+      else f8::wait_vmcnt<0>();
+      f8::lds_barrier();
+      if (kt + STAGES < nk) {
+        char* ns = smem + (kt % STAGES) * SB;
+        ga.issue(A, lda, M, m0, (kt + STAGES) * BK8, ns, wid);
+        gb.issue(B, ldb, N, n0, (kt + STAGES) * BK8, ns + A_BYTES, wid);
+      }
+      const char* nx = smem + ((kt + 1) % STAGES) * SB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = f8::frag(nx, abase + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = f8::frag(nx + A_BYTES, bbase + 16 * j, lane);
+    }
+  }
+
+  // ---------------- epilogue: dequant, bias, relu -> bf16 LDS image -> 16-byte stores
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int SROW = WTN * 2 + 16;
+  constexpr int CPR = WTN / 8;
+  const float alpha = 1.f / (sa[0] * sb[0]);
+  const float s8 = C8 ? sc8[0] : 0.f;
+  f8::lds_barrier();
+  char* wimg = smem + wid * (WTM * SROW);
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + 16 * j + cl;
+    float bn = 0.f;
+    if constexpr (EPI != F8_EPI_NONE) bn = bias[n < N ? n : N - 1];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = alpha * acc[i][j][r] + bn;
+        if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+        *reinterpret_cast<bf16_t*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * 2) = f2bf(v);
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float amax = 0.f;
+#pragma unroll
+  for (int tt = 0; tt < (WTM * CPR) / 64; ++tt) {
+    const int id = lane + 64 * tt;
+    const int row = id / CPR, ch = id % CPR;
+    const int m = m0 + wm * WTM + row;
+    const int n = n0 + wn * WTN + ch * 8;
+    if (m >= M || n >= N) continue;
+    const short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
+    if (n + 8 <= N) {
+      *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
+    }
+    if (C8) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = bf2f((bf16_t)v[e]);
+        amax = fmaxf(amax, fabsf(f[e]));
+      }
+      int lo = f8::pack2_e4m3<false>(f[0] * s8, f[1] * s8, 0);
+      lo = f8::pack2_e4m3<true>(f[2] * s8, f[3] * s8, lo);
+      int hi = f8::pack2_e4m3<false>(f[4] * s8, f[5] * s8, 0);
+      hi = f8::pack2_e4m3<true>(f[6] * s8, f[7] * s8, hi);
+      if (n + 8 <= N) {
+        *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
+      } else {
+        const uint8_t* b8 = reinterpret_cast<const uint8_t*>(&lo);
+        const uint8_t* c8 = reinterpret_cast<const uint8_t*>(&hi);
+        for (int e = 0; e < 8 && n + e < N; ++e) C8[(size_t)m * ldc8 + n + e] = e < 4 ? b8[e] : c8[e - 4];
+      }
+    }
+  }
+  if (C8 && amax_out) {  // one atomic per workgroup, spread over AMAX_SPREAD words
+    amax = wave_max(amax);
+    float* red = reinterpret_cast<float*>(smem + NW * WTM * SROW);
+    if (lane == 0) red[wid] = amax;
+    __syncthreads();
+    if (tid == 0) {
+      float m = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m = fmaxf(m, red[w]);
+      f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)), m);
+    }
+  }
+}
+
+// y8 = e4m3(x * scale[0]); amax_out = max|x| (both optional sides)
+__global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict__ x,
+                                                        uint8_t* __restrict__ y8, long long n,
+                                                        const float* __restrict__ scale,
+                                                        unsigned* __restrict__ amax_out) {
+  const float s = scale[0];
+  float amax = 0.f;
+  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n;
+       i += (long long)gridDim.x * blockDim.x * 8) {
+    if (i + 8 <= n) {
+      const short8_t v = *reinterpret_cast<const short8_t*>(x + i);
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = bf2f((bf16_t)v[e]);
+        amax = fmaxf(amax, fabsf(f[e]));
+      }
+      int lo = f8::pack2_e4m3<false>(f[0] * s, f[1] * s, 0);
+      lo = f8::pack2_e4m3<true>(f[2] * s, f[3] * s, lo);
+      int hi = f8::pack2_e4m3<false>(f[4] * s, f[5] * s, 0);
+      hi = f8::pack2_e4m3<true>(f[6] * s, f[7] * s, hi);
+      *reinterpret_cast<int2*>(y8 + i) = make_int2(lo, hi);
+    } else {
+      for (long long e = i; e < n; ++e) {
+        const float f = bf2f(x[e]);
+        amax = fmaxf(amax, fabsf(f));
+        const int w = f8::pack2_e4m3<false>(f * s, 0.f, 0);
+        y8[e] = (uint8_t)(w & 0xff);
+      }
+    }
+  }
+  // one atomic per block: thousands of same-address atomics serialise in L2
+  __shared__ float red[4];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  if (threadIdx.x == 0 && amax_out)
+    f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)),
+                    fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// Delayed scaling: scale[i] = 448 / (amax[i] * 2^margin) from last step's
+// amax (kept when nothing was recorded), then amax[i] = 0.
+__global__ void fp8_scale_update_kernel(float* __restrict__ scale, unsigned* __restrict__ amax,
+                                        int n, float margin_pow2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned m = 0u;
+#pragma unroll
+  for (int j = 0; j < AMAX_SPREAD; ++j) {
+    m = max(m, amax[i * AMAX_SPREAD + j]);
+    amax[i * AMAX_SPREAD + j] = 0u;
+  }
+  const float a = __uint_as_float(m);
+  if (a > 0.f && isfinite(a)) scale[i] = E4M3_MAX / (a * margin_pow2);
+}
+
+// e4m3 -> f32 (tests / debugging)
+__global__ void fp8_dequant_kernel(const uint8_t* __restrict__ x8, float* __restrict__ y,
+                                   long long n, float inv_scale) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  y[i] = __builtin_amdgcn_cvt_f32_fp8((int)x8[i], 0) * inv_scale;
+}
+
+}  // namespace tdg
+
+using namespace tdg;
+
+namespace {
+template <int BM, int BN, int WM, int WN, int ST, int EPI>
+int launch_f8(const void* A, const void* B, void* C, const float* bias, const float* sa,
+              const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
+              int lda, int ldb, int ldc, int ldc8, hipStream_t st) {
+  constexpr int img = WM * WN * (BM / WM) * ((BN / WN) * 2 + 16) + 64;  // + amax scratch
+  constexpr int lds = std::max(ST * (BM + BN) * BK8, img);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI>), dim3(tiles), dim3(WM * WN * 64),
+                     lds, st, (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C, bias, sa, sb,
+                     (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8);
+  return 0;
+}
+
+template <int EPI>
+int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, const float* sa,
+             const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
+             int lda, int ldb, int ldc, int ldc8, hipStream_t st) {
+#define TDG_F8(ID, BM_, BN_, WM_, WN_, ST_) \
+  case ID:                                 \
+    return launch_f8<BM_, BN_, WM_, WN_, ST_, EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
+  switch (cfg) {
+    TDG_F8(0, 128, 128, 2, 2, 2)
+    TDG_F8(1, 128, 64, 2, 2, 3)
+    TDG_F8(2, 64, 128, 2, 2, 3)
+    TDG_F8(3, 256, 128, 4, 2, 2)
+    TDG_F8(4, 128, 128, 2, 4, 3)
+    default:
+      TDG_F8(5, 64, 128, 2, 2, 2)
+  }
+#undef TDG_F8
+}
+}  // namespace
+
+extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias,
+                            const float* sa, const float* sb, void* C8, const float* sc8,
+                            unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
+                            int ldc8, int epi, int cfg, hipStream_t st) {
+  if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
+  switch (epi) {
+    case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
+    case F8_EPI_BIAS: return tiles_f8<F8_EPI_BIAS>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
+    case F8_EPI_BIAS_RELU: return tiles_f8<F8_EPI_BIAS_RELU>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
+    default: return -1;
+  }
+}
+
+extern "C" int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale,
+                             unsigned* amax, hipStream_t st) {
+  const int blocks = (int)std::min<long long>(1024, (n / 8 + 255) / 256 + 1);
+  hipLaunchKernelGGL(fp8_quant_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x,
+                     (uint8_t*)y8, n, scale, amax);
+  return 0;
+}
+
+extern "C" int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2,
+                                    hipStream_t st) {
+  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, scale, amax,
+                     n, margin_pow2);
+  return 0;
+}
+
+extern "C" int tdg_fp8_dequant(const void* x8, float* y, long long n, float inv_scale,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(fp8_dequant_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (const uint8_t*)x8, y, n, inv_scale);
+  return 0;
+}

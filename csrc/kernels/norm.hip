@@ -85,11 +85,22 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ s, const float* __restrict__ gamma,
     const float* __restrict__ beta, bf16_t* __restrict__ y, bf16_t* __restrict__ hsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, float p, uint32_t thresh,
-    uint64_t seed, const long long* ctr, uint64_t site, float eps) {
+    uint64_t seed, const long long* ctr, uint64_t site, float eps, uint8_t* __restrict__ y8,
+    const float* __restrict__ s8p, unsigned* __restrict__ amax8) {
   constexpr int VEC = D / 64;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  __shared__ float red8[4];
+  if (row >= M) {
+    if (y8 && lane == 0) red8[threadIdx.x >> 6] = 0.f;
+    if (y8) {
+      __syncthreads();
+      if (threadIdx.x == 0 && amax8)
+        atomic_amax(amax8 + (blockIdx.x & (AMAX_SPREAD - 1)),
+                    fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
+    }
+    return;
+  }
   const size_t base = (size_t)row * D + lane * VEC;
   RowVec<VEC> h, t;
   h.load_bf(x + base);
@@ -132,6 +143,36 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
+  }
+  if (y8) {  // fused e4m3 copy of y for an fp8 GEMM (delayed per-tensor scale)
+    const float s8 = s8p[0];
+    float am = 0.f;
+    int w[(VEC + 3) / 4];
+#pragma unroll
+    for (int i = 0; i < (VEC + 3) / 4; ++i) w[i] = 0;
+#pragma unroll
+    for (int i = 0; i < VEC; i += 2) {
+      const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
+      am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
+      if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
+      else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+    }
+    uint8_t* dst = y8 + base;
+    if constexpr (VEC == 2) {
+      *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
+    } else if constexpr (VEC == 4) {
+      *reinterpret_cast<int*>(dst) = w[0];
+    } else {
+#pragma unroll
+      for (int i = 0; i < VEC / 8; ++i)
+        *reinterpret_cast<int2*>(dst + 8 * i) = make_int2(w[2 * i], w[2 * i + 1]);
+    }
+    am = wave_max(am);
+    if (lane == 0) red8[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0 && amax8)
+      atomic_amax(amax8 + (blockIdx.x & (AMAX_SPREAD - 1)),
+                  fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
   }
 }
 
@@ -237,11 +278,12 @@ namespace {
 template <int D>
 void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* beta, void* y,
               void* hsave, float* mean, float* rstd, int M, float p, uint64_t seed,
-              const long long* ctr, uint64_t site, float eps, hipStream_t st) {
+              const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
+              unsigned* amax8, hipStream_t st) {
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
   hipLaunchKernelGGL(ln_fwd_kernel<D>, dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)s, gamma, beta, (bf16_t*)y, (bf16_t*)hsave, mean, rstd, M, p,
-                     thresh, seed, ctr, site, eps);
+                     thresh, seed, ctr, site, eps, (uint8_t*)y8, s8, amax8);
 }
 template <int D>
 void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
@@ -267,14 +309,19 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
 
 extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta,
                           void* y, void* hsave, float* mean, float* rstd, int M, int D, float p,
-                          uint64_t seed, const long long* ctr, uint64_t site, float eps, hipStream_t st) {
+                          uint64_t seed, const long long* ctr, uint64_t site, float eps, void* y8,
+                          const float* s8, unsigned* amax8, hipStream_t st) {
+#define TDG_LN_F(DD) \
+  ln_fwd_d<DD>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, y8, s8, amax8, st); \
+  return 0;
   switch (D) {
-    case 128: ln_fwd_d<128>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
-    case 256: ln_fwd_d<256>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
-    case 512: ln_fwd_d<512>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
-    case 1024: ln_fwd_d<1024>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, st); return 0;
+    case 128: TDG_LN_F(128)
+    case 256: TDG_LN_F(256)
+    case 512: TDG_LN_F(512)
+    case 1024: TDG_LN_F(1024)
     default: return -1;
   }
+#undef TDG_LN_F
 }
 
 // ws must hold 3 * ceil(M/8) * D floats.

@@ -41,7 +41,7 @@ import torch
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.ops.streams import offload
-from tensorflow_distributed_on_gke_amd.ops import philox
+from tensorflow_distributed_on_gke_amd.ops import fp8, philox
 
 LN_EPS = 1e-6
 
@@ -58,6 +58,8 @@ class RunCtx:
     store: Optional[ParamStore] = None
     # inference probe: {site: [B,H,Lq,Lk] f32 attention weights} when set
     attn_maps: Optional[dict] = None
+    # ops.fp8.Fp8State: FFN forward GEMMs in e4m3 (BASELINE config 5)
+    fp8: Optional[object] = None
 
     @property
     def p(self) -> float:
@@ -108,8 +110,14 @@ def _write_grad(p: Param, g: torch.Tensor, rt: RunCtx) -> None:
 def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
     """Returns (y, saved) for y = LN(x + dropout(s))."""
     if x.is_cuda:
+        y8 = s8 = a8 = None
+        slot = rt.fp8.ln_slots.get(id(gamma)) if rt.fp8 is not None else None
+        if slot is not None:  # this LN feeds an fp8 GEMM: emit its e4m3 copy too
+            y8 = torch.empty(x.shape, dtype=fp8.FP8, device=x.device)
+            s8, a8 = rt.fp8.meta.s(slot), rt.fp8.meta.a(slot)
+            rt.fp8.stash[slot] = y8
         y, h, mean, rstd = K.ln_fwd(x.contiguous(), s.contiguous(), gamma.master, beta.master,
-                                    rt.p, rt.seed, rt.ctr, site)
+                                    rt.p, rt.seed, rt.ctr, site, y8=y8, s8=s8, amax8=a8)
         return y, (h, mean, rstd, None)
     ks = _keep_scale(rt, site, s.shape, s.device)
     h = x + (s * ks if ks is not None else s)
@@ -422,7 +430,18 @@ class FFNBlockFn(torch.autograd.Function):
         x2 = x.reshape(B * L, d)
         ctx.p = (w1, b1, w2, b2, gamma, beta)
         ctx.meta = (site, rt)
-        if x.is_cuda:
+        if x.is_cuda and rt.fp8 is not None:
+            st = rt.fp8
+            xs, hs = st.ffn_slots[id(w1)]
+            w1_8, s1 = st.weights.get(w1)
+            w2_8, s2 = st.weights.get(w2)
+            x8 = st.stash.pop(xs, None)  # fused into the producing LayerNorm
+            if x8 is None:
+                x8 = fp8.quantize(x2, st.meta, xs)
+            x8 = x8.view(x2.shape)
+            h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs)
+            f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2)
+        elif x.is_cuda:
             h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
             f = K.linear_fwd(h, w2.compute, b2.master)
         else:

@@ -1,0 +1,176 @@
+"""FP8 (OCP e4m3) forward GEMMs with delayed per-tensor scaling.
+
+BASELINE config 5 ("Transformer-big seq_len=512 fp8 MFMA attention+FFN").
+Every fp8 operand has a slot in one device-resident `Fp8Meta`: `scale[i]`
+(x8 = e4m3(x * scale)) and `amax[i]` (max |x| recorded by whoever quantised
+slot i this step). Once per step, after the optimizer,
+`Fp8Meta.update()` turns the recorded amax into the next step's scale
+(448 / (amax * 2^margin)) and clears amax -- all on device, so the step stays
+one HIP graph. Weights are re-quantised right after that update, with the
+scale the next forward will dequantise with.
+
+Forward: activation -> e4m3 (fp8_quant, or fused into the producing GEMM's
+epilogue), e4m3 x e4m3 GEMM on the block-scaled MFMA (csrc/kernels/fp8.hip),
+bf16 out. Backward and the optimizer stay bf16 / fp32 (the bf16 activations
+the fp8 GEMMs were fed are what the backward saves).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from tensorflow_distributed_on_gke_amd.ops._ext import C
+from tensorflow_distributed_on_gke_amd.ops import kernels as K
+
+FP8 = torch.float8_e4m3fn
+E4M3_MAX = 448.0
+_CANDS = (0, 1, 2, 3, 4, 5)
+_TUNED: Dict[tuple, int] = {}
+
+
+class Fp8Meta:
+    def __init__(self, device, capacity: int = 256, margin: int = 0):
+        self.device = torch.device(device)
+        self.scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
+        # [slot, 64]: producers spread their atomics over 64 words (AMAX_SPREAD)
+        self.amax = torch.zeros(capacity, 64, dtype=torch.int32, device=self.device)
+        self.margin = margin
+        self.names: List[str] = []
+
+    def slot(self, name: str) -> int:
+        if len(self.names) >= self.scale.numel():
+            raise RuntimeError("Fp8Meta capacity exhausted")
+        self.names.append(name)
+        return len(self.names) - 1
+
+    def s(self, i: int) -> torch.Tensor:
+        return self.scale[i:i + 1]
+
+    def a(self, i: int) -> torch.Tensor:
+        return self.amax[i]
+
+    def update(self) -> None:
+        n = len(self.names)
+        if n:
+            C().fp8_scale_update(self.scale[:n], self.amax[:n], float(2 ** self.margin))
+
+    def amax_values(self) -> torch.Tensor:
+        return self.amax[: len(self.names)].view(torch.float32).amax(dim=1)
+
+
+def quantize(x: torch.Tensor, meta: Fp8Meta, i: int, out: Optional[torch.Tensor] = None,
+             record: bool = True) -> torch.Tensor:
+    if out is None:
+        out = torch.empty(x.shape, dtype=FP8, device=x.device)
+    C().fp8_quant(x.contiguous(), out, meta.s(i), meta.a(i) if record else None)
+    return out
+
+
+def dequantize(x8: torch.Tensor, scale: float) -> torch.Tensor:
+    return x8.float() / scale
+
+
+def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
+             out8_slot: Optional[int] = None, cfg: Optional[int] = None
+             ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """y[M,N] = dequant(a8[M,K] @ b8[N,K]^T) + bias (relu), bf16; with
+    out8_slot also y8 = e4m3(y * scale[out8_slot]) (amax recorded)."""
+    M, Kd = a8.shape
+    N = b8.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device)
+    y8 = torch.empty(M, N, dtype=FP8, device=a8.device) if out8_slot is not None else None
+    epi = 2 if relu else (1 if bias is not None else 0)
+
+    def run(c):
+        C().gemm_fp8(a8, b8, y, bias, meta.s(ia), meta.s(ib), y8,
+                     meta.s(out8_slot) if y8 is not None else None,
+                     meta.a(out8_slot) if y8 is not None else None,
+                     M, N, Kd, a8.stride(0), b8.stride(0), N, N, epi, c)
+
+    if cfg is None:
+        key = (M, N, Kd, epi, y8 is not None)
+        cfg = _TUNED.get(key)
+        if cfg is None:
+            if K.AUTOTUNE and a8.is_cuda and not torch.cuda.is_current_stream_capturing():
+                cfg = _autotune(run)
+            else:
+                cfg = 0 if M * N >= 256 * 128 * 128 else 5
+            _TUNED[key] = cfg
+    run(cfg)
+    return y, y8
+
+
+def _autotune(run) -> int:
+    times = {}
+    for rnd in range(2):
+        for c in _CANDS:
+            try:
+                run(c)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    run(c)
+                e1.record()
+                e1.synchronize()
+                times[c] = min(times.get(c, math.inf), e0.elapsed_time(e1))
+            except RuntimeError:
+                continue
+    return min(times, key=times.get)
+
+
+class Fp8Weights:
+    """fp8 copies of selected weight matrices, refreshed from the bf16 shadow
+    after every optimizer step (after the scale update)."""
+
+    def __init__(self, meta: Fp8Meta):
+        self.meta = meta
+        self.items: List[Tuple[object, torch.Tensor, int]] = []
+        self.by_param: Dict[int, Tuple[torch.Tensor, int]] = {}
+
+    def add(self, param) -> Tuple[torch.Tensor, int]:
+        w8 = torch.empty(param.shape, dtype=FP8, device=self.meta.device)
+        slot = self.meta.slot("w:" + param.name)
+        self.items.append((param, w8, slot))
+        self.by_param[id(param)] = (w8, slot)
+        return w8, slot
+
+    def get(self, param) -> Tuple[torch.Tensor, int]:
+        return self.by_param[id(param)]
+
+    def refresh(self) -> None:
+        for p, w8, slot in self.items:
+            C().fp8_quant(p.compute, w8, self.meta.s(slot), self.meta.a(slot))
+
+    def calibrate(self) -> None:
+        """Initial weight scales from their actual amax."""
+        self.refresh()
+        self.meta.update()
+        self.refresh()
+
+
+class Fp8State:
+    """Per-model fp8 bookkeeping: meta, weight copies and activation slots
+    (one set per FFN layer)."""
+
+    def __init__(self, model, margin: int = 0):
+        self.meta = Fp8Meta(model.device, margin=margin)
+        self.weights = Fp8Weights(self.meta)
+        self.ffn_slots: Dict[int, Tuple[int, int]] = {}
+        # LayerNorms whose output is an FFN input: they emit the e4m3 copy
+        self.ln_slots: Dict[int, int] = {}
+        self.stash: Dict[int, torch.Tensor] = {}
+        for layer in list(model.enc_layers) + list(model.dec_layers):
+            self.weights.add(layer.ff1.w)
+            self.weights.add(layer.ff2.w)
+            xs = self.meta.slot(f"x:{id(layer)}")
+            hs = self.meta.slot(f"h:{id(layer)}")
+            self.ffn_slots[id(layer.ff1.w)] = (xs, hs)
+            feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
+            self.ln_slots[id(feeder.gamma)] = xs
+        self.weights.calibrate()
+
+    def after_step(self) -> None:
+        self.meta.update()
+        self.weights.refresh()

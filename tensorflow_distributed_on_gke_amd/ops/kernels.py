@@ -274,14 +274,17 @@ def attn_probs(q, k, kv_len, scale: float, causal: bool) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ layernorm
-def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True):
+def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, s8=None,
+           amax8=None):
+    """y = LN(x + dropout(s)); optionally also y8 = e4m3(y * s8) (fp8 copy,
+    amax recorded into amax8)."""
     D = x.shape[-1]
     M = x.numel() // D
     y = torch.empty_like(x)
     h = torch.empty_like(x) if save else None
     mean = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
     rstd = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
-    C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps)
+    C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps, y8, s8, amax8)
     return y, h, mean, rstd
 
 

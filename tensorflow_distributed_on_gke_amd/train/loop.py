@@ -89,7 +89,12 @@ class Trainer:
         comm = torch.bfloat16 if s.grad_comm_dtype == "bf16" else None
         self.ddp = (DataParallel(self.model.store, bucket_mb=s.bucket_mb, comm_dtype=comm)
                     if info.world > 1 else None)
-        self.step_fn = TrainStep(self.model, self.opt, self.ddp, workers=info.world, seed=s.seed + 17)
+        self.fp8 = None
+        if s.dtype == "fp8" and info.device.type == "cuda":
+            from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
+            self.fp8 = Fp8State(self.model)
+        self.step_fn = TrainStep(self.model, self.opt, self.ddp, workers=info.world, seed=s.seed + 17,
+                                 fp8_state=self.fp8)
         self.train_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab, s.tgt_vocab,
                                          seed=s.seed, rank=info.rank, world=info.world, min_len=s.min_len,
                                          copy_task=s.copy_task, pin=info.device.type == "cuda")
@@ -132,6 +137,8 @@ class Trainer:
             dist.broadcast(flag, 0)
         self.start_epoch = int(flag[1].item()) if int(flag[0].item()) else 0
         self._broadcast_state()
+        if self.fp8 is not None:
+            self.fp8.weights.calibrate()  # weights may have changed (resume / warm start)
 
     def save_resume_state(self, epochs_done: int) -> None:
         bundle.save_weights(self.model.store, self.resume_prefix)

@@ -25,7 +25,7 @@ from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 class TrainStep:
     def __init__(self, model: Transformer, opt: Adam, ddp: Optional[DataParallel], workers: float,
-                 seed: int = 0, dropout: Optional[float] = None):
+                 seed: int = 0, dropout: Optional[float] = None, fp8_state=None):
         self.model = model
         self.opt = opt
         self.ddp = ddp
@@ -33,7 +33,8 @@ class TrainStep:
         dev = model.device
         self.rt = RunCtx(training=True, dropout=model.cfg.dropout if dropout is None else dropout,
                          seed=seed, ctr=torch.zeros(1, dtype=torch.int64, device=dev),
-                         store=model.store)
+                         store=model.store, fp8=fp8_state)
+        self.fp8 = fp8_state
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
         self.last = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -49,6 +50,8 @@ class TrainStep:
         else:
             join(self.model.device)  # weight gradients from the side stream
         self.opt.apply()
+        if self.fp8 is not None:
+            self.fp8.after_step()  # new scales, then fp8 weight copies
         return self.last
 
     # ------------------------------------------------------------------ HIP graph
