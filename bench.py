@@ -50,6 +50,8 @@ def main() -> None:
                     help="gradient all-reduce dtype (bf16 halves xGMI bytes)")
     ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--defer-wgrad", type=int, default=-1,
+                    help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: FFN forward GEMMs in e4m3 with delayed scaling (BASELINE config 5)")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
@@ -71,7 +73,8 @@ def main() -> None:
     if args.dtype == "fp8":
         from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
         fp8_state = Fp8State(model)
-    step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17, fp8_state=fp8_state)
+    step = TrainStep(model, opt, ddp, workers=world, seed=args.seed + 17, fp8_state=fp8_state,
+                     defer_wgrad=None if args.defer_wgrad < 0 else bool(args.defer_wgrad))
 
     S = T = args.seq_len
     data = SyntheticPairs(batch=args.local_batch, src_len=S, tgt_len=T + 1, src_vocab=cfg.src_vocab,
@@ -135,6 +138,7 @@ def main() -> None:
                 "parallelism": f"dp{world}",
                 "hip_graph": bool(use_graph),
                 "grad_comm": args.grad_comm,
+                "defer_wgrad": step.rt.wgrad is not None,
                 "bucket_mb": args.bucket_mb,
                 "last_loss": round(loss, 4),
             },

@@ -1,3 +1,4 @@
+#include <vector>
 // Python bindings for the gfx950 kernels (module `_C`).
 // Every op launches on the current HIP stream of the tensors' device, takes
 // caller-allocated outputs (no allocation inside an op: HIP-graph capturable)
@@ -40,6 +41,9 @@ int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtabl
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
+int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
+                     int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc, int out_f32,
+                     float alpha, float beta, int tile_cfg, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
@@ -449,6 +453,43 @@ void embed_bwd_det(const Tensor& tok, const Tensor& dout, const Tensor& dtable, 
   check_err(rc, "tdg embed_bwd_det");
 }
 
+// ---------------------------------------------------------------- grouped GEMM
+void gemm_grouped(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
+                  const std::vector<Tensor>& Cs, int64_t M, int64_t N, int64_t K, int64_t lda,
+                  int64_t ldb, int64_t ldc, bool a_kc, bool b_kc, double alpha, double beta,
+                  int64_t tile_cfg) {
+  const size_t G = As.size();
+  TORCH_CHECK(G >= 1 && G <= 32 && Bs.size() == G && Cs.size() == G, "gemm_grouped: 1..32 problems");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc >= N, "gemm_grouped: shape");
+  auto r8 = [](int64_t v) { return (v + 7) / 8 * 8; };
+  const bool f32 = Cs[0].scalar_type() == at::kFloat;
+  std::vector<const void*> a(G), b(G);
+  std::vector<void*> c(G);
+  for (size_t i = 0; i < G; ++i) {
+    check_bf16(As[i], "A");
+    check_bf16(Bs[i], "B");
+    TORCH_CHECK(Cs[i].is_cuda() && (Cs[i].scalar_type() == at::kFloat) == f32 &&
+                    (f32 || Cs[i].scalar_type() == at::kBFloat16),
+                "gemm_grouped: C dtypes must match (f32 or bf16)");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(As[i].data_ptr()) % 16) == 0 &&
+                    (reinterpret_cast<uintptr_t>(Bs[i].data_ptr()) % 16) == 0,
+                "gemm_grouped: A/B must be 16-byte aligned");
+    if (a_kc) check_extent(As[i], M, lda, r8(K), "A");
+    else check_extent(As[i], K, lda, r8(M), "A");
+    if (b_kc) check_extent(Bs[i], N, ldb, r8(K), "B");
+    else check_extent(Bs[i], K, ldb, r8(N), "B");
+    check_extent(Cs[i], M, ldc, N, "C");
+    a[i] = As[i].data_ptr();
+    b[i] = Bs[i].data_ptr();
+    c[i] = Cs[i].data_ptr();
+  }
+  c10::DeviceGuard g(As[0].device());
+  const int rc = tdg_gemm_grouped(a.data(), b.data(), c.data(), (int)G, (int)M, (int)N, (int)K,
+                                  (int)lda, (int)ldb, (int)ldc, a_kc, b_kc, f32, (float)alpha,
+                                  (float)beta, (int)tile_cfg, stream_of(As[0]));
+  check_err(rc, "tdg gemm_grouped");
+}
+
 // ---------------------------------------------------------------- fp8
 void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
               const Tensor& sa, const Tensor& sb, const optional<Tensor>& C8,
@@ -599,6 +640,7 @@ void to_bf16(const Tensor& p, const Tensor& o) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
+  m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_scale_update", &fp8_scale_update);

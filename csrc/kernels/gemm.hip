@@ -180,12 +180,28 @@ __device__ __forceinline__ short8_t frag(const char* lds, int base, int s, int l
   }
 }
 
+// Grouped launch: up to MAXG same-shape problems in one grid (blockIdx.y =
+// problem). Used for the weight gradients, deferred to the end of backward and
+// issued per shape: long-K tiles for the whole chip without split-K slabs.
+constexpr int MAXG = 32;
+struct GemmGroup {
+  const bf16_t* A[MAXG];
+  const bf16_t* B[MAXG];
+  void* C[MAXG];
+};
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool A_KC, bool B_KC, int EPI,
           bool OUT_F32>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
     const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
-    int ldb, int ldc, int ldaux, float alpha, float beta, int k_per_split, long long split_stride) {
+    int ldb, int ldc, int ldaux, float alpha, float beta, int k_per_split, long long split_stride,
+    const GemmGroup grp) {
+  if (gridDim.y > 1) {
+    A = grp.A[blockIdx.y];
+    B = grp.B[blockIdx.y];
+    Cv = grp.C[blockIdx.y];
+  }
   constexpr int NW = WM * WN;
   constexpr int NT = NW * 64;
   constexpr int TM = BM / WM / 16;  // 16x16 subtiles per wave along M
@@ -488,7 +504,9 @@ namespace {
 template <int BM, int BN, int WM, int WN, int ST, bool AK, bool BKc, int EPI, bool F32>
 void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, const bf16_t* aux,
                 int M, int N, int K, int lda, int ldb, int ldc, int ldaux, float alpha, float beta,
-                int splits, float* ws, hipStream_t st) {
+                int splits, float* ws, hipStream_t st, const GemmGroup* grp = nullptr, int G = 1) {
+  static const GemmGroup kNoGroup{};
+  const GemmGroup& gr = grp ? *grp : kNoGroup;
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   const int img = WM * (BM / WM) * ((BN / WN) * (F32 ? 4 : 2) + 16) * WN;
   const int img32 = WM * (BM / WM) * ((BN / WN) * 4 + 16) * WN;  // split-K slab staging
@@ -501,17 +519,17 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (splits <= 1) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>), dim3(tiles, 1, 1),
+  if (splits <= 1 || G > 1) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>), dim3(tiles, G, 1),
                        dim3(WM * WN * 64), lds, st, A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                       ldaux, alpha, beta, K, 0LL);
+                       ldaux, alpha, beta, K, 0LL, gr);
   } else {
     int kps = cdiv(cdiv(K, splits), BK) * BK;
     splits = cdiv(K, kps);
     const long long stride = (long long)M * ldc;
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI_NONE, true>),
                        dim3(tiles, 1, splits), dim3(WM * WN * 64), lds, st, A, B, (void*)ws, bias,
-                       aux, M, N, K, lda, ldb, ldc, ldaux, 1.f, 0.f, kps, stride);
+                       aux, M, N, K, lda, ldb, ldc, ldaux, 1.f, 0.f, kps, stride, gr);
     const long long total = (long long)M * N;
     const int blocks = (int)std::min<long long>(4096, (total + 255) / 256);
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, F32>), dim3(blocks), dim3(256), 0, st, ws, C,
@@ -522,12 +540,13 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
 template <bool AK, bool BKc, int EPI, bool F32>
 void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const float* bias,
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
-                  float alpha, float beta, int splits, float* ws, hipStream_t st) {
+                  float alpha, float beta, int splits, float* ws, hipStream_t st,
+                  const GemmGroup* grp = nullptr, int G = 1) {
 #define TDG_CFG(ID, BM_, BN_, WM_, WN_, ST_)                                                  \
   case ID:                                                                                    \
     launch_cfg<BM_, BN_, WM_, WN_, ST_, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, \
                                                           ldc, ldaux, alpha, beta, splits, ws,   \
-                                                          st);                                   \
+                                                          st, grp, G);                           \
     break;
   // Tile table (BM, BN, waves M x N, pipeline stages). LDS = ST*(BM+BN)*128 B;
   // the table keeps >= 2 waves per SIMD resident (1 is latency-bound).
@@ -591,6 +610,31 @@ extern "C" int tdg_gemm(const void* A, const void* B, void* C, const float* bias
                                       ldc, ldaux, alpha, beta, splits, ws, st);
   return dispatch_epi<false, true>(epi, out_f32, tile_cfg, a, b, C, bias, x, M, N, K, lda, ldb,
                                    ldc, ldaux, alpha, beta, splits, ws, st);
+}
+
+// Grouped GEMM: G (<= 32) problems of one shape / layout, plain epilogue
+// (alpha, beta), one launch. Returns 0 on success.
+extern "C" int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G,
+                                int M, int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc,
+                                int out_f32, float alpha, float beta, int tile_cfg, hipStream_t st) {
+  if (G < 1 || G > MAXG) return -2;
+  GemmGroup g{};
+  for (int i = 0; i < G; ++i) {
+    g.A[i] = (const bf16_t*)A[i];
+    g.B[i] = (const bf16_t*)B[i];
+    g.C[i] = C[i];
+  }
+  const bf16_t* a0 = g.A[0];
+  const bf16_t* b0 = g.B[0];
+#define TDG_GR(AK, BKc, F)                                                                      \
+  launch_tiles<AK, BKc, EPI_NONE, F>(tile_cfg, a0, b0, C[0], nullptr, nullptr, M, N, K, lda, ldb, \
+                                     ldc, 0, alpha, beta, 1, nullptr, st, &g, G);               \
+  return 0;
+  if (a_kc && b_kc) { if (out_f32) { TDG_GR(true, true, true) } else { TDG_GR(true, true, false) } }
+  if (a_kc && !b_kc) { if (out_f32) { TDG_GR(true, false, true) } else { TDG_GR(true, false, false) } }
+  if (!a_kc && !b_kc) { if (out_f32) { TDG_GR(false, false, true) } else { TDG_GR(false, false, false) } }
+  if (out_f32) { TDG_GR(false, true, true) } else { TDG_GR(false, true, false) }
+#undef TDG_GR
 }
 
 extern "C" void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld,

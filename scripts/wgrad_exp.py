@@ -17,7 +17,7 @@ for M, N, K in shapes:
     C = torch.empty(M, N, device="cuda", dtype=torch.float32)
     fl = 2.0 * M * N * K
     res = []
-    for c in (0, 2, 4, 7, 8, 1, 3):
+    for c in (0, 2, 4, 5, 6, 7, 8, 9, 10, 11, 1, 3):
         for sp in (1, 2, 4, 8):
             try:
                 t_tn = graph_time(lambda: kk.gemm(dy, x, C, M, N, K, M, N, N, False, False, cfg=(c, sp)))
@@ -30,3 +30,5 @@ for M, N, K in shapes:
     tt = graph_time(lambda: (dy.t().contiguous(), x.t().contiguous()))
     print(f"{M}x{N}x{K}: TN best {best_tn[0]:.1f}us (c{best_tn[2]} s{best_tn[3]}, {fl/best_tn[0]/1e6:.0f} TF) | "
           f"NT best {best_nt[1]:.1f}us (c{best_nt[2]} s{best_nt[3]}, {fl/best_nt[1]/1e6:.0f} TF) | torch transposes {tt:.1f}us", flush=True)
+    top = sorted(res)[:6]
+    print("   TN top:", ", ".join(f"c{c}s{sp}={t:.1f}" for t, _, c, sp in top), flush=True)

@@ -60,6 +60,8 @@ class RunCtx:
     attn_maps: Optional[dict] = None
     # ops.fp8.Fp8State: FFN forward GEMMs in e4m3 (BASELINE config 5)
     fp8: Optional[object] = None
+    # WgradQueue: weight gradients deferred to the end of backward (grouped)
+    wgrad: Optional["WgradQueue"] = None
 
     @property
     def p(self) -> float:
@@ -104,6 +106,66 @@ def _write_grad(p: Param, g: torch.Tensor, rt: RunCtx) -> None:
         p.grad.add_(g.to(p.grad.dtype))
     else:
         p.grad.copy_(g.to(p.grad.dtype))
+
+
+class WgradQueue:
+    """Weight-gradient GEMMs deferred to the end of backward.
+
+    Nothing in backward reads a weight gradient, so instead of one small
+    long-K GEMM per layer (split-K slabs + a reduce kernel, 64x64 tiles to
+    fill the chip) the wgrads of all layers with the same shape run as ONE
+    grouped launch (ops.kernels.wgrad_grouped): e.g. the 24 d x d projections
+    of Transformer-base become 1536 whole-K tiles. Bias column sums and the
+    data-parallel grad_ready notifications follow in backward order."""
+
+    def __init__(self, flush_at_boundary: bool = False):
+        self.items = []
+        # data parallel: also flush when the decoder's backward is complete,
+        # so the decoder-side buckets are all-reduced while the encoder's
+        # backward runs
+        self.flush_at_boundary = flush_at_boundary
+
+    def boundary(self) -> None:
+        if self.flush_at_boundary and self.items:
+            self.flush()
+
+    def add(self, dy2, x2, N, w: Param, b: Optional[Param], beta: float, rt: "RunCtx"):
+        self.items.append((dy2, x2, N, w, b, beta, rt))
+
+    def flush(self) -> None:
+        groups = {}
+        for it in self.items:
+            dy2, x2, N, w, b, beta, rt = it
+            key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), N, beta)
+            groups.setdefault(key, []).append(it)
+        for key, items in groups.items():
+            for c0 in range(0, len(items), 32):
+                chunk = items[c0:c0 + 32]
+                beta = chunk[0][5]
+                if len(chunk) == 1:
+                    dy2, x2, N, w, *_ = chunk[0]
+                    K.linear_wgrad(dy2, x2, N, w.grad, beta)
+                else:
+                    K.wgrad_grouped([i[0] for i in chunk], [i[1] for i in chunk],
+                                    [i[3].grad for i in chunk], beta)
+        for dy2, x2, N, w, b, beta, rt in self.items:
+            if b is not None:
+                K.colsum(dy2, N, b.grad, beta)
+            _ready(rt, w, *([b] if b is not None else []))
+        self.items = []
+
+
+def _wgrad(rt: RunCtx, dy2, x2, N: int, w: Param, b: Optional[Param] = None) -> None:
+    """dW (+ bias grad) of a Linear on the GPU: deferred (rt.wgrad) or now."""
+    bt = _beta(rt)
+    if rt.wgrad is not None:
+        rt.wgrad.add(dy2, x2, N, w, b, bt, rt)
+        return
+    with offload(dy2, x2):
+        K.linear_wgrad(dy2, x2, N, w.grad, bt)
+        if b is not None:
+            K.colsum(dy2, N, b.grad, bt)
+        _ready(rt, w, *([b] if b is not None else []))
 
 
 # =============================================================================== LN helpers
@@ -265,18 +327,13 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ds2 = ds.reshape(M, d)
         q5 = qkv.view(B, L, 3, heads, hd)
         if dy.is_cuda:
-            with offload(ds2, o):
-                K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
-                _ready(rt, wo)
+            _wgrad(rt, ds2, o.view(M, d), d, wo)
             do = K.linear_dgrad(ds2, wo.compute, d)
             dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
             g5 = dqkv.view(B, L, 3, heads, hd)
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
-            with offload(dqkv, x2):
-                K.linear_wgrad(dqkv, x2, 3 * d, wqkv.grad, bt)
-                K.colsum(dqkv, 3 * d, bqkv.grad, bt)
-                _ready(rt, wqkv, bqkv)
+            _wgrad(rt, dqkv, x2, 3 * d, wqkv, bqkv)
             dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
             return (dx.view(B, L, d),) + (None,) * 11
         else:
@@ -323,10 +380,9 @@ class CrossKVFn(torch.autograd.Function):
         N = wkv.shape[0]
         bt = _beta(rt)
         if e2.is_cuda:
-            with offload(dkv, e2):
-                K.linear_wgrad(dkv, e2, N, wkv.grad, bt)
-                K.colsum(dkv, N, bkv.grad, bt)
-                _ready(rt, wkv, bkv)
+            _wgrad(rt, dkv, e2, N, wkv, bkv)
+            if rt.wgrad is not None:
+                rt.wgrad.boundary()  # every decoder layer's backward is done
             denc = K.linear_dgrad(dkv, wkv.compute, N)
         else:
             _write_grad(wkv, dkv.t() @ e2, rt)
@@ -388,18 +444,13 @@ class CrossAttnBlockFn(torch.autograd.Function):
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:
-            with offload(ds2, o):
-                K.linear_wgrad(ds2, o.view(M, d), d, wo.grad, bt)
-                _ready(rt, wo)
+            _wgrad(rt, ds2, o.view(M, d), d, wo)
             do = K.linear_dgrad(ds2, wo.compute, d)
             dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
             K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
                        do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
                        g5[:, :, 1], kv_len, scale, False)
-            with offload(dq, x2):
-                K.linear_wgrad(dq, x2, d, wq.grad, bt)
-                K.colsum(dq, d, bq.grad, bt)
-                _ready(rt, wq, bq)
+            _wgrad(rt, dq, x2, d, wq, bq)
         else:
             _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
             _ready(rt, wo)
@@ -462,14 +513,9 @@ class FFNBlockFn(torch.autograd.Function):
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
-            with offload(ds2, h):
-                K.linear_wgrad(ds2, h, d, w2.grad, bt)
-                _ready(rt, w2)
+            _wgrad(rt, ds2, h, d, w2)
             dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
-            with offload(dpre, x2):
-                K.linear_wgrad(dpre, x2, ff, w1.grad, bt)
-                K.colsum(dpre, ff, b1.grad, bt)
-                _ready(rt, w1, b1)
+            _wgrad(rt, dpre, x2, ff, w1, b1)
             dx = _dgrad_into(dpre, w1, ff, dh)
             return (dx.view(B, L, d),) + (None,) * 8
         else:

@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from tensorflow_distributed_on_gke_amd.models.layers import (CrossAttnBlockFn, CrossKVFn, EmbedFn,
+from tensorflow_distributed_on_gke_amd.models.layers import (_wgrad, CrossAttnBlockFn, CrossKVFn, EmbedFn,
                                                               FFNBlockFn, KVGrad, RunCtx,
                                                               SelfAttnBlockFn)
 from tensorflow_distributed_on_gke_amd.models.params import (ParamStore, TFSlot, const,
@@ -289,13 +289,7 @@ class Transformer:
                 return step_out
             beta = 1.0 if rt.accumulate else 0.0
             dl = logits  # now holds dlogits (pad columns zeroed)
-            d2c = dec2.contiguous()
-            with offload(dl, d2c):  # off the critical path (ops/streams.py)
-                K.linear_wgrad(dl, d2c, cfg.tgt_vocab, self.final.w.grad, beta)
-                K.colsum(dl, cfg.tgt_vocab, self.final.b.grad, beta)
-                if rt.store is not None:
-                    rt.store.grad_ready(self.final.w)
-                    rt.store.grad_ready(self.final.b)
+            _wgrad(rt, dl, dec2.contiguous(), cfg.tgt_vocab, self.final.w, self.final.b)
             ddec = K.linear_dgrad(dl, self.final.w.compute, cfg.tgt_vocab)
         else:
             lg = self.project(dec.detach())
@@ -332,6 +326,8 @@ class Transformer:
                 rt.store.grad_ready(fb)
             ddec = dl @ fw.master
         dec.backward(ddec.view(B, T, cfg.d_model).to(dec.dtype))
+        if rt.wgrad is not None:
+            rt.wgrad.flush()
         if dev.type == "cuda":
             join(dev)  # weight gradients are final when this returns
         return step_out

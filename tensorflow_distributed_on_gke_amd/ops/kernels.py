@@ -242,6 +242,52 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, N: int, dw: torch.Tensor,
                 EPI_NONE, beta=beta)
 
 
+_GROUP_TUNED: Dict[tuple, int] = {}
+_GROUP_CANDS = (0, 4, 5, 6, 7, 8, 2)
+
+
+def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
+    """dws[i][N,K] (f32) (+)= dys[i][M,N]^T @ xs[i][M,K] for up to 32 same-shape
+    problems in ONE launch (blockIdx.y = problem): whole-K tiles over the
+    whole chip, no split-K slabs."""
+    M, K = xs[0].shape
+    N = dws[0].shape[0]
+    lda, ldb, ldc = dys[0].stride(0), xs[0].stride(0), dws[0].stride(0)
+
+    def run(c):
+        C().gemm_grouped(dys, xs, dws, N, K, M, lda, ldb, ldc, False, False, 1.0, beta, c)
+
+    key = (M, N, K, len(dys), lda, ldb, beta != 0.0)
+    cfg = _GROUP_TUNED.get(key)
+    if cfg is None:
+        if AUTOTUNE and not torch.cuda.is_current_stream_capturing():
+            scratch = [workspace(f"gw{i}", d.numel(), d.device)[: d.numel()].view_as(d)
+                       for i, d in enumerate(dws)]
+
+            def trial(c):
+                C().gemm_grouped(dys, xs, scratch, N, K, M, lda, ldb, ldc, False, False, 1.0, 0.0, c)
+
+            times: Dict[int, float] = {}
+            for _ in range(2):
+                for c in _GROUP_CANDS:
+                    try:
+                        trial(c)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(3):
+                            trial(c)
+                        e1.record()
+                        e1.synchronize()
+                        times[c] = min(times.get(c, float("inf")), e0.elapsed_time(e1))
+                    except RuntimeError:
+                        continue
+            cfg = min(times, key=times.get)
+        else:
+            cfg = 0
+        _GROUP_TUNED[key] = cfg
+    run(cfg)
+
+
 def colsum(x2: torch.Tensor, N: int, out: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
     """out[N] (+)= sum over rows of bf16 x2[M, N]."""
     M = x2.shape[0]

@@ -16,7 +16,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
+from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.ops.streams import join
@@ -25,7 +25,8 @@ from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 class TrainStep:
     def __init__(self, model: Transformer, opt: Adam, ddp: Optional[DataParallel], workers: float,
-                 seed: int = 0, dropout: Optional[float] = None, fp8_state=None):
+                 seed: int = 0, dropout: Optional[float] = None, fp8_state=None,
+                 defer_wgrad: Optional[bool] = None):
         self.model = model
         self.opt = opt
         self.ddp = ddp
@@ -34,6 +35,14 @@ class TrainStep:
         self.rt = RunCtx(training=True, dropout=model.cfg.dropout if dropout is None else dropout,
                          seed=seed, ctr=torch.zeros(1, dtype=torch.int64, device=dev),
                          store=model.store, fp8=fp8_state)
+        # weight gradients grouped per shape (layers.WgradQueue): at the end of
+        # backward on one GPU; with data parallelism also at the decoder /
+        # encoder boundary so the decoder-side buckets' all-reduce overlaps
+        # the encoder backward
+        if defer_wgrad is None:
+            defer_wgrad = True
+        if defer_wgrad and dev.type == "cuda":
+            self.rt.wgrad = WgradQueue(flush_at_boundary=ddp is not None and ddp.world > 1)
         self.fp8 = fp8_state
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
