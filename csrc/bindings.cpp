@@ -41,6 +41,8 @@ int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtabl
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
+int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* part, int M, int N,
+                       int ld, int rows_per_block, float beta, hipStream_t st);
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
                      int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc, int out_f32,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
@@ -490,6 +492,30 @@ void gemm_grouped(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
   check_err(rc, "tdg gemm_grouped");
 }
 
+void colsum_grouped(const std::vector<Tensor>& Xs, const std::vector<Tensor>& outs,
+                    const Tensor& part, int64_t M, int64_t N, int64_t ld, int64_t rows_per_block,
+                    double beta) {
+  const size_t G = Xs.size();
+  TORCH_CHECK(G >= 1 && G <= 32 && outs.size() == G, "colsum_grouped: 1..32 problems");
+  check_f32(part, "part");
+  const int64_t nparts = (M + rows_per_block - 1) / rows_per_block;
+  TORCH_CHECK(part.numel() >= (int64_t)G * nparts * N, "colsum_grouped: partials too small");
+  std::vector<const void*> x(G);
+  std::vector<float*> o(G);
+  for (size_t i = 0; i < G; ++i) {
+    check_bf16(Xs[i], "X");
+    check_extent(Xs[i], M, ld, N, "X");
+    check_f32(outs[i], "out");
+    TORCH_CHECK(outs[i].numel() >= N, "colsum_grouped: out too short");
+    x[i] = Xs[i].data_ptr();
+    o[i] = outs[i].data_ptr<float>();
+  }
+  c10::DeviceGuard g(Xs[0].device());
+  check_err(tdg_colsum_grouped(x.data(), o.data(), (int)G, part.data_ptr<float>(), (int)M, (int)N,
+                               (int)ld, (int)rows_per_block, (float)beta, stream_of(Xs[0])),
+            "tdg colsum_grouped");
+}
+
 // ---------------------------------------------------------------- fp8
 void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
               const Tensor& sa, const Tensor& sb, const optional<Tensor>& C8,
@@ -641,6 +667,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
   m.def("gemm_grouped", &gemm_grouped);
+  m.def("colsum_grouped", &colsum_grouped);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_scale_update", &fp8_scale_update);

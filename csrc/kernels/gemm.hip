@@ -494,6 +494,73 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __res
   }
 }
 
+// Grouped column sums: up to 32 same-shape problems (blockIdx.z), partials
+// [z][P][N] in one workspace, then one grouped stage-2 fold.
+struct ColsumGroup {
+  const bf16_t* X[32];
+  float* out[32];
+};
+
+__global__ __launch_bounds__(256) void colsum_partial_grouped_kernel(ColsumGroup grp,
+                                                                     float* __restrict__ part, int M,
+                                                                     int N, int ld,
+                                                                     int rows_per_block) {
+  __shared__ float red[32][65];
+  const bf16_t* X = grp.X[blockIdx.z];
+  float* pz = part + (size_t)blockIdx.z * gridDim.y * N;
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int col0 = blockIdx.x * 64 + cg * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  const bool vec = (col0 + 8 <= N) && (ld % 8 == 0);
+  for (int r = r0 + rl; r < r1; r += 32) {
+    const bf16_t* p = X + (size_t)r * ld + col0;
+    if (vec) {
+      const short8_t v = *reinterpret_cast<const short8_t*>(p);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (col0 + i < N) acc[i] += bf2f(p[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rl][cg * 8 + i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) s += red[k][threadIdx.x];
+    const int col = blockIdx.x * 64 + threadIdx.x;
+    if (col < N) pz[(size_t)blockIdx.y * N + col] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_grouped_kernel(ColsumGroup grp,
+                                                                      const float* __restrict__ part,
+                                                                      int N, int P, float beta) {
+  __shared__ float red[4][64];
+  const float* pz = part + (size_t)blockIdx.y * P * N;
+  float* out = grp.out[blockIdx.y];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (col < N) {
+#pragma unroll 8
+    for (int p = g; p < P; p += 4) s += pz[(size_t)p * N + col];
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
+  }
+}
+
 }  // namespace tdg
 
 // ============================================================================ host
@@ -644,4 +711,22 @@ extern "C" void tdg_colsum(const void* X, float* out, float* part, int M, int N,
   hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(256), 0, st, (const bf16_t*)X, part, M, N,
                      ld, rows_per_block);
   launch_reduce_partials(part, out, N, nparts, beta, st);
+}
+
+// Grouped bias gradients: out[g][n] (=|+=) sum_m X[g][m][n], G <= 32 problems.
+extern "C" int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* part,
+                                  int M, int N, int ld, int rows_per_block, float beta,
+                                  hipStream_t st) {
+  if (G < 1 || G > 32) return -2;
+  ColsumGroup g{};
+  for (int i = 0; i < G; ++i) {
+    g.X[i] = (const bf16_t*)X[i];
+    g.out[i] = out[i];
+  }
+  const int nparts = cdiv(M, rows_per_block);
+  hipLaunchKernelGGL(colsum_partial_grouped_kernel, dim3(cdiv(N, 64), nparts, G), dim3(256), 0, st,
+                     g, part, M, N, ld, rows_per_block);
+  hipLaunchKernelGGL(reduce_partials_grouped_kernel, dim3(cdiv(N, 64), G), dim3(256), 0, st, g,
+                     part, N, nparts, beta);
+  return 0;
 }

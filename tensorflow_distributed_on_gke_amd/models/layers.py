@@ -148,9 +148,19 @@ class WgradQueue:
                 else:
                     K.wgrad_grouped([i[0] for i in chunk], [i[1] for i in chunk],
                                     [i[3].grad for i in chunk], beta)
+        # bias gradients, grouped by shape as well
+        bgroups = {}
         for dy2, x2, N, w, b, beta, rt in self.items:
             if b is not None:
-                K.colsum(dy2, N, b.grad, beta)
+                bgroups.setdefault((tuple(dy2.shape), dy2.stride(0), N, beta), []).append((dy2, b))
+        for (shape, ld, N, beta), items in bgroups.items():
+            for c0 in range(0, len(items), 32):
+                chunk = items[c0:c0 + 32]
+                if len(chunk) == 1:
+                    K.colsum(chunk[0][0], N, chunk[0][1].grad, beta)
+                else:
+                    K.colsum_grouped([i[0] for i in chunk], [i[1].grad for i in chunk], beta)
+        for dy2, x2, N, w, b, beta, rt in self.items:
             _ready(rt, w, *([b] if b is not None else []))
         self.items = []
 

@@ -281,11 +281,22 @@ def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
                         times[c] = min(times.get(c, float("inf")), e0.elapsed_time(e1))
                     except RuntimeError:
                         continue
+            if not times:
+                run(0)  # surfaces the binding's error for this problem
             cfg = min(times, key=times.get)
         else:
             cfg = 0
         _GROUP_TUNED[key] = cfg
     run(cfg)
+
+
+def colsum_grouped(xs, outs, beta: float = 0.0) -> None:
+    """outs[i][N] (+)= column sums of bf16 xs[i][M, N] (same shape), one
+    partial pass + one fold for the whole group."""
+    M, N = xs[0].shape[0], outs[0].numel()
+    rpb = 256
+    part = workspace("colsum_g", len(xs) * math.ceil(M / rpb) * N, xs[0].device)
+    C().colsum_grouped(xs, outs, part, M, N, xs[0].stride(0), rpb, beta)
 
 
 def colsum(x2: torch.Tensor, N: int, out: torch.Tensor, beta: float = 0.0) -> torch.Tensor:

@@ -290,3 +290,21 @@ def test_adam_keras_semantics():
     assert step.item() == 11
     assert gd.abs().max().item() == 0.0
     _close(sh, ref, 1e-2, "adam shadow")
+
+
+# --------------------------------------------------------------------------- grouped launches
+@pytest.mark.parametrize("G,M,N,Kd", [(5, 192, 128, 1000), (24, 512, 512, 2048), (3, 72, 2048, 333)])
+def test_grouped_wgrad_and_colsum(G, M, N, Kd):
+    """dW_i = dy_i^T x_i for G problems in one launch; bias grads grouped."""
+    torch.manual_seed(0)
+    dys = [_bf(torch.randn(Kd, M)).to(DEV) for _ in range(G)]
+    xs = [_bf(torch.randn(Kd, N)).to(DEV) for _ in range(G)]
+    dws = [torch.full((M, N), 3.0, device=DEV) for _ in range(G)]
+    kk.wgrad_grouped(dys, xs, dws, beta=1.0)
+    for i in range(G):
+        ref = dys[i].float().t() @ xs[i].float() + 3.0
+        _close(dws[i], ref, 1e-2, f"grouped wgrad {i}")
+    outs = [torch.zeros(M, device=DEV) for _ in range(G)]
+    kk.colsum_grouped(dys, outs)
+    for i in range(G):
+        _close(outs[i], dys[i].float().sum(0), 1e-3, f"grouped colsum {i}")
