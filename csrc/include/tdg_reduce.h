@@ -32,22 +32,26 @@ struct ReduceSet {
   const float* part[3];
   float* out[3];
 };
+// 16 columns x 16 partial-lanes per block: many blocks even for small N
+// (a LayerNorm's D = 512 columns x 3 sets = 96 blocks instead of 24).
 static __global__ __launch_bounds__(256) void reduce_partials3_kernel(ReduceSet rs, int N, int P,
                                                                       float beta) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][17];
   const float* part = rs.part[blockIdx.y];
   float* out = rs.out[blockIdx.y];
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + c;
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + c;
   float s = 0.f;
   if (col < N) {
 #pragma unroll 8
-    for (int p = g; p < P; p += 4) s += part[(size_t)p * N + col];
+    for (int p = g; p < P; p += 16) s += part[(size_t)p * N + col];
   }
   red[g][c] = s;
   __syncthreads();
   if (g == 0 && col < N) {
-    const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][c];
     out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
   }
 }

@@ -101,13 +101,16 @@ __device__ __forceinline__ short8_t gfrag(const bf16_t* __restrict__ rowp, bool 
 // ============================================================================ forward
 // NWV waves per workgroup, 16 query rows per wave (NWV = 8 covers a whole
 // <= 128-query sequence, so K/V are read from HBM once per (batch, head)).
-template <int HD, int NWV>
+// KT keys per LDS tile (64 or 128: one load phase and one barrier pair for a
+// whole <= 128-key sequence).
+template <int HD, int NWV, int KT>
 __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   using T = ATile<HD>;
   constexpr int QBW = 16 * NWV;
+  constexpr int NT16 = KT / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
-  char* ldsV = smem + T::BYTES;
+  char* ldsV = smem + (KT / 64) * T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
   const int qrow = q0 + 16 * w + cl;
@@ -130,13 +133,16 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   for (int i = 0; i < T::DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-  for (int k0 = 0; k0 < klim; k0 += KB) {
-    T::template load<NWV * 64>(ldsK, kb, a.k_sl, k0, a.Lk, tid);
-    T::template load<NWV * 64>(ldsV, vb, a.v_sl, k0, a.Lk, tid);
-    __syncthreads();
-    f32x4 s[4];
+  for (int k0 = 0; k0 < klim; k0 += KT) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int h64 = 0; h64 < KT / 64; ++h64) {
+      T::template load<NWV * 64>(ldsK + h64 * T::BYTES, kb, a.k_sl, k0 + 64 * h64, a.Lk, tid);
+      T::template load<NWV * 64>(ldsV + h64 * T::BYTES, vb, a.v_sl, k0 + 64 * h64, a.Lk, tid);
+    }
+    __syncthreads();
+    f32x4 s[NT16];
+#pragma unroll
+    for (int t = 0; t < NT16; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < T::KS; ++ks) s[t] = mfma16(T::frag_row(ldsK, 16 * t, ks, lane), qf[ks], s[t]);
@@ -144,7 +150,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
     // mask + scale (log2 domain); s[t][r] = S[key=k0+16t+4g+r][q=qrow]
     float tmax = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + 16 * t + 4 * g + r;
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
     const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = (mn == -INFINITY) ? 0.f : exp2f(s[t][r] - mn);
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < T::DT; ++i) oacc[i] *= alpha;
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int s2 = 0; s2 < NT16 / 2; ++s2) {
       const short8_t pf = pack8(s[2 * s2][0], s[2 * s2][1], s[2 * s2][2], s[2 * s2][3],
                                 s[2 * s2 + 1][0], s[2 * s2 + 1][1], s[2 * s2 + 1][2],
                                 s[2 * s2 + 1][3]);
@@ -631,10 +637,10 @@ template <int HD>
 int fwd_hd(const AttnArgs& a, hipStream_t st) {
   if (a.Lq > 64) {
     dim3 grid(cdiv(a.Lq, 128), a.H, a.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8>), grid, dim3(512), 2 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8, 128>), grid, dim3(512), 4 * ATile<HD>::BYTES, st, a);
   } else {
     dim3 grid(cdiv(a.Lq, 64), a.H, a.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 4>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 4, 64>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
   }
   return 0;
 }

@@ -302,7 +302,7 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
                      (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site);
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
-  hipLaunchKernelGGL(reduce_partials3_kernel, dim3(cdiv(D, 64), dbias ? 3 : 2), dim3(256), 0, st,
+  hipLaunchKernelGGL(reduce_partials3_kernel, dim3(cdiv(D, 16), dbias ? 3 : 2), dim3(256), 0, st,
                      rs, D, nb, beta);
 }
 }  // namespace
