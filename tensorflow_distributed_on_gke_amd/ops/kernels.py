@@ -149,17 +149,21 @@ ALLOW_BLAS = True
 def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N) -> bool:
     """Plain GEMMs only (no fused epilogue): dgrad (KC x MC, bf16 out) and
     wgrad (MC x MC, f32 out) may go to hipBLASLt if it is faster."""
-    if not ALLOW_BLAS or epi != EPI_NONE or alpha != 1.0 or beta != 0.0 or ldc != N:
+    if not ALLOW_BLAS or epi != EPI_NONE or alpha != 1.0 or beta not in (0.0, 1.0) or ldc != N:
         return False
+    if beta == 1.0:  # C += A B (standard GEMM beta; residual-gradient accumulation)
+        return a_kc and not b_kc and Cout.dtype == torch.bfloat16
     return (a_kc and not b_kc and Cout.dtype == torch.bfloat16) or \
         (not a_kc and not b_kc and Cout.dtype == torch.float32)
 
 
-def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc):
+def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc, beta=0.0):
     a = A.as_strided((M, K), (lda, 1)) if a_kc else A.as_strided((K, M), (lda, 1)).t()
     b = B.as_strided((K, N), (ldb, 1))
     c = Cout.as_strided((M, N), (N, 1))
-    if Cout.dtype == torch.bfloat16:
+    if beta == 1.0:
+        c.addmm_(a, b)
+    elif Cout.dtype == torch.bfloat16:
         torch.mm(a, b, out=c)
     else:
         torch.mm(a, b, out_dtype=torch.float32, out=c)
@@ -173,7 +177,7 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None
         if c == BLAS:
             if not blas_ok:
                 raise RuntimeError("library GEMM not applicable")
-            _blas(A, B, out, M, N, K, lda, ldb, a_kc)
+            _blas(A, B, out, M, N, K, lda, ldb, a_kc, beta)
             return
         tile, splits = c
         ws = workspace("splitk", splits * M * ldc, A.device) if splits > 1 else None
@@ -192,7 +196,7 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None
                 # accumulate into C: tune on a scratch copy so C is untouched
                 scratch = workspace("tune_c", Cout.numel(), A.device, Cout.dtype)[: Cout.numel()]
                 scratch = scratch.view_as(Cout)
-                best = _autotune(key, lambda c: run(c, scratch), False)
+                best = _autotune(key, lambda c: run(c, scratch), blas_ok)
             else:
                 best = _autotune(key, run, blas_ok)
             ent = (best, best)

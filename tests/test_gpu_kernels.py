@@ -308,3 +308,16 @@ def test_grouped_wgrad_and_colsum(G, M, N, Kd):
     kk.colsum_grouped(dys, outs)
     for i in range(G):
         _close(outs[i], dys[i].float().sum(0), 1e-3, f"grouped colsum {i}")
+
+
+def test_gemm_library_beta_accumulate():
+    """hipBLASLt candidate for C += A B (bf16) matches the HIP kernel."""
+    M, N, Kd = 512, 256, 384
+    A = _bf(torch.randn(M, Kd)).to(DEV)
+    B = _bf(torch.randn(Kd, N)).to(DEV)
+    C0 = _bf(torch.randn(M, N)).to(DEV)
+    ref = C0.float() + A.float() @ B.float()
+    for cfg in (kk.BLAS, (8, 1)):
+        C = C0.clone()
+        kk.gemm(A, B, C, M, N, Kd, Kd, N, N, True, False, beta=1.0, cfg=cfg)
+        _close(C, ref, 2e-2, f"beta=1 {cfg}")
