@@ -429,62 +429,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
   if (a.kv_len) klim = min(klim, a.kv_len[b]);
   const float c = a.scale * LOG2E;
 
-  // ---- prologue: Q, dO, K tiles -> LDS; lse, delta -> LDS
+  // ---- prologue. Every global load is issued before any is used (one
+  // memory latency): this wave's K / V register fragments for phase 1, the
+  // Q / dO / K tile chunks, O chunks for delta, and lse.
   const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
   const bf16_t* kbp = a.k + b * a.k_sb + h * a.k_sh;
-  {
-    constexpr int CPR = HD / 8;
-    constexpr int TOTAL = R * CPR;
-#pragma unroll
-    for (int i = 0; i < (TOTAL + 511) / 512; ++i) {
-      const int id = tid + i * 512;
-      if (TOTAL % 512 != 0 && id >= TOTAL) break;
-      const int row = id / CPR, cc = id % CPR;
-      short8_t vq = {0, 0, 0, 0, 0, 0, 0, 0}, vo = vq, vk = vq;
-      if (row < a.Lq) {
-        vq = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
-        vo = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
-      }
-      if (row < a.Lk) vk = *reinterpret_cast<const short8_t*>(kbp + (long long)row * a.k_sl + cc * 8);
-      *reinterpret_cast<short8_t*>(ldsQ + T::off(row, cc * 16)) = vq;
-      *reinterpret_cast<short8_t*>(ldsO + T::off(row, cc * 16)) = vo;
-      *reinterpret_cast<short8_t*>(ldsK + T::off(row, cc * 16)) = vk;
-    }
-    // delta[q] = sum_d dO[q][d] * O[q][d]: 4 threads per row
-    const int row = tid >> 2, part = tid & 3;
-    float d = 0.f;
-    if (row < a.Lq) {
-      const bf16_t* op = a.o + b * a.o_sb + (long long)row * a.o_sl + h * a.o_sh;
-      const bf16_t* dp = ob + (long long)row * a.do_sl;
-#pragma unroll
-      for (int e0 = part * 8; e0 < HD; e0 += 32) {
-        const short8_t x = *reinterpret_cast<const short8_t*>(op + e0);
-        const short8_t y = *reinterpret_cast<const short8_t*>(dp + e0);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)x[e]) * bf2f((bf16_t)y[e]);
-      }
-    }
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    if (part == 0) {
-      ldsD[row] = row < a.Lq ? d : 0.f;
-      ldsL[row] = row < a.Lq ? a.lse[((long long)b * a.H + h) * a.Lq + row] : INFINITY;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 1: this wave's 16 keys against all queries
+  const bf16_t* obo = a.o + b * a.o_sb + h * a.o_sh;
   const int key = 16 * w + cl;
-  const bool kvalid = key < klim;
-  const bool active = 16 * w < klim;  // wave-uniform
-  f32x4 dk[T::DT], dv[T::DT];
-#pragma unroll
-  for (int i = 0; i < T::DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // P and dS of [q = 16t + 4g + r][key], packed to bf16 pairs as produced
-  uint32_t pk[8][2], dk2[8][2];
-  if (active) {
-    short8_t kf[T::KS], vf[T::KS];
+  short8_t kf[T::KS], vf[T::KS];
+  {
     const int krow = min(key, a.Lk - 1);
     const bf16_t* kp = kbp + (long long)krow * a.k_sl;
     const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
@@ -493,6 +447,58 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
       kf[ks] = gfrag<HD>(kp, key < a.Lk, ks, lane);
       vf[ks] = gfrag<HD>(vp, key < a.Lk, ks, lane);
     }
+  }
+  {
+    constexpr int CPR = HD / 8;  // 16-byte chunks per row
+    constexpr int TOTAL = R * CPR;
+    constexpr int NI = (TOTAL + 511) / 512;
+    short8_t vq[NI], vo[NI], vk[NI], vx[NI];
+    const short8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int id = tid + i * 512;
+      const int row = id / CPR, cc = id % CPR;
+      vq[i] = vo[i] = vk[i] = vx[i] = z;
+      if (id < TOTAL && row < a.Lq) {
+        vq[i] = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
+        vo[i] = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
+        vx[i] = *reinterpret_cast<const short8_t*>(obo + (long long)row * a.o_sl + cc * 8);
+      }
+      if (id < TOTAL && row < a.Lk)
+        vk[i] = *reinterpret_cast<const short8_t*>(kbp + (long long)row * a.k_sl + cc * 8);
+    }
+    const float lse_v = (tid < R && tid < a.Lq) ? a.lse[((long long)b * a.H + h) * a.Lq + tid] : INFINITY;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int id = tid + i * 512;
+      const int row = id / CPR, cc = id % CPR;
+      if (id < TOTAL) {
+        *reinterpret_cast<short8_t*>(ldsQ + T::off(row, cc * 16)) = vq[i];
+        *reinterpret_cast<short8_t*>(ldsO + T::off(row, cc * 16)) = vo[i];
+        *reinterpret_cast<short8_t*>(ldsK + T::off(row, cc * 16)) = vk[i];
+      }
+      // delta[row] = sum_d dO * O: partial over this chunk, then over the
+      // CPR consecutive lanes holding the row (xor shuffles)
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)vo[i][e]) * bf2f((bf16_t)vx[i][e]);
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) d += __shfl_xor(d, o, 64);
+      if (id < TOTAL && cc == 0) ldsD[row] = row < a.Lq ? d : 0.f;
+    }
+    if (tid < R) ldsL[tid] = lse_v;
+  }
+  __syncthreads();
+
+  // ---- phase 1: this wave's 16 keys against all queries
+  const bool kvalid = key < klim;
+  const bool active = 16 * w < klim;  // wave-uniform
+  f32x4 dk[T::DT], dv[T::DT];
+#pragma unroll
+  for (int i = 0; i < T::DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // P and dS of [q = 16t + 4g + r][key], packed to bf16 pairs as produced
+  uint32_t pk[8][2], dk2[8][2];
+  if (active) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
