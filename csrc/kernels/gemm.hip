@@ -422,6 +422,204 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// 256x256-tile NT GEMM (both operands K-contiguous): 8 waves as 2 (M) x 4 (N),
+// each wave a 128 x 64 block = 8 x 4 MFMA subtiles. A K-tile (64 deep) is
+// processed in four phases, one output quadrant of every wave (4 x 2 subtiles
+// x 2 k-steps = 16 MFMAs) each: (a0,b0) (a0,b1) (a1,b1) (a1,b0), where a0/a1
+// are the upper/lower 64 rows of a wave's block and b0/b1 its left/right 32
+// columns. So each phase reads only the operand half it adds (8 or 4
+// ds_read_b128) and a K-tile's fragments stay in registers.
+// The LDS-DMA stages the next K-tile one half-tile per phase, in consumption
+// order: A-half 0 (the a0 rows of both wave rows), B-half 0, B-half 1, A-half 1
+// -- i.e. a half-tile is a set of 128 non-contiguous rows (2 x 64 of A, 4 x 32
+// of B), remapped on the global side. A phase that needs a new half waits
+// vmcnt(4) (the two younger halves stay in flight) + one barrier; two LDS
+// buffers. MFMA groups run at raised wave priority.
+// Used for the large-N shapes (FFN up-projection, fused QKV, cross K/V,
+// vocabulary projection): 128 FLOP per LDS byte vs 64 for 128x128 tiles.
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm256_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+    float beta) {
+  constexpr int BM = 256, BN = 256, NW = 8;
+  constexpr int HB = 128 * BK * 2;  // bytes of one half-tile image (128 rows x 128 B)
+  constexpr int SB = 4 * HB;        // stage: A-half0, A-half1, B-half0, B-half1
+  using GH = Glds<true, 128, NW>;   // per half-tile: 2 LDS-DMA per wave
+  static_assert(GH::P == 2, "half-tile = 2 pieces per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / BK;  // host guarantees K % 64 == 0
+
+  GH gh;
+  gh.init(wid, lane);
+  // LDS image row r (0..127) of a half-tile <- global row of the tile:
+  //   A-half hA: (r / 64) * 128 + hA * 64 + r % 64
+  //   B-half hB: (r / 32) * 64 + hB * 32 + r % 32
+  int ga_row[2][GH::P], gb_row[2][GH::P];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < GH::P; ++i) {
+      const int r = gh.row[i];
+      ga_row[hh][i] = (r >> 6) * 128 + hh * 64 + (r & 63);
+      gb_row[hh][i] = (r >> 5) * 64 + hh * 32 + (r & 31);
+    }
+  auto issue = [&](const bf16_t* X, int ld, int len, int base, const int* rows, int k0, char* dst) {
+#pragma unroll
+    for (int i = 0; i < GH::P; ++i) {
+      int mn = base + rows[i];
+      mn = mn < len ? mn : len - 1;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(X + (long long)mn * ld + k0 + gh.col[i]),
+          (__attribute__((address_space(3))) void*)(dst + (wid * GH::P + i) * 1024), 16, 0, 0);
+    }
+  };
+  // half h of K-tile kt: 0 = A-half0, 1 = B-half0, 2 = B-half1, 3 = A-half1
+  auto issue_half = [&](int kt, int h) {
+    char* st = smem + (kt & 1) * SB;
+    const int k0 = kt * BK;
+    if (h == 0) issue(A, lda, M, m0, ga_row[0], k0, st + 0 * HB);
+    else if (h == 1) issue(B, ldb, N, n0, gb_row[0], k0, st + 2 * HB);
+    else if (h == 2) issue(B, ldb, N, n0, gb_row[1], k0, st + 3 * HB);
+    else issue(A, lda, M, m0, ga_row[1], k0, st + 1 * HB);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue_half(0, h);
+
+  // this wave's rows inside the half-tile images: a-subtile i (0..3) of
+  // half hA at row wm*64 + 16i; b-subtile j (0..1) of half hB at wn*32 + 16j
+  const int arow = wm * 64, brow = wn * 32;
+  short8_t fa[8][2], fb[4][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * SB;
+    const bool more = kt + 1 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      if (ph < 3) {
+        if (more) wait_vmcnt<4>();
+        else wait_vmcnt<0>();
+        lds_barrier();
+      }
+      if (ph == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<true, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<true, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
+      } else if (ph == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<true, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
+      } else if (ph == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<true, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
+      }
+      if (more) issue_half(kt + 1, ph);
+      const int i0 = (ph < 2) ? 0 : 4;
+      const int j0 = (ph == 0 || ph == 3) ? 0 : 2;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i0 + i][j0 + j] = mfma16(fa[i0 + i][s2], fb[j0 + j][s2], acc[i0 + i][j0 + j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // ---------------- epilogue: two 64-row halves through a per-wave LDS image
+  using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
+  constexpr int ES = sizeof(OutT);
+  constexpr int WTN = 64;
+  constexpr int SROW = WTN * ES + 16;
+  constexpr int EPC = 16 / ES;
+  constexpr int CPR = WTN / EPC;
+  wait_vmcnt<0>();
+  lds_barrier();
+  char* wimg = smem + wid * (64 * SROW);
+  const int g = lane >> 4, cl = lane & 15;
+  OutT* C = reinterpret_cast<OutT*>(Cv);
+  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + 16 * j + cl;
+      float bn = 0.f;
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = alpha * acc[4 * hf + i][j][r];
+          if constexpr (EPI == EPI_BIAS) v += bn;
+          if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v + bn, 0.f);
+          OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * ES);
+          if constexpr (OUT_F32) *dst = v;
+          else *dst = f2bf(v);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int tt = 0; tt < (64 * CPR) / 64; ++tt) {
+      const int id = lane + 64 * tt;
+      const int row = id / CPR, ch = id % CPR;
+      const int m = m0 + wm * 128 + hf * 64 + row;
+      const int n = n0 + wn * 64 + ch * EPC;
+      if (m >= M || n >= N) continue;
+      OutT vals[EPC];
+      *reinterpret_cast<int4*>(vals) = *reinterpret_cast<const int4*>(wimg + row * SROW + ch * 16);
+      OutT* cp = C + (size_t)m * ldc + n;
+      if (vec_ok && n + EPC <= N && beta == 0.f) {
+        *reinterpret_cast<int4*>(cp) = *reinterpret_cast<const int4*>(vals);
+      } else {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          if (n + e >= N) break;
+          OutT v = vals[e];
+          if (beta != 0.f) {
+            if constexpr (OUT_F32) v += beta * cp[e];
+            else v = f2bf(bf2f(v) + beta * bf2f(cp[e]));
+          }
+          cp[e] = v;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before rewrite
+  }
+}
+
 // Split-K reduction: C = sum_z slab[z] (+beta*C) with the epilogue.
 template <int EPI, bool OUT_F32>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, void* __restrict__ Cv,
@@ -604,11 +802,37 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
   }
 }
 
+template <int EPI, bool F32>
+int launch_256(const bf16_t* A, const bf16_t* B, void* C, const float* bias, int M, int N, int K,
+               int lda, int ldb, int ldc, float alpha, float beta, hipStream_t st) {
+  if (K % BK != 0) return -3;
+  constexpr int stages = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
+  constexpr int img = 8 * 64 * (64 * (F32 ? 4 : 2) + 16);
+  constexpr int lds = stages > img ? stages : img;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm256_kernel<EPI, F32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int tiles = cdiv(M, 256) * cdiv(N, 256);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, F32>), dim3(tiles), dim3(512), lds, st, A, B, C, bias,
+                     M, N, K, lda, ldb, ldc, alpha, beta);
+  return 0;
+}
+
 template <bool AK, bool BKc, int EPI, bool F32>
 void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const float* bias,
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st,
                   const GemmGroup* grp = nullptr, int G = 1) {
+  if constexpr (AK && BKc && EPI != EPI_DRELU) {
+    // 256x256 tiles (K % 64 == 0, no split / group); otherwise cfg 0
+    if (tile_cfg == 12 && splits <= 1 && G == 1 &&
+        launch_256<EPI, F32>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, beta, st) == 0)
+      return;
+    if (tile_cfg == 12) tile_cfg = 0;
+  }
 #define TDG_CFG(ID, BM_, BN_, WM_, WN_, ST_)                                                  \
   case ID:                                                                                    \
     launch_cfg<BM_, BN_, WM_, WN_, ST_, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, \

@@ -1,0 +1,14 @@
+#!/usr/bin/env python3
+"""Run the attention fwd+bwd of the base shape repeatedly (for PMC collection)."""
+import os, sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+B, H, L, hd = 64, 8, 128, 64
+q, k, v, do = (torch.randn(B, L, H, hd, device="cuda").bfloat16() for _ in range(4))
+kv = torch.full((B,), L, dtype=torch.int32, device="cuda")
+for _ in range(20):
+    o, lse = kk.attn_fwd(q, k, v, kv, 0.125, False)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, False)
+torch.cuda.synchronize()

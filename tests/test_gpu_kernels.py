@@ -31,8 +31,8 @@ def _close(a, b, tol, what):
 
 # --------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 7010, 128),
-                                   (64, 64, 4096), (130, 520, 1000)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+                                   (64, 64, 4096), (130, 520, 1000), (1024, 2048, 512), (300, 600, 192)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 12])
 def test_gemm_forward_bias_relu(M, N, K, cfg):
     x = _bf(_rand(M, K, seed=1))
     w = _bf(_rand(N, K, scale=0.5, seed=2))
