@@ -46,6 +46,9 @@ int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* pa
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
                      int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc, int out_f32,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
+int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
+                    const int* shapes, int K, int a_kc, int b_kc, int out_f32, float alpha,
+                    float beta, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
@@ -492,6 +495,48 @@ void gemm_grouped(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
   check_err(rc, "tdg gemm_grouped");
 }
 
+// Ragged grouped GEMM (256x256 tiles): problems i = (As[i], Bs[i], Cs[i]) with
+// shapes[i] = (M, N, lda, ldb, ldc), sharing K and the operand layouts.
+void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
+                 const std::vector<Tensor>& Cs, const std::vector<int64_t>& shapes, int64_t K,
+                 bool a_kc, bool b_kc, double alpha, double beta) {
+  const size_t P = As.size();
+  TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && shapes.size() == 5 * P,
+              "gemm_ragged: 1..64 problems, 5 shape values each");
+  TORCH_CHECK(K > 0 && K % 64 == 0, "gemm_ragged: K must be a multiple of 64");
+  auto r8 = [](int64_t v) { return (v + 7) / 8 * 8; };
+  const bool f32 = Cs[0].scalar_type() == at::kFloat;
+  std::vector<const void*> a(P), b(P);
+  std::vector<void*> c(P);
+  std::vector<int> sh(5 * P);
+  for (size_t i = 0; i < P; ++i) {
+    const int64_t M = shapes[5 * i], N = shapes[5 * i + 1], lda = shapes[5 * i + 2],
+                  ldb = shapes[5 * i + 3], ldc = shapes[5 * i + 4];
+    TORCH_CHECK(M > 0 && N > 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc >= N, "gemm_ragged: shape");
+    check_bf16(As[i], "A");
+    check_bf16(Bs[i], "B");
+    TORCH_CHECK(Cs[i].is_cuda() && (Cs[i].scalar_type() == at::kFloat) == f32 &&
+                    (f32 || Cs[i].scalar_type() == at::kBFloat16),
+                "gemm_ragged: C dtypes must match (f32 or bf16)");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(As[i].data_ptr()) % 16) == 0 &&
+                    (reinterpret_cast<uintptr_t>(Bs[i].data_ptr()) % 16) == 0,
+                "gemm_ragged: A/B must be 16-byte aligned");
+    if (a_kc) check_extent(As[i], M, lda, r8(K), "A");
+    else check_extent(As[i], K, lda, r8(M), "A");
+    if (b_kc) check_extent(Bs[i], N, ldb, r8(K), "B");
+    else check_extent(Bs[i], K, ldb, r8(N), "B");
+    check_extent(Cs[i], M, ldc, N, "C");
+    a[i] = As[i].data_ptr();
+    b[i] = Bs[i].data_ptr();
+    c[i] = Cs[i].data_ptr();
+    for (int j = 0; j < 5; ++j) sh[5 * i + j] = (int)shapes[5 * i + j];
+  }
+  c10::DeviceGuard g(As[0].device());
+  const int rc = tdg_gemm_ragged(a.data(), b.data(), c.data(), (int)P, sh.data(), (int)K, a_kc,
+                                 b_kc, f32, (float)alpha, (float)beta, stream_of(As[0]));
+  check_err(rc, "tdg gemm_ragged");
+}
+
 void colsum_grouped(const std::vector<Tensor>& Xs, const std::vector<Tensor>& outs,
                     const Tensor& part, int64_t M, int64_t N, int64_t ld, int64_t rows_per_block,
                     double beta) {
@@ -667,6 +712,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
   m.def("gemm_grouped", &gemm_grouped);
+  m.def("gemm_ragged", &gemm_ragged);
   m.def("colsum_grouped", &colsum_grouped);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);

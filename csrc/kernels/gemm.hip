@@ -423,81 +423,130 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// 256x256-tile NT GEMM (both operands K-contiguous): 8 waves as 2 (M) x 4 (N),
-// each wave a 128 x 64 block = 8 x 4 MFMA subtiles. A K-tile (64 deep) is
-// processed in four phases, one output quadrant of every wave (4 x 2 subtiles
-// x 2 k-steps = 16 MFMAs) each: (a0,b0) (a0,b1) (a1,b1) (a1,b0), where a0/a1
-// are the upper/lower 64 rows of a wave's block and b0/b1 its left/right 32
-// columns. So each phase reads only the operand half it adds (8 or 4
-// ds_read_b128) and a K-tile's fragments stay in registers.
+// 256x256-tile GEMM, any operand layout: 8 waves as 2 (M) x 4 (N), each wave a
+// 128 x 64 block = 8 x 4 MFMA subtiles. A K-tile (64 deep) is processed in
+// four phases, one output quadrant of every wave (4 x 2 subtiles x 2 k-steps =
+// 16 MFMAs) each: (a0,b0) (a0,b1) (a1,b1) (a1,b0), where a0/a1 are the
+// upper/lower 64 rows of a wave's block and b0/b1 its left/right 32 columns.
+// So each phase reads only the operand half it adds and a K-tile's fragments
+// stay in registers.
 // The LDS-DMA stages the next K-tile one half-tile per phase, in consumption
 // order: A-half 0 (the a0 rows of both wave rows), B-half 0, B-half 1, A-half 1
-// -- i.e. a half-tile is a set of 128 non-contiguous rows (2 x 64 of A, 4 x 32
-// of B), remapped on the global side. A phase that needs a new half waits
+// -- i.e. a half-tile is a set of 128 non-contiguous rows / columns (2 x 64 of
+// A, 4 x 32 of B), remapped on the global side. A half-tile image is 16 KiB in
+// either layout (K-contiguous: 128 rows x 64 k; MN-contiguous: 64 k x 128
+// columns, read with ds_read_b64_tr_b16). A phase that needs a new half waits
 // vmcnt(4) (the two younger halves stay in flight) + one barrier; two LDS
 // buffers. MFMA groups run at raised wave priority.
-// Used for the large-N shapes (FFN up-projection, fused QKV, cross K/V,
-// vocabulary projection): 128 FLOP per LDS byte vs 64 for 128x128 tiles.
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm256_kernel(
-    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
-    const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-    float beta) {
-  constexpr int BM = 256, BN = 256, NW = 8;
-  constexpr int HB = 128 * BK * 2;  // bytes of one half-tile image (128 rows x 128 B)
+//
+// Ragged grouping: one launch covers up to R256_MAXP problems in up to
+// R256_MAXC shape classes sharing K (the deferred weight gradients of a whole
+// model: 60+ long-K problems of 5 shapes -> ~700 tiles, one launch, no split-K).
+// 128 FLOP per LDS byte vs 64 for 128x128 tiles.
+constexpr int R256_MAXP = 64, R256_MAXC = 8;
+struct R256Class {
+  int M, N, lda, ldb, ldc, tiles_m, tiles_n, tile_start, prob_start;
+};
+struct R256Args {
+  const bf16_t* A[R256_MAXP];
+  const bf16_t* B[R256_MAXP];
+  void* C[R256_MAXP];
+  R256Class cls[R256_MAXC];
+  int ncls;
+};
+
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
+                                                      const float* __restrict__ bias,
+                                                      const bf16_t* __restrict__ aux, int K,
+                                                      int ldaux, float alpha, float beta) {
+  constexpr int NW = 8;
+  constexpr int HB = 128 * BK * 2;  // bytes of one half-tile image
   constexpr int SB = 4 * HB;        // stage: A-half0, A-half1, B-half0, B-half1
-  using GH = Glds<true, 128, NW>;   // per half-tile: 2 LDS-DMA per wave
-  static_assert(GH::P == 2, "half-tile = 2 pieces per wave");
+  using GA = Glds<A_KC, 128, NW>;
+  using GB = Glds<B_KC, 128, NW>;
+  static_assert(GA::P == 2 && GB::P == 2, "half-tile = 2 pieces per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
-  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+
+  // ragged tile id -> (class, problem, tile); class fields picked with
+  // constant indices (scalar selects, no private copy of the argument block)
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  R256Class cl = args.cls[0];
+#pragma unroll
+  for (int i = 1; i < R256_MAXC; ++i)
+    if (i < args.ncls && t0 >= args.cls[i].tile_start) cl = args.cls[i];
+  const int M = cl.M, N = cl.N, lda = cl.lda, ldb = cl.ldb, ldc = cl.ldc;
+  const int tpp = cl.tiles_m * cl.tiles_n;
+  const int lt = t0 - cl.tile_start;
+  const int p = cl.prob_start + lt / tpp;
+  const int t = lt % tpp;
+  const bf16_t* __restrict__ A = args.A[p];
+  const bf16_t* __restrict__ B = args.B[p];
+  void* __restrict__ Cv = args.C[p];
   int tm, tn;
-  if (tiles_n <= tiles_m) {
-    tn = t % tiles_n;
-    tm = t / tiles_n;
+  if (cl.tiles_n <= cl.tiles_m) {
+    tn = t % cl.tiles_n;
+    tm = t / cl.tiles_n;
   } else {
-    tm = t % tiles_m;
-    tn = t / tiles_m;
+    tm = t % cl.tiles_m;
+    tn = t / cl.tiles_m;
   }
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * 256, n0 = tn * 256;
   const int nk = K / BK;  // host guarantees K % 64 == 0
 
-  GH gh;
-  gh.init(wid, lane);
-  // LDS image row r (0..127) of a half-tile <- global row of the tile:
-  //   A-half hA: (r / 64) * 128 + hA * 64 + r % 64
-  //   B-half hB: (r / 32) * 64 + hB * 32 + r % 32
-  int ga_row[2][GH::P], gb_row[2][GH::P];
+  GA ga;
+  GB gb;
+  ga.init(wid, lane);
+  gb.init(wid, lane);
+  // Image row/column x (0..127) of a half-tile <- tile row/column:
+  //   A-half hA: (x / 64) * 128 + hA * 64 + x % 64
+  //   B-half hB: (x / 32) * 64 + hB * 32 + x % 32
+  // (KC images remap rows, MC images remap 8-element column chunks.)
+  int a_mn[2][2], b_mn[2][2], a_k[2], b_k[2];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
+  for (int i = 0; i < 2; ++i) {
+    const int xa = A_KC ? ga.row[i] : ga.col[i];
+    const int xb = B_KC ? gb.row[i] : gb.col[i];
+    a_k[i] = A_KC ? ga.col[i] : ga.row[i];
+    b_k[i] = B_KC ? gb.col[i] : gb.row[i];
 #pragma unroll
-    for (int i = 0; i < GH::P; ++i) {
-      const int r = gh.row[i];
-      ga_row[hh][i] = (r >> 6) * 128 + hh * 64 + (r & 63);
-      gb_row[hh][i] = (r >> 5) * 64 + hh * 32 + (r & 31);
+    for (int hh = 0; hh < 2; ++hh) {
+      a_mn[hh][i] = (xa >> 6) * 128 + hh * 64 + (xa & 63);
+      b_mn[hh][i] = (xb >> 5) * 64 + hh * 32 + (xb & 31);
     }
-  auto issue = [&](const bf16_t* X, int ld, int len, int base, const int* rows, int k0, char* dst) {
+  }
+  auto issue = [&](auto kc, const bf16_t* X, int ld, int len, int base, const int* mns,
+                   const int* ks, int k0, char* dst) {
 #pragma unroll
-    for (int i = 0; i < GH::P; ++i) {
-      int mn = base + rows[i];
-      mn = mn < len ? mn : len - 1;
+    for (int i = 0; i < 2; ++i) {
+      int mn = base + mns[i];
+      long long off;
+      if constexpr (decltype(kc)::value) {
+        mn = mn < len ? mn : len - 1;
+        off = (long long)mn * ld + k0 + ks[i];
+      } else {
+        mn = mn < len ? mn : 0;  // never stored
+        off = (long long)(k0 + ks[i]) * ld + mn;
+      }
       __builtin_amdgcn_global_load_lds(
-          (const void*)(X + (long long)mn * ld + k0 + gh.col[i]),
-          (__attribute__((address_space(3))) void*)(dst + (wid * GH::P + i) * 1024), 16, 0, 0);
+          (const void*)(X + off),
+          (__attribute__((address_space(3))) void*)(dst + (wid * 2 + i) * 1024), 16, 0, 0);
     }
   };
+  using AKC = std::integral_constant<bool, A_KC>;
+  using BKC = std::integral_constant<bool, B_KC>;
   // half h of K-tile kt: 0 = A-half0, 1 = B-half0, 2 = B-half1, 3 = A-half1
   auto issue_half = [&](int kt, int h) {
     char* st = smem + (kt & 1) * SB;
     const int k0 = kt * BK;
-    if (h == 0) issue(A, lda, M, m0, ga_row[0], k0, st + 0 * HB);
-    else if (h == 1) issue(B, ldb, N, n0, gb_row[0], k0, st + 2 * HB);
-    else if (h == 2) issue(B, ldb, N, n0, gb_row[1], k0, st + 3 * HB);
-    else issue(A, lda, M, m0, ga_row[1], k0, st + 1 * HB);
+    if (h == 0) issue(AKC{}, A, lda, M, m0, a_mn[0], a_k, k0, st + 0 * HB);
+    else if (h == 1) issue(BKC{}, B, ldb, N, n0, b_mn[0], b_k, k0, st + 2 * HB);
+    else if (h == 2) issue(BKC{}, B, ldb, N, n0, b_mn[1], b_k, k0, st + 3 * HB);
+    else issue(AKC{}, A, lda, M, m0, a_mn[1], a_k, k0, st + 1 * HB);
   };
 
   f32x4 acc[8][4];
@@ -509,8 +558,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue_half(0, h);
 
-  // this wave's rows inside the half-tile images: a-subtile i (0..3) of
-  // half hA at row wm*64 + 16i; b-subtile j (0..1) of half hB at wn*32 + 16j
+  // this wave's rows/columns inside the half-tile images: a-subtile i (0..3)
+  // of half hA at wm*64 + 16i; b-subtile j (0..1) of half hB at wn*32 + 16j
   const int arow = wm * 64, brow = wn * 32;
   short8_t fa[8][2], fb[4][2];
   for (int kt = 0; kt < nk; ++kt) {
@@ -527,21 +576,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<true, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
+          for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<A_KC, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<true, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
+          for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<B_KC, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
       } else if (ph == 1) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<true, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
+          for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<B_KC, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
       } else if (ph == 2) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<true, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
+          for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
       }
       if (more) issue_half(kt + 1, ph);
       const int i0 = (ph < 2) ? 0 : 4;
@@ -568,14 +617,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(
   wait_vmcnt<0>();
   lds_barrier();
   char* wimg = smem + wid * (64 * SROW);
-  const int g = lane >> 4, cl = lane & 15;
+  const int g = lane >> 4, cl16 = lane & 15;
   OutT* C = reinterpret_cast<OutT*>(Cv);
-  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                      (EPI != EPI_DRELU ||
+                       ((ldaux % 8) == 0 && (reinterpret_cast<uintptr_t>(aux) & 15) == 0));
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + 16 * j + cl;
+      const int n = n0 + wn * 64 + 16 * j + cl16;
       float bn = 0.f;
       if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
 #pragma unroll
@@ -585,7 +636,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(
           float v = alpha * acc[4 * hf + i][j][r];
           if constexpr (EPI == EPI_BIAS) v += bn;
           if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v + bn, 0.f);
-          OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * ES);
+          OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl16) * ES);
           if constexpr (OUT_F32) *dst = v;
           else *dst = f2bf(v);
         }
@@ -601,13 +652,31 @@ __global__ __launch_bounds__(512) void gemm256_kernel(
       OutT vals[EPC];
       *reinterpret_cast<int4*>(vals) = *reinterpret_cast<const int4*>(wimg + row * SROW + ch * 16);
       OutT* cp = C + (size_t)m * ldc + n;
-      if (vec_ok && n + EPC <= N && beta == 0.f) {
+      if (vec_ok && n + EPC <= N) {
+        if constexpr (EPI == EPI_DRELU) {
+          const short8_t x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e)
+            if (!(bf2f((bf16_t)x[e * (8 / EPC)]) > 0.f)) vals[e] = OutT(0);
+        }
+        if (beta != 0.f) {
+          OutT old[EPC];
+          *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            if constexpr (OUT_F32) vals[e] += beta * old[e];
+            else vals[e] = f2bf(bf2f(vals[e]) + beta * bf2f(old[e]));
+          }
+        }
         *reinterpret_cast<int4*>(cp) = *reinterpret_cast<const int4*>(vals);
       } else {
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
           if (n + e >= N) break;
           OutT v = vals[e];
+          if constexpr (EPI == EPI_DRELU) {
+            if (!(bf2f(aux[(size_t)m * ldaux + n + e]) > 0.f)) v = OutT(0);
+          }
           if (beta != 0.f) {
             if constexpr (OUT_F32) v += beta * cp[e];
             else v = f2bf(bf2f(v) + beta * bf2f(cp[e]));
@@ -802,23 +871,53 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
   }
 }
 
-template <int EPI, bool F32>
-int launch_256(const bf16_t* A, const bf16_t* B, void* C, const float* bias, int M, int N, int K,
-               int lda, int ldb, int ldc, float alpha, float beta, hipStream_t st) {
-  if (K % BK != 0) return -3;
-  constexpr int stages = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
-  constexpr int img = 8 * 64 * (64 * (F32 ? 4 : 2) + 16);
-  constexpr int lds = stages > img ? stages : img;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)gemm256_kernel<EPI, F32>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+// Which (layout, epilogue) combinations have a 256x256 instantiation:
+// forward NT (plain / bias / bias+relu), dgrad NN (plain / relu-backward),
+// wgrad TN (f32 or bf16 out).
+template <bool AK, bool BKc, int EPI, bool F32>
+constexpr bool has_256() {
+  if (AK && BKc) return EPI != EPI_DRELU;
+  if (AK && !BKc) return !F32 && (EPI == EPI_NONE || EPI == EPI_DRELU);
+  if (!AK && !BKc) return EPI == EPI_NONE;
+  return false;
+}
+
+template <bool AK, bool BKc, int EPI, bool F32>
+int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t* aux, int K,
+               int ldaux, float alpha, float beta, hipStream_t st) {
+  if constexpr (!has_256<AK, BKc, EPI, F32>()) {
+    return -4;
+  } else {
+    if (K % BK != 0 || tiles <= 0) return -3;
+    constexpr int stages = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
+    constexpr int img = 8 * 64 * (64 * (F32 ? 4 : 2) + 16);
+    constexpr int lds = stages > img ? stages : img;
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds, st, args,
+                       bias, aux, K, ldaux, alpha, beta);
+    return 0;
   }
-  const int tiles = cdiv(M, 256) * cdiv(N, 256);
-  hipLaunchKernelGGL((gemm256_kernel<EPI, F32>), dim3(tiles), dim3(512), lds, st, A, B, C, bias,
-                     M, N, K, lda, ldb, ldc, alpha, beta);
-  return 0;
+}
+
+// One shape class of G problems (G == 1: a plain GEMM). Returns the tile count.
+inline int r256_single(R256Args& a, const bf16_t* const* A, const bf16_t* const* B,
+                       void* const* C, int G, int M, int N, int lda, int ldb, int ldc) {
+  a.ncls = 1;
+  for (int i = 0; i < G; ++i) {
+    a.A[i] = A[i];
+    a.B[i] = B[i];
+    a.C[i] = C[i];
+  }
+  R256Class& c = a.cls[0];
+  c.M = M; c.N = N; c.lda = lda; c.ldb = ldb; c.ldc = ldc;
+  c.tiles_m = cdiv(M, 256); c.tiles_n = cdiv(N, 256);
+  c.tile_start = 0; c.prob_start = 0;
+  return G * c.tiles_m * c.tiles_n;
 }
 
 template <bool AK, bool BKc, int EPI, bool F32>
@@ -826,12 +925,20 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st,
                   const GemmGroup* grp = nullptr, int G = 1) {
-  if constexpr (AK && BKc && EPI != EPI_DRELU) {
-    // 256x256 tiles (K % 64 == 0, no split / group); otherwise cfg 0
-    if (tile_cfg == 12 && splits <= 1 && G == 1 &&
-        launch_256<EPI, F32>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, beta, st) == 0)
-      return;
-    if (tile_cfg == 12) tile_cfg = 0;
+  if (tile_cfg == 12) {
+    // 256x256 tiles (K % 64 == 0, no split-K; MN-contiguous operands need
+    // ld % 8 == 0); otherwise cfg 0
+    if (splits <= 1 && (AK || lda % 8 == 0) && (BKc || ldb % 8 == 0)) {
+      R256Args args{};
+      const bf16_t* a1 = A;
+      const bf16_t* b1 = B;
+      void* c1 = C;
+      const int tiles = grp ? r256_single(args, grp->A, grp->B, grp->C, G, M, N, lda, ldb, ldc)
+                            : r256_single(args, &a1, &b1, &c1, 1, M, N, lda, ldb, ldc);
+      if (launch_256<AK, BKc, EPI, F32>(args, tiles, bias, aux, K, ldaux, alpha, beta, st) == 0)
+        return;
+    }
+    tile_cfg = 0;
   }
 #define TDG_CFG(ID, BM_, BN_, WM_, WN_, ST_)                                                  \
   case ID:                                                                                    \
@@ -926,6 +1033,45 @@ extern "C" int tdg_gemm_grouped(const void* const* A, const void* const* B, void
   if (!a_kc && !b_kc) { if (out_f32) { TDG_GR(false, false, true) } else { TDG_GR(false, false, false) } }
   if (out_f32) { TDG_GR(false, true, true) } else { TDG_GR(false, true, false) }
 #undef TDG_GR
+}
+
+// Ragged grouped GEMM: P (<= 64) problems sharing K and layout, in runs of
+// equal shape (<= 8 distinct shapes), plain epilogue, ONE launch of 256x256
+// tiles. shapes[5*i..] = (M, N, lda, ldb, ldc) of problem i. Returns 0 on
+// success.
+extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
+                               const int* shapes, int K, int a_kc, int b_kc, int out_f32,
+                               float alpha, float beta, hipStream_t st) {
+  if (P < 1 || P > R256_MAXP) return -2;
+  R256Args args{};
+  int ncls = 0, tiles = 0;
+  for (int i = 0; i < P; ++i) {
+    const int* s = shapes + 5 * i;
+    const bool same = ncls > 0 && args.cls[ncls - 1].M == s[0] && args.cls[ncls - 1].N == s[1] &&
+                      args.cls[ncls - 1].lda == s[2] && args.cls[ncls - 1].ldb == s[3] &&
+                      args.cls[ncls - 1].ldc == s[4];
+    if (!same) {
+      if (ncls == R256_MAXC) return -5;
+      R256Class& c = args.cls[ncls++];
+      c.M = s[0]; c.N = s[1]; c.lda = s[2]; c.ldb = s[3]; c.ldc = s[4];
+      c.tiles_m = cdiv(s[0], 256); c.tiles_n = cdiv(s[1], 256);
+      c.tile_start = tiles; c.prob_start = i;
+      if ((!a_kc && s[2] % 8) || (!b_kc && s[3] % 8)) return -6;
+    }
+    const R256Class& c = args.cls[ncls - 1];
+    tiles += c.tiles_m * c.tiles_n;
+    args.A[i] = (const bf16_t*)A[i];
+    args.B[i] = (const bf16_t*)B[i];
+    args.C[i] = C[i];
+  }
+  args.ncls = ncls;
+#define TDG_RG(AK, BKc, F) \
+  return launch_256<AK, BKc, EPI_NONE, F>(args, tiles, nullptr, nullptr, K, 0, alpha, beta, st);
+  if (a_kc && b_kc) { if (out_f32) { TDG_RG(true, true, true) } else { TDG_RG(true, true, false) } }
+  if (a_kc && !b_kc) { TDG_RG(true, false, false) }
+  if (!a_kc && !b_kc) { if (out_f32) { TDG_RG(false, false, true) } else { TDG_RG(false, false, false) } }
+  return -4;
+#undef TDG_RG
 }
 
 extern "C" void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld,

@@ -33,6 +33,7 @@ Reference semantics (distributed_training_transformer/transformer_model.py):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -44,6 +45,9 @@ from tensorflow_distributed_on_gke_amd.ops.streams import offload
 from tensorflow_distributed_on_gke_amd.ops import fp8, philox
 
 LN_EPS = 1e-6
+# deferred weight gradients as ragged 256x256-tile launches (else per-shape
+# grouped launches of the tile table)
+RAGGED_WGRAD = os.environ.get("TDG_WGRAD_RAGGED", "1") != "0"
 
 
 @dataclass
@@ -113,10 +117,11 @@ class WgradQueue:
 
     Nothing in backward reads a weight gradient, so instead of one small
     long-K GEMM per layer (split-K slabs + a reduce kernel, 64x64 tiles to
-    fill the chip) the wgrads of all layers with the same shape run as ONE
-    grouped launch (ops.kernels.wgrad_grouped): e.g. the 24 d x d projections
-    of Transformer-base become 1536 whole-K tiles. Bias column sums and the
-    data-parallel grad_ready notifications follow in backward order."""
+    fill the chip) all of them run as ONE ragged launch of 256x256 whole-K
+    tiles (ops.kernels.wgrad_ragged: 5 shapes, 62 problems, ~730 tiles for
+    Transformer-base), or, with TDG_WGRAD_RAGGED=0, one grouped launch per
+    shape (ops.kernels.wgrad_grouped). Bias column sums and the data-parallel
+    grad_ready notifications follow in backward order."""
 
     def __init__(self, flush_at_boundary: bool = False):
         self.items = []
@@ -133,6 +138,37 @@ class WgradQueue:
         self.items.append((dy2, x2, N, w, b, beta, rt))
 
     def flush(self) -> None:
+        if RAGGED_WGRAD and self._flush_ragged():
+            pass
+        else:
+            self._flush_grouped()
+        self._flush_bias()
+        for dy2, x2, N, w, b, beta, rt in self.items:
+            _ready(rt, w, *([b] if b is not None else []))
+        self.items = []
+
+    def _flush_ragged(self) -> bool:
+        """All weight gradients as ragged launches of 256x256 tiles: one per
+        (token count, beta) -- e.g. the 62 wgrads of Transformer-base are ~730
+        long-K tiles in ONE launch."""
+        runs = {}
+        for it in self.items:
+            dy2, x2, N, w, b, beta, rt = it
+            if x2.shape[0] % 64 or dy2.stride(0) % 8 or x2.stride(0) % 8:
+                return False
+            runs.setdefault((x2.shape[0], beta), {}).setdefault(
+                (N, x2.shape[1], dy2.stride(0), x2.stride(0)), []).append(it)
+        for (_, beta), by_shape in runs.items():
+            shapes = list(by_shape.values())
+            for s0 in range(0, len(shapes), K.RAGGED_MAX_SHAPES):
+                chunk = [it for grp in shapes[s0:s0 + K.RAGGED_MAX_SHAPES] for it in grp]
+                for c0 in range(0, len(chunk), K.RAGGED_MAX_PROBLEMS):
+                    part = chunk[c0:c0 + K.RAGGED_MAX_PROBLEMS]
+                    K.wgrad_ragged([i[0] for i in part], [i[1] for i in part],
+                                   [i[3].grad for i in part], beta)
+        return True
+
+    def _flush_grouped(self) -> None:
         groups = {}
         for it in self.items:
             dy2, x2, N, w, b, beta, rt = it
@@ -148,7 +184,8 @@ class WgradQueue:
                 else:
                     K.wgrad_grouped([i[0] for i in chunk], [i[1] for i in chunk],
                                     [i[3].grad for i in chunk], beta)
-        # bias gradients, grouped by shape as well
+
+    def _flush_bias(self) -> None:
         bgroups = {}
         for dy2, x2, N, w, b, beta, rt in self.items:
             if b is not None:
@@ -160,9 +197,6 @@ class WgradQueue:
                     K.colsum(chunk[0][0], N, chunk[0][1].grad, beta)
                 else:
                     K.colsum_grouped([i[0] for i in chunk], [i[1].grad for i in chunk], beta)
-        for dy2, x2, N, w, b, beta, rt in self.items:
-            _ready(rt, w, *([b] if b is not None else []))
-        self.items = []
 
 
 def _wgrad(rt: RunCtx, dy2, x2, N: int, w: Param, b: Optional[Param] = None) -> None:

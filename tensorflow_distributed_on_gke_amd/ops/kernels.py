@@ -84,7 +84,7 @@ def _autotune(key, run, blas_ok=False) -> Tuple[int, int]:
     M, N, K, a_kc, b_kc = key[:5]
     cands = list(_CANDIDATES)
     if not a_kc and not b_kc:
-        cands = [(c, s) for c in (0, 7, 8) for s in (1, 2, 4, 8) if K // s >= 256]
+        cands = [(c, s) for c in (0, 7, 8) for s in (1, 2, 4, 8) if K // s >= 256] + [(12, 1)]
     if blas_ok:
         cands.append(BLAS)
     times: Dict[Tuple[int, int], float] = {}
@@ -248,7 +248,7 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, N: int, dw: torch.Tensor,
 
 
 _GROUP_TUNED: Dict[tuple, int] = {}
-_GROUP_CANDS = (0, 4, 5, 6, 7, 8, 2)
+_GROUP_CANDS = (0, 4, 5, 6, 7, 8, 2, 12)
 
 
 def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
@@ -293,6 +293,23 @@ def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
             cfg = 0
         _GROUP_TUNED[key] = cfg
     run(cfg)
+
+
+RAGGED_MAX_PROBLEMS, RAGGED_MAX_SHAPES = 64, 8
+
+
+def wgrad_ragged(dys, xs, dws, beta: float = 0.0) -> None:
+    """dws[i][N_i,K_i] (f32) (+)= dys[i][M,N_i]^T @ xs[i][M,K_i] for up to 64
+    problems of up to 8 shapes sharing the token count M, as ONE launch of
+    256x256 tiles (ragged grouping, csrc/kernels/gemm.hip gemm256_kernel).
+    Problems of equal shape must be adjacent."""
+    M = xs[0].shape[0]
+    shapes = []
+    for dy, x, dw in zip(dys, xs, dws):
+        if x.shape[0] != M or dy.shape[0] != M:
+            raise ValueError("wgrad_ragged: all problems must share the token count")
+        shapes += [dw.shape[0], x.shape[1], dy.stride(0), x.stride(0), dw.stride(0)]
+    C().gemm_ragged(list(dys), list(xs), list(dws), shapes, M, False, False, 1.0, beta)
 
 
 def colsum_grouped(xs, outs, beta: float = 0.0) -> None:

@@ -54,8 +54,8 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(out.cpu(), bmat.float().t())
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 128, 512), (300, 96, 200), (8192, 512, 2048)])
-@pytest.mark.parametrize("cfg", [0, 3])
+@pytest.mark.parametrize("M,N,K", [(512, 128, 512), (300, 96, 200), (8192, 512, 2048), (1024, 2048, 512)])
+@pytest.mark.parametrize("cfg", [0, 3, 12])
 def test_gemm_dgrad_drelu(M, N, K, cfg):
     dy = _bf(_rand(M, N, seed=4))
     w = _bf(_rand(N, K, scale=0.5, seed=5))
@@ -85,6 +85,49 @@ def test_gemm_wgrad_f32(M, N, K, splits):
     C().gemm(dy.to(DEV), x.to(DEV), out, None, None, N, K_, M, N, K_, K_, 0, False, False, 0, 1.0, 1.0,
              0, 1, None)
     _close(out, 2 * ref, 2e-3, "gemm wgrad beta=1")
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 1024), (300, 520, 128), (7010, 512, 256)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm256_nn_tn(M, N, K, beta):
+    """256x256 tiles (cfg 12) with MN-contiguous operands: dgrad NN (bf16, beta)
+    and wgrad TN (f32, beta)."""
+    from tensorflow_distributed_on_gke_amd.ops._ext import C
+    ld = (M + 7) // 8 * 8
+    # NN: out[M,N] = dy[M,K] @ w[K,N]
+    dy = _bf(_rand(M, K, seed=21)).to(DEV)
+    w = _bf(_rand(K, N, scale=0.5, seed=22)).to(DEV)
+    out = _bf(_rand(M, N, seed=23)).to(DEV)
+    ref = dy.float() @ w.float() + beta * out.float()
+    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=beta, cfg=(12, 1))
+    _close(out, ref, 1e-2, "gemm256 NN")
+    # TN: dw[M,N] = a[K,M]^T @ x[K,N]  (a stored [K][ld])
+    a = _bf(_rand(K, ld, seed=24)).to(DEV)
+    x = _bf(_rand(K, N, seed=25)).to(DEV)
+    dw = _rand(M, N, seed=26).to(DEV)
+    ref = a[:, :M].float().t() @ x.float() + beta * dw
+    C().gemm(a, x, dw, None, None, M, N, K, ld, N, N, 0, False, False, 0, 1.0, beta, 12, 1, None)
+    _close(dw, ref, 2e-3, "gemm256 TN")
+
+
+def test_wgrad_ragged():
+    """All deferred weight gradients of a model in ONE ragged 256x256 launch:
+    5 shapes (incl. a padded-vocab operand, ld 7040 for 7010 rows), 17 problems."""
+    T = 512
+    spec = [(1536, 512)] * 3 + [(512, 512)] * 6 + [(2048, 512)] * 3 + [(512, 2048)] * 4 + [(7010, 512)]
+    dys, xs, dws, refs = [], [], [], []
+    for i, (n_out, n_in) in enumerate(spec):
+        ldy = 7040 if n_out == 7010 else n_out
+        dy = _bf(_rand(T, ldy, seed=100 + i)).to(DEV)
+        x = _bf(_rand(T, n_in, seed=200 + i)).to(DEV)
+        dw = _rand(n_out, n_in, seed=300 + i).to(DEV)
+        refs.append(dy[:, :n_out].float().t() @ x.float() + dw)
+        dys.append(dy[:, :n_out] if n_out == 7010 else dy)
+        xs.append(x)
+        dws.append(dw)
+    kk.wgrad_ragged(dys, xs, dws, beta=1.0)
+    for i in range(len(spec)):
+        _close(dws[i], refs[i], 2e-3, f"ragged wgrad {i} {spec[i]}")
 
 
 def test_linear_wrappers_padded_vocab():
