@@ -55,9 +55,11 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: FFN forward GEMMs in e4m3 with delayed scaling (BASELINE config 5)")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
+    ap.add_argument("--force-dp", type=int, default=0,
+                    help="1: run the RCCL data-parallel path even with one rank (testing)")
     args = ap.parse_args()
 
-    info = tdist.init_distributed()
+    info = tdist.init_distributed(force=bool(args.force_dp))
     world = info.world
     if world != args.gpus and info.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -66,7 +68,8 @@ def main() -> None:
     model = Transformer(cfg).build(dev, seed=args.seed)
     opt = Adam(model.store, cfg.d_model)
     comm = torch.bfloat16 if args.grad_comm == "bf16" else None
-    ddp = DataParallel(model.store, bucket_mb=args.bucket_mb, comm_dtype=comm) if world > 1 else None
+    ddp = DataParallel(model.store, bucket_mb=args.bucket_mb, comm_dtype=comm,
+                       force=bool(args.force_dp)) if (world > 1 or args.force_dp) else None
     if ddp is not None:
         ddp.broadcast_params(0)
     fp8_state = None

@@ -64,11 +64,15 @@ def plan_buckets(store: ParamStore, bucket_bytes: int) -> List[Bucket]:
 
 class DataParallel:
     def __init__(self, store: ParamStore, bucket_mb: float = 64.0, group=None,
-                 comm_dtype: Optional[torch.dtype] = None, overlap: bool = True):
+                 comm_dtype: Optional[torch.dtype] = None, overlap: bool = True,
+                 force: bool = False):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # `force`: run the collective path with a single rank (tests the RCCL
+        # plumbing on one GPU)
+        self.active = self.world > 1 or (force and dist.is_initialized())
         self.overlap = overlap
         self.comm_dtype = comm_dtype
         self.buckets = plan_buckets(store, int(bucket_mb * 1024 * 1024))
@@ -77,14 +81,14 @@ class DataParallel:
             for pi in b.params:
                 self.bucket_of[pi] = i
         self._comm_bufs = {}
-        if self.world > 1:
+        if self.active:
             store.on_grad_ready(self._on_ready)
         self.reset()
 
     # ------------------------------------------------------------------ init
     def broadcast_params(self, src: int = 0) -> None:
         """Rank `src`'s initial weights to everyone (MWMS variable broadcast)."""
-        if self.world > 1:
+        if self.active:
             dist.broadcast(self.store.flat, src, group=self.group)
             self.store.refresh_compute()
 
@@ -122,7 +126,7 @@ class DataParallel:
         """Launch any bucket not yet reduced and make the current stream wait
         for all of them (device-side wait; no host sync)."""
         join(self.store.flat_grad.device)
-        if self.world <= 1:
+        if not self.active:
             self.reset()
             return
         for b in self.buckets:

@@ -29,7 +29,9 @@ class DistInfo:
         return self.rank == 0
 
 
-def init_distributed(device: str = "auto", timeout_s: float = 900.0) -> DistInfo:
+def init_distributed(device: str = "auto", timeout_s: float = 900.0, force: bool = False) -> DistInfo:
+    """`force`: create the process group even for a single rank (exercises the
+    RCCL data-parallel path on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -39,7 +41,7 @@ def init_distributed(device: str = "auto", timeout_s: float = 900.0) -> DistInfo
         dev = torch.device("cuda", local_rank)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         # RCCL async error handling: a dead peer aborts collectives instead of

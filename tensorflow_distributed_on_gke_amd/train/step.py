@@ -42,7 +42,7 @@ class TrainStep:
         if defer_wgrad is None:
             defer_wgrad = True
         if defer_wgrad and dev.type == "cuda":
-            self.rt.wgrad = WgradQueue(flush_at_boundary=ddp is not None and ddp.world > 1)
+            self.rt.wgrad = WgradQueue(flush_at_boundary=ddp is not None and ddp.active)
         self.fp8 = fp8_state
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
