@@ -121,6 +121,41 @@ __device__ __forceinline__ short4_t lds_read_tr(const void* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p));
 }
 
+// The same read as inline asm, for kernels that stage tiles with LDS-DMA
+// (global_load_lds). The compiler's waitcnt pass treats the builtin above as
+// possibly aliasing every in-flight LDS-DMA and puts an `s_waitcnt vmcnt(0)`
+// in front of it -- which drains the DMA prefetch of the NEXT tile before the
+// current one can be read (measured: the whole multi-stage pipeline collapses
+// to one tile in flight). The asm form is invisible to that pass; in exchange
+// the caller owns the wait: `lgkm_wait<N>()` then `tie()` on every fragment
+// before its first use (the tie orders the consuming MFMAs after the wait).
+__device__ __forceinline__ short4_t lds_read_tr_async(const void* p) {
+  short4_t r;
+  // low 32 bits of a generic pointer into LDS = the LDS byte address
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+// 16-byte LDS read, likewise untracked (a tracked read mixed into an untracked
+// stream makes the pass fall back to lgkmcnt(0) at loop boundaries).
+__device__ __forceinline__ short8_t lds_read_b128_async(const void* p) {
+  short8_t r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15) : "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ void tie(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
 __device__ __forceinline__ short8_t cat4(short4_t a, short4_t b) {
   short8_t r;
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];

@@ -169,15 +169,29 @@ __device__ __forceinline__ short8_t frag(const char* lds, int base, int s, int l
   if constexpr (KC) {
     const int row = base + (lane & 15);
     const int byte = (s * 4 + (lane >> 4)) * 16;
-    return *reinterpret_cast<const short8_t*>(lds + lds_off<KC, R>(row, byte));
+    return lds_read_b128_async(lds + lds_off<KC, R>(row, byte));
   } else {
     const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
     const int krow = s * 32 + 8 * g + q;
     const int byte = (base + 4 * p) * 2;
-    const short4_t lo = lds_read_tr(lds + lds_off<KC, R>(krow, byte));
-    const short4_t hi = lds_read_tr(lds + lds_off<KC, R>(krow + 4, byte));
+    const short4_t lo = lds_read_tr_async(lds + lds_off<KC, R>(krow, byte));
+    const short4_t hi = lds_read_tr_async(lds + lds_off<KC, R>(krow + 4, byte));
     return cat4(lo, hi);
   }
+}
+
+// LDS instructions one frag<KC>() issues (MN-contiguous: two transposing reads)
+template <bool KC>
+constexpr int frag_ops() {
+  return KC ? 1 : 2;
+}
+
+// Fragments read with lds_read_tr_async are not tracked by the compiler:
+// make every later use wait for them (see tdg_common.h).
+template <int N>
+__device__ __forceinline__ void tie_all(short8_t (&f)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) tie(f[i]);
 }
 
 // Grouped launch: up to MAXG same-shape problems in one grid (blockIdx.y =
@@ -245,6 +259,35 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   ga.init(wid, lane);
   gb.init(wid, lane);
 
+  // Epilogue operands (ReLU-mask aux, beta*C_old) of the wave's sub-tile are
+  // loaded into registers HERE, before the first LDS-DMA: in the training
+  // step they are cold in HBM (the ReLU input was written in forward), and
+  // loaded after the MFMAs their latency sat fully exposed at the end of
+  // every tile. Issued first, they are older than every DMA, so the
+  // pipeline's vmcnt waits stay exact (they only also cover these loads).
+  using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int ES = sizeof(OutT);
+  constexpr int EPC = 16 / ES;                  // elements per 16-byte chunk
+  constexpr int CPR = WTN / EPC;                // chunks per sub-tile row
+  constexpr int NPRE = (WTM * CPR) / 64;        // 16-byte chunks per lane
+  const bool split = gridDim.z > 1;
+  const bool pre_aux = EPI == EPI_DRELU && !split && (ldaux % 8) == 0 &&
+                       (reinterpret_cast<uintptr_t>(aux) & 15) == 0;
+  const bool pre_c = beta != 0.f && !split && ((ldc * ES) % 16) == 0 &&
+                     (reinterpret_cast<uintptr_t>(Cv) & 15) == 0;
+  int4 aux_r[NPRE], c_r[NPRE];
+#pragma unroll
+  for (int t = 0; t < NPRE; ++t) {
+    const int id = lane + 64 * t;
+    const int m = m0 + wm * WTM + id / CPR;
+    const int n = n0 + wn * WTN + (id % CPR) * EPC;
+    const bool in = m < M && n + EPC <= N;
+    if (pre_aux && in) aux_r[t] = *reinterpret_cast<const int4*>(aux + (size_t)m * ldaux + n);
+    if (pre_c && in)
+      c_r[t] = *reinterpret_cast<const int4*>(reinterpret_cast<const OutT*>(Cv) + (size_t)m * ldc + n);
+  }
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -285,12 +328,18 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     for (int j = 0; j < TN; ++j) fb0[j] = frag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, 0, lane);
   }
 
+  // LDS instructions of one k-step's fragment reads (for the counted waits)
+  constexpr int STEP_OPS = TM * frag_ops<A_KC>() + TN * frag_ops<B_KC>();
   for (int kt = 0; kt < nk; ++kt) {
     const char* st = smem + (kt % STAGES) * SB;
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa1[i] = frag<A_KC, BM>(st, abase + 16 * i, 1, lane);
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb1[j] = frag<B_KC, BN>(st + A_BYTES, bbase + 16 * j, 1, lane);
+    // step-0 fragments landed; the step-1 reads just issued stay in flight
+    lgkm_wait<STEP_OPS>();
+    tie_all(fa0);
+    tie_all(fb0);
     prio_hi();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -320,7 +369,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
       for (int i = 0; i < TM; ++i) fa0[i] = frag<A_KC, BM>(nx, abase + 16 * i, 0, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb0[j] = frag<B_KC, BN>(nx + A_BYTES, bbase + 16 * j, 0, lane);
+      // (the step-1 fragments completed at the barrier's lgkmcnt(0))
+    } else {
+      lgkm_wait<0>();
     }
+    tie_all(fa1);
+    tie_all(fb1);
     prio_hi();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -336,13 +390,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   //    chunks, applies the elementwise epilogue that needs a second operand
   //    (ReLU-mask aux, beta*C) with vector loads, and stores 16 bytes per lane.
   // Split-K partial products take the same path into the f32 slab of split z.
-  using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int ES = sizeof(OutT);
   constexpr int SROW = WTN * ES + 16;          // padded LDS row (bytes)
-  constexpr int EPC = 16 / ES;                  // elements per 16-byte chunk
-  constexpr int CPR = WTN / EPC;                // chunks per sub-tile row
-  const bool split = gridDim.z > 1;
   OutT* C = reinterpret_cast<OutT*>(Cv) + (split ? (size_t)blockIdx.z * split_stride : 0);
   const float a_ = split ? 1.f : alpha;
   const float b_ = split ? 0.f : beta;
@@ -389,14 +437,17 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     OutT* cp = C + (size_t)m * ldc + n;
     if (vec_ok && n + EPC <= N) {
       if constexpr (EPI == EPI_DRELU) {
-        const short8_t x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
+        short8_t x;
+        if (pre_aux) x = *reinterpret_cast<const short8_t*>(&aux_r[t]);
+        else x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
 #pragma unroll
         for (int e = 0; e < EPC; ++e)
           if (!(bf2f((bf16_t)x[e * (8 / EPC)]) > 0.f)) vals[e] = OutT(0);
       }
       if (b_ != 0.f) {
         OutT old[EPC];
-        *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
+        if (pre_c) *reinterpret_cast<int4*>(old) = c_r[t];
+        else *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
           if constexpr (OUT_F32) vals[e] += b_ * old[e];
@@ -593,6 +644,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
           for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
       }
       if (more) issue_half(kt + 1, ph);
+      // this phase's fragment reads (untracked transposing reads included)
+      if (ph < 3) {
+        lgkm_wait<0>();
+        if (ph == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tie_all(fa[i]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) tie_all(fb[j]);
+        } else if (ph == 1) {
+#pragma unroll
+          for (int j = 2; j < 4; ++j) tie_all(fb[j]);
+        } else {
+#pragma unroll
+          for (int i = 4; i < 8; ++i) tie_all(fa[i]);
+        }
+      }
       const int i0 = (ph < 2) ? 0 : 4;
       const int j0 = (ph == 0 || ph == 3) ? 0 : 2;
       __builtin_amdgcn_s_setprio(1);

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""GEMMs whose epilogue reads a second operand (ReLU-backward mask, beta*C
+residual accumulation), timed with COLD caches as in the training step (a
+512 MB buffer is rewritten between reps so L2/MALL hold nothing useful):
+every tile config vs hipBLASLt. Also checks each config against fp32.
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk  # noqa: E402
+
+DEV = "cuda"
+FLUSH = None
+
+
+def timeit(fn, reps=20, cold=True):
+    global FLUSH
+    if FLUSH is None:
+        FLUSH = torch.empty(128 * 1024 * 1024, dtype=torch.float32, device=DEV)
+    ts = []
+    for r in range(reps + 2):
+        if cold:
+            FLUSH.fill_(float(r))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        if r >= 2:
+            ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    torch.manual_seed(0)
+    T, d, ff = 8192, 512, 2048
+    res = []
+    # (name, M, N, K, epi): dgrad dx[M,N] = dy[M,K] @ W[K,N]  (A KC, B MC)
+    cases = [("ffn2_dgrad_drelu", T, ff, d, "drelu"),
+             ("qkv_dgrad_beta1", T, d, 3 * d, "beta"),
+             ("ffn1_dgrad_beta1", T, d, ff, "beta"),
+             ("q_dgrad_beta1", T, d, d, "beta"),
+             ("o_dgrad", T, d, d, "none")]
+    for name, M, N, K, kind in cases:
+        A = torch.randn(M, K, device=DEV).bfloat16()
+        B = (torch.randn(K, N, device=DEV) * 0.05).bfloat16()
+        aux = torch.randn(M, N, device=DEV).bfloat16() if kind == "drelu" else None
+        C0 = torch.randn(M, N, device=DEV).bfloat16()
+        C = C0.clone()
+        ref = A.float() @ B.float()
+        if kind == "drelu":
+            ref = ref * (aux.float() > 0)
+        if kind == "beta":
+            ref = ref + C0.float()
+        epi = kk.EPI_DRELU if kind == "drelu" else kk.EPI_NONE
+        beta = 1.0 if kind == "beta" else 0.0
+        row = {"name": name, "M": M, "N": N, "K": K}
+        cfgs = [(c, 1) for c in (0, 1, 2, 3, 4, 7, 8, 11, 12)]
+        for cfg in cfgs:
+            def run(cfg=cfg):
+                kk.gemm(A, B, C, M, N, K, K, N, N, True, False, epi=epi, aux=aux, ldaux=N,
+                        beta=beta, cfg=cfg)
+            try:
+                C.copy_(C0)
+                run()
+                err = ((C.float() - ref).abs().max() / ref.abs().max()).item()
+                t = timeit(run)
+            except RuntimeError as e:  # unsupported combination
+                row[f"cfg{cfg[0]}"] = str(e)[:40]
+                continue
+            row[f"cfg{cfg[0]}"] = round(t, 2)
+            row[f"err{cfg[0]}"] = float(f"{err:.1e}")
+        if kind != "drelu":
+            def blas():
+                if beta:
+                    C.addmm_(A, B)
+                else:
+                    torch.mm(A, B, out=C)
+            row["hipblaslt"] = round(timeit(blas), 2)
+        row["flops_T"] = 2 * M * N * K / 1e12
+        res.append(row)
+        print(json.dumps(row), flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(res, open("gpurun_out/gemm_epi_bench.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

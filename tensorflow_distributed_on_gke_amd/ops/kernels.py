@@ -138,7 +138,8 @@ def load_tuned(path: str) -> int:
     return len(data)
 
 
-TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned_gfx950.json")
+TUNED_FILE = os.environ.get("TDG_GEMM_TUNED_FILE") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "gemm_tuned_gfx950.json")
 if os.environ.get("TDG_GEMM_TUNED", "1") != "0":
     load_tuned(TUNED_FILE)
 

@@ -67,6 +67,23 @@ def test_gemm_dgrad_drelu(M, N, K, cfg):
     _close(out, ref, 1e-2, "gemm dgrad")
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 1536), (300, 200, 136), (130, 2048, 512)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 4, 7, 8, 11])
+def test_gemm_nn_epilogue_operands(M, N, K, cfg):
+    """Every tile config of the NN (dgrad) kernel with an epilogue operand
+    prefetched into registers before the main loop: beta*C residual
+    accumulation, and the ReLU-backward mask."""
+    dy = _bf(_rand(M, K, seed=31)).to(DEV)
+    w = _bf(_rand(K, N, scale=0.5, seed=32)).to(DEV)
+    c0 = _bf(_rand(M, N, seed=33)).to(DEV)
+    out = c0.clone()
+    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=1.0, cfg=(cfg, 1))
+    _close(out, dy.float() @ w.float() + c0.float(), 1e-2, "gemm NN beta=1")
+    h = _bf(_rand(M, N, seed=34)).to(DEV)
+    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_DRELU, aux=h, ldaux=N, cfg=(cfg, 1))
+    _close(out, (dy.float() @ w.float()) * (h.float() > 0), 1e-2, "gemm NN drelu")
+
+
 @pytest.mark.parametrize("M,N,K,splits", [(512, 128, 256, 1), (8192, 512, 512, 8), (1000, 7016, 64, 1),
                                           (4000, 200, 136, 3)])
 def test_gemm_wgrad_f32(M, N, K, splits):
