@@ -109,6 +109,9 @@ def main() -> None:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    if ddp is not None and info.rank == 0:
+        spans = [round((b.end - b.start) * 4 / 2 ** 20, 1) for b in ddp.last_buckets]
+        print(f"all-reduce spans per step (MB, launch order): {spans}", file=sys.stderr)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -63,7 +63,8 @@ int tdg_xent_stats(const float* row_loss, const float* row_correct, int M, const
                    float workers, float* step_out, float* accum, hipStream_t st);
 int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, long long* step,
              float beta1, float beta2, float eps, float lr_const, float d_model, float warmup,
-             float grad_scale, float weight_decay, int sched, int zero_grad, hipStream_t st);
+             float grad_scale, float weight_decay, int sched, int zero_grad, int inc_step,
+             hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
 }
 
@@ -676,7 +677,7 @@ void xent_stats(const Tensor& row_loss, const Tensor& row_correct, const Tensor&
 void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
           const optional<Tensor>& shadow, const Tensor& step, double beta1, double beta2,
           double eps, double lr_const, double d_model, double warmup, double grad_scale,
-          double weight_decay, int64_t sched, bool zero_grad) {
+          double weight_decay, int64_t sched, bool zero_grad, bool inc_step) {
   for (auto* t : {&p, &g, &m, &v}) {
     check_f32(*t, "adam buffers");
     check_contig(*t, "adam buffers");
@@ -693,7 +694,7 @@ void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
                      v.data_ptr<float>(), shadow.has_value() ? shadow->data_ptr() : nullptr,
                      p.numel(), reinterpret_cast<long long*>(step.data_ptr<int64_t>()), (float)beta1, (float)beta2, (float)eps,
                      (float)lr_const, (float)d_model, (float)warmup, (float)grad_scale,
-                     (float)weight_decay, (int)sched, zero_grad, stream_of(p)),
+                     (float)weight_decay, (int)sched, zero_grad, inc_step, stream_of(p)),
             "tdg adam");
 }
 

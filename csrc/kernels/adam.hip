@@ -90,7 +90,7 @@ using namespace tdg;
 extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n,
                         long long* step, float beta1, float beta2, float eps, float lr_const,
                         float d_model, float warmup, float grad_scale, float weight_decay,
-                        int sched, int zero_grad, hipStream_t st) {
+                        int sched, int zero_grad, int inc_step, hipStream_t st) {
   if (n % 4 != 0) return -1;
   AdamCfg c{beta1, beta2, eps, lr_const, d_model, warmup, grad_scale, weight_decay, sched,
             zero_grad};
@@ -98,7 +98,8 @@ extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, lo
   const int blocks = (int)std::min<long long>(8192, (n4 + 255) / 256);
   hipLaunchKernelGGL(adam_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p, g, m, v,
                      (bf16_t*)shadow, n, step, c);
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
+  // per-bucket updates (data parallel) share one step: only the last advances it
+  if (inc_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   return 0;
 }
 

@@ -80,8 +80,10 @@ struct Stage {
 __device__ __forceinline__ i32x8 frag(const char* lds, int base, int lane) {
   const int row = base + (lane & 15);
   const int g = lane >> 4;
-  const int4 lo = *reinterpret_cast<const int4*>(lds + lds_off(row, 32 * g));
-  const int4 hi = *reinterpret_cast<const int4*>(lds + lds_off(row, 32 * g + 16));
+  // untracked reads (tdg_common.h): a tracked LDS read after an LDS-DMA issue
+  // gets an s_waitcnt vmcnt(0) that drains the next tile's prefetch
+  const int4 lo = __builtin_bit_cast(int4, tdg::lds_read_b128_async(lds + lds_off(row, 32 * g)));
+  const int4 hi = __builtin_bit_cast(int4, tdg::lds_read_b128_async(lds + lds_off(row, 32 * g + 16)));
   return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 }
 
@@ -159,6 +161,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   for (int j = 0; j < TN; ++j) fb[j] = f8::frag(smem + A_BYTES, bbase + 16 * j, lane);
 
   for (int kt = 0; kt < nk; ++kt) {
+    tdg::lgkm_wait<0>();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) tdg::tie(fa[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) tdg::tie(fb[j]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i)

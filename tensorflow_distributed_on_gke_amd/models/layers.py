@@ -123,16 +123,42 @@ class WgradQueue:
     shape (ops.kernels.wgrad_grouped). Bias column sums and the data-parallel
     grad_ready notifications follow in backward order."""
 
-    def __init__(self, flush_at_boundary: bool = False):
+    def __init__(self, flush_at_boundary: bool = False, wave_tiles: int = 0):
         self.items = []
         # data parallel: also flush when the decoder's backward is complete,
         # so the decoder-side buckets are all-reduced while the encoder's
         # backward runs
         self.flush_at_boundary = flush_at_boundary
+        # data parallel: also flush at a layer end when waiting for one more
+        # layer would overflow `wave_tiles` 256x256 tiles (one tile per CU):
+        # a whole-K wgrad tile runs ~K/32 us, so a launch costs ceil(tiles /
+        # wave_tiles) "waves" -- flushing in chunks that each fit a wave costs
+        # no more waves than the two-flush schedule, while every chunk's
+        # all-reduce starts layers earlier (only the last chunk stays exposed)
+        self.wave_tiles = wave_tiles
+        self._layer_tiles = 0
+        self._at_last_end = 0
 
     def boundary(self) -> None:
         if self.flush_at_boundary and self.items:
             self.flush()
+
+    @staticmethod
+    def _tiles(it) -> int:
+        dy2, x2, N = it[0], it[1], it[2]
+        return -(-N // 256) * -(-x2.shape[1] // 256)
+
+    def layer_end(self) -> None:
+        """A decoder or encoder layer's backward is complete."""
+        if not self.wave_tiles or not self.items:
+            return
+        queued = sum(self._tiles(it) for it in self.items)
+        layer = queued - self._at_last_end
+        self._layer_tiles = layer if layer > 0 else self._layer_tiles
+        if queued + self._layer_tiles > self.wave_tiles:
+            self.flush()
+        else:
+            self._at_last_end = queued
 
     def add(self, dy2, x2, N, w: Param, b: Optional[Param], beta: float, rt: "RunCtx"):
         self.items.append((dy2, x2, N, w, b, beta, rt))
@@ -145,7 +171,10 @@ class WgradQueue:
         self._flush_bias()
         for dy2, x2, N, w, b, beta, rt in self.items:
             _ready(rt, w, *([b] if b is not None else []))
+        if self.items and self.items[0][6].store is not None:
+            self.items[0][6].store.grad_sync()
         self.items = []
+        self._at_last_end = 0
 
     def _flush_ragged(self) -> bool:
         """All weight gradients as ragged launches of 256x256 tiles: one per
@@ -379,6 +408,8 @@ class SelfAttnBlockFn(torch.autograd.Function):
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
             _wgrad(rt, dqkv, x2, 3 * d, wqkv, bqkv)
             dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
+            if rt.wgrad is not None:
+                rt.wgrad.layer_end()  # self-attention is a layer's first block
             return (dx.view(B, L, d),) + (None,) * 11
         else:
             _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)
@@ -433,6 +464,10 @@ class CrossKVFn(torch.autograd.Function):
             _write_grad(bkv, dkv.sum(0), rt)
             _ready(rt, wkv, bkv)
             denc = dkv @ wkv.master
+        if rt.store is not None:
+            # the rest of backward (encoder) reads no decoder-side weight: the
+            # data-parallel optimizer may update those buckets from here on
+            rt.store.release_point()
         return denc.view(B, S, d), None, None, None, None
 
 

@@ -105,6 +105,8 @@ class ParamStore:
         self.device = torch.device("cpu")
         self.compute_dtype = torch.float32
         self._ready_hooks: List[Callable[[Param], None]] = []
+        self._release_hooks: List[Callable[[], None]] = []
+        self._sync_hooks: List[Callable[[], None]] = []
         # autograd anchor: gives layers whose only inputs are token ids a
         # tensor that requires grad, so backward reaches them.
         self.anchor = torch.zeros((), requires_grad=True)
@@ -166,6 +168,26 @@ class ParamStore:
     def grad_ready(self, p: Param) -> None:
         for h in self._ready_hooks:
             h(p)
+
+    def on_grad_sync(self, fn: Callable[[], None]) -> None:
+        self._sync_hooks.append(fn)
+
+    def grad_sync(self) -> None:
+        """A batch of gradients just became final together (one flush of the
+        deferred weight-gradient GEMMs): a natural collective boundary."""
+        for h in self._sync_hooks:
+            h()
+
+    def on_release(self, fn: Callable[[], None]) -> None:
+        self._release_hooks.append(fn)
+
+    def release_point(self) -> None:
+        """Called by the model during backward at a point after which no
+        kernel still to be issued in this backward reads any parameter whose
+        gradient is already final: from here on those parameters may be
+        updated concurrently with the rest of backward."""
+        for h in self._release_hooks:
+            h()
 
     def zero_grad(self) -> None:
         self.flat_grad.zero_()

@@ -419,6 +419,6 @@ def xent_stats(row_loss, row_correct, ntok, workers, step_out=None, accum=None):
 
 
 def adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale=1.0,
-         weight_decay=0.0, sched=1, zero_grad=True):
+         weight_decay=0.0, sched=1, zero_grad=True, inc_step=True):
     C().adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale,
-             weight_decay, sched, zero_grad)
+             weight_decay, sched, zero_grad, inc_step)

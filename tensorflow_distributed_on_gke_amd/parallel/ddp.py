@@ -1,21 +1,28 @@
-"""Synchronous data parallelism over RCCL (xGMI) with bucketed, backward-
-overlapped gradient all-reduce.
+"""Synchronous data parallelism over RCCL (xGMI) with backward-overlapped,
+ready-driven gradient all-reduce.
 
 Replaces the reference's tf.distribute.MultiWorkerMirroredStrategy gradient
 aggregation (reference: distributed_training_transformer/cluster/cluster.py:66,
-__main__.py:105-132 — loss scaled by 1/workers, SUM all-reduce inside
+__main__.py:105-132 -- loss scaled by 1/workers, SUM all-reduce inside
 `apply_gradients`, initial variables broadcast from worker 0).
 
 Design (MI355X): the model's gradients live in one flat f32 buffer laid out in
-backward order (models/params.py). The buffer is cut into contiguous buckets
-of ~`bucket_mb`; each layer op notifies `grad_ready(param)` as soon as it has
-written a gradient, and the bucket whose last gradient just landed is
-all-reduced immediately with `async_op=True`. ProcessGroupNCCL (RCCL on ROCm)
-runs the collective on its own HIP stream, ordered after the producing kernels
-by an event, so communication overlaps the rest of backward; the optimizer's
-stream waits on the outstanding work handles (no host sync). Buckets are large
-(default 64 MB) because a ring all-reduce over point-to-point xGMI needs big
-messages to spread over RCCL's channels / the 7 links per GPU.
+backward order (models/params.py), so gradients complete roughly front to
+back. Every layer op notifies `grad_ready(param)` once it has written a
+gradient; the DataParallel keeps the *frontier* -- the longest prefix of the
+flat buffer whose gradients are all final -- and all-reduces the span between
+the last reduced offset and the frontier:
+  * as soon as the span reaches `bucket_mb` (the classic bucket), and
+  * at every sync point (`ParamStore.grad_sync`, issued after each flush of
+    the deferred weight-gradient GEMMs) once it is >= `min_mb`,
+so collective boundaries follow the real completion order of the step instead
+of a fixed bucket grid (a fixed grid straddling two flushes delays its
+collective to the later one). ProcessGroupNCCL (RCCL on ROCm) runs each
+collective on its own HIP stream, ordered after the producing kernels by an
+event, so communication overlaps the rest of backward; the optimizer's stream
+waits on the work handles (no host sync). Large spans (tens of MB) are what a
+ring all-reduce over point-to-point xGMI needs to spread over RCCL's channels
+and the 7 links per GPU.
 """
 from __future__ import annotations
 
@@ -37,11 +44,13 @@ class Bucket:
     params: List[int]
     remaining: int = 0
     work: Optional[object] = None
+    updated: bool = False
 
 
 def plan_buckets(store: ParamStore, bucket_bytes: int) -> List[Bucket]:
-    """Cut the flat buffer (ordered by offset) at parameter boundaries into
-    buckets of at least `bucket_bytes` (the last may be smaller). Pure."""
+    """The static bucket grid (cut at parameter boundaries into buckets of at
+    least `bucket_bytes`, the last may be smaller): the spans the frontier
+    launches when every gradient arrives one at a time in flat order. Pure."""
     order = sorted(store.params, key=lambda p: p.offset)
     buckets: List[Bucket] = []
     cur: Optional[Bucket] = None
@@ -65,7 +74,7 @@ def plan_buckets(store: ParamStore, bucket_bytes: int) -> List[Bucket]:
 class DataParallel:
     def __init__(self, store: ParamStore, bucket_mb: float = 64.0, group=None,
                  comm_dtype: Optional[torch.dtype] = None, overlap: bool = True,
-                 force: bool = False):
+                 force: bool = False, min_mb: float = 4.0):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -75,15 +84,34 @@ class DataParallel:
         self.active = self.world > 1 or (force and dist.is_initialized())
         self.overlap = overlap
         self.comm_dtype = comm_dtype
-        self.buckets = plan_buckets(store, int(bucket_mb * 1024 * 1024))
-        self.bucket_of = {}
-        for i, b in enumerate(self.buckets):
-            for pi in b.params:
-                self.bucket_of[pi] = i
+        self.bucket_elems = max(64, int(bucket_mb * 1024 * 1024) // 4)
+        self.min_elems = max(64, int(min_mb * 1024 * 1024) // 4)
+        self._order = sorted(store.params, key=lambda p: p.offset)
+        self._pos = {p.index: i for i, p in enumerate(self._order)}
         self._comm_bufs = {}
+        self.opt = None
+        self._upd_stream = None
+        self.buckets: List[Bucket] = []       # this step's launched spans
+        self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
         if self.active:
             store.on_grad_ready(self._on_ready)
+            store.on_grad_sync(self._on_sync)
         self.reset()
+
+    def attach_optimizer(self, opt) -> None:
+        """Overlap the optimizer with backward: a bucket is updated (Adam over
+        its flat range) as soon as its all-reduce is done AND the model has
+        passed a release point (ParamStore.release_point: no later backward
+        kernel reads those weights) -- for the Transformer, the decoder side
+        is updated while the encoder's backward runs. finish() updates the
+        rest and advances the step. The optimizer must offer
+        apply_range(start, end, inc_step) / advance_step()."""
+        if not self.active:
+            return
+        self.opt = opt
+        if self.store.flat.is_cuda:
+            self._upd_stream = torch.cuda.Stream(self.store.flat.device)
+        self.store.on_release(self._on_release)
 
     # ------------------------------------------------------------------ init
     def broadcast_params(self, src: int = 0) -> None:
@@ -94,9 +122,27 @@ class DataParallel:
 
     # ------------------------------------------------------------------ step
     def reset(self) -> None:
-        for b in self.buckets:
-            b.remaining = len(b.params)
-            b.work = None
+        if self.buckets:
+            self.last_buckets = self.buckets
+        self.buckets = []
+        self._ready = [False] * len(self._order)
+        self._front = 0      # params [0, _front) of the flat order are all final
+        self._reduced = 0    # flat offset up to which all-reduces are launched
+
+    def _front_off(self) -> int:
+        if self._front >= len(self._order):
+            return self.store.total
+        return self._order[self._front].offset
+
+    def _launch_span(self, end: int) -> None:
+        if end <= self._reduced:
+            return
+        lo = self._reduced
+        params = [p.index for p in self._order if lo <= p.offset < end]
+        b = Bucket(lo, end, params)
+        self._reduced = end
+        self.buckets.append(b)
+        self._launch(b)
 
     def _launch(self, b: Bucket) -> None:
         # gradients come from both the compute stream and the weight-gradient
@@ -107,36 +153,73 @@ class DataParallel:
     def _launch_now(self, b: Bucket) -> None:
         view = self.store.flat_grad[b.start:b.end]
         if self.comm_dtype is not None and self.comm_dtype != view.dtype:
-            buf = self._comm_bufs.get(b.start)
+            buf = self._comm_bufs.get((b.start, b.end))
             if buf is None:
                 buf = torch.empty(view.numel(), dtype=self.comm_dtype, device=view.device)
-                self._comm_bufs[b.start] = buf
+                self._comm_bufs[(b.start, b.end)] = buf
             buf.copy_(view)
             b.work = (dist.all_reduce(buf, group=self.group, async_op=True), buf, view)
         else:
             b.work = (dist.all_reduce(view, group=self.group, async_op=True), None, None)
 
     def _on_ready(self, p: Param) -> None:
-        b = self.buckets[self.bucket_of[p.index]]
-        b.remaining -= 1
-        if b.remaining == 0 and self.overlap and b.work is None:
-            self._launch(b)
+        self._ready[self._pos[p.index]] = True
+        while self._front < len(self._order) and self._ready[self._front]:
+            self._front += 1
+        if self.overlap and self._front_off() - self._reduced >= self.bucket_elems:
+            self._launch_span(self._front_off())
+
+    def _on_sync(self) -> None:
+        if self.overlap and self._front_off() - self._reduced >= self.min_elems:
+            self._launch_span(self._front_off())
+
+    def _complete(self, b: Bucket) -> None:
+        """Current stream waits for the bucket's all-reduce (device-side)."""
+        work, buf, view = b.work
+        work.wait()
+        if buf is not None:
+            view.copy_(buf)
+
+    def _on_release(self) -> None:
+        if self.opt is None:
+            return
+        ready = [b for b in self.buckets if b.work is not None and not b.updated]
+        if not ready:
+            return
+        if self._upd_stream is None:  # CPU (gloo): in order
+            for b in ready:
+                self._complete(b)
+                self.opt.apply_range(b.start, b.end, inc_step=False)
+                b.updated = True
+            return
+        upd = self._upd_stream
+        # ordered after every kernel issued so far (the last reads of these weights)
+        upd.wait_stream(torch.cuda.current_stream(upd.device))
+        with torch.cuda.stream(upd):
+            for b in ready:
+                self._complete(b)
+                self.opt.apply_range(b.start, b.end, inc_step=False)
+                b.updated = True
 
     def finish(self) -> None:
-        """Launch any bucket not yet reduced and make the current stream wait
-        for all of them (device-side wait; no host sync)."""
+        """Launch the rest of the buffer and make the current stream wait for
+        every collective (device-side wait; no host sync). With an attached
+        optimizer, also update every span not yet updated and advance the
+        optimizer step."""
         join(self.store.flat_grad.device)
         if not self.active:
             self.reset()
             return
+        self._launch_span(self.store.total)
+        if self._upd_stream is not None:
+            torch.cuda.current_stream(self._upd_stream.device).wait_stream(self._upd_stream)
         for b in self.buckets:
-            if b.work is None:
-                self._launch(b)
-        for b in self.buckets:
-            work, buf, view = b.work
-            work.wait()
-            if buf is not None:
-                view.copy_(buf)
+            if not b.updated:
+                self._complete(b)
+                if self.opt is not None:
+                    self.opt.apply_range(b.start, b.end, inc_step=False)
+        if self.opt is not None:
+            self.opt.advance_step()
         self.reset()
 
     def verify_replicas(self) -> None:

@@ -45,21 +45,36 @@ class Adam:
         return noam_lr(step, self.d_model, self.warmup)
 
     def apply(self, grad_scale: float = 1.0) -> None:
+        self.apply_range(0, self.store.total, grad_scale, inc_step=True)
+
+    def apply_range(self, start: int, end: int, grad_scale: float = 1.0, inc_step: bool = True) -> None:
+        """Update flat[start:end] only (one data-parallel bucket, as soon as its
+        all-reduce is done). Every range of a step reads the same step
+        counter; exactly one call per step (the last) passes inc_step."""
         s = self.store
+        sl = slice(start, end)
         if s.flat.is_cuda:
-            K.adam(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, self.step, self.beta1,
-                   self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model), float(self.warmup),
-                   grad_scale, self.weight_decay, 0 if self.lr_const is not None else 1, True)
+            K.adam(s.flat[sl], s.flat_grad[sl], self.m[sl], self.v[sl],
+                   s.flat_compute[sl] if s.flat_compute is not None else None, self.step,
+                   self.beta1, self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model),
+                   float(self.warmup), grad_scale, self.weight_decay,
+                   0 if self.lr_const is not None else 1, True, inc_step)
             return
         step = int(self.step.item())
         lr = self.lr_at(step)
         t = step + 1
         lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
-        g = s.flat_grad * grad_scale
-        self.m.add_((g - self.m) * (1 - self.beta1))
-        self.v.add_((g * g - self.v) * (1 - self.beta2))
-        s.flat.sub_(lr_t * self.m / (self.v.sqrt() + self.eps) + lr * self.weight_decay * s.flat)
-        s.flat_grad.zero_()
+        p, g, m, v = s.flat[sl], s.flat_grad[sl], self.m[sl], self.v[sl]
+        g = g * grad_scale
+        m.add_((g - m) * (1 - self.beta1))
+        v.add_((g * g - v) * (1 - self.beta2))
+        p.sub_(lr_t * m / (v.sqrt() + self.eps) + lr * self.weight_decay * p)
+        s.flat_grad[sl].zero_()
+        if inc_step:
+            self.step += 1
+
+    def advance_step(self) -> None:
+        """Keras `iterations += 1` after a step applied as several ranges."""
         self.step += 1
 
     def state_dict(self) -> dict:

@@ -12,6 +12,7 @@ replicas only when the host reads it (log points).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -19,8 +20,13 @@ import torch
 from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
+from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.ops.streams import join
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
+
+
+# data parallel: weight gradients flushed in wave-sized chunks at layer ends
+CHUNKED_WGRAD = os.environ.get("TDG_DP_CHUNKED_WGRAD", "1") != "0"
 
 
 class TrainStep:
@@ -42,8 +48,17 @@ class TrainStep:
         if defer_wgrad is None:
             defer_wgrad = True
         if defer_wgrad and dev.type == "cuda":
-            self.rt.wgrad = WgradQueue(flush_at_boundary=ddp is not None and ddp.active)
+            dp = ddp is not None and ddp.active
+            self.rt.wgrad = WgradQueue(flush_at_boundary=dp,
+                                       wave_tiles=K.NUM_CU if dp and CHUNKED_WGRAD else 0)
         self.fp8 = fp8_state
+        # data parallel: each bucket's Adam runs as soon as its all-reduce is
+        # done (decoder side during the encoder's backward)
+        # (opt-in: on one MI355X with --force-dp the concurrent Adam contended
+        # with the encoder backward for more than it hid, 6.45 vs 6.34 ms)
+        if ddp is not None and ddp.active and fp8_state is None and \
+                os.environ.get("TDG_DP_OVERLAP_OPT", "0") != "0":
+            ddp.attach_optimizer(opt)
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
         self.last = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -58,7 +73,8 @@ class TrainStep:
             self.ddp.finish()
         else:
             join(self.model.device)  # weight gradients from the side stream
-        self.opt.apply()
+        if self.ddp is None or self.ddp.opt is None:
+            self.opt.apply()
         if self.fp8 is not None:
             self.fp8.after_step()  # new scales, then fp8 weight copies
         return self.last

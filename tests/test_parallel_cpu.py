@@ -40,9 +40,10 @@ def _data(rank, world):
     return SyntheticPairs(4, 10, 11, 60, 50, seed=3, rank=rank, world=world, min_len=3)
 
 
-def _worker(rank, world, port, out, bucket_mb, comm=None):
+def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      TDG_DP_OVERLAP_OPT=str(overlap_opt))
     torch.set_num_threads(2)
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.train.step import TrainStep
@@ -52,6 +53,15 @@ def _worker(rank, world, port, out, bucket_mb, comm=None):
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     ddp = DataParallel(m.store, bucket_mb=bucket_mb, comm_dtype=comm)
     ddp.broadcast_params(0)
+    early = []  # buckets the optimizer updated at the release point (mid-backward)
+    release = ddp._on_release
+
+    def spy():
+        before = sum(b.updated for b in ddp.buckets)
+        release()
+        early.append(sum(b.updated for b in ddp.buckets) - before)
+
+    ddp._on_release = spy
     step = TrainStep(m, opt, ddp, workers=world, seed=5)
     data = _data(rank, world)
     losses = []
@@ -67,8 +77,8 @@ def _worker(rank, world, port, out, bucket_mb, comm=None):
     except RuntimeError:
         diverged = True
     m.store.flat[0] = saved
-    torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.buckets),
-                "diverged": diverged},
+    torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.last_buckets),
+                "diverged": diverged, "early": torch.tensor(early)},
                f"{out}.{rank}")
     tdist.barrier()
     tdist.shutdown()
@@ -91,16 +101,19 @@ def _single_process_reference(world):
     return m.store.flat, torch.stack(losses)
 
 
-@pytest.mark.parametrize("bucket_mb", [0.05, 64.0])
-def test_dp2_matches_single_process(tmp_path, bucket_mb):
+@pytest.mark.parametrize("bucket_mb,overlap_opt", [(0.05, 1), (64.0, 0)])
+def test_dp2_matches_single_process(tmp_path, bucket_mb, overlap_opt):
     world = 2
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _free_port(), out, bucket_mb), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), out, bucket_mb, None, overlap_opt),
+                       nprocs=world, join=True, start_method="spawn")
     r0 = torch.load(out + ".0", weights_only=True)
     r1 = torch.load(out + ".1", weights_only=True)
     if bucket_mb < 1:
         assert r0["nb"] > 3  # several buckets, launched from inside backward
+    if overlap_opt:
+        # decoder-side buckets were updated during the encoder's backward
+        assert len(r0["early"]) == STEPS and bool((r0["early"] > 0).all()), r0["early"]
     assert torch.equal(r0["flat"], r1["flat"])  # replicas stay identical
     assert r0["diverged"] and r1["diverged"]
     ref_flat, ref_loss = _single_process_reference(world)
@@ -135,6 +148,55 @@ def test_plan_buckets_cover_flat_buffer():
         assert idx == list(range(len(m.store.params)))
         for b in bs[:-1]:
             assert (b.end - b.start) * 4 >= mb * 2 ** 20
+
+
+def _frontier_dp(m, bucket_mb, min_mb):
+    """A DataParallel whose collectives are recorded instead of launched."""
+    dp = DataParallel(m.store, bucket_mb=bucket_mb, min_mb=min_mb)
+    dp.active = True
+    launched = []
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def fake_launch(b):
+        launched.append((b.start, b.end))
+        b.work = (_Done(), None, None)
+
+    dp._launch = fake_launch
+    m.store.clear_grad_hooks()
+    m.store.on_grad_ready(dp._on_ready)
+    m.store.on_grad_sync(dp._on_sync)
+    return dp, launched
+
+
+def test_frontier_spans_follow_completion_order():
+    """Gradients arriving one at a time in flat order reproduce the static
+    bucket grid; a sync point launches the completed prefix early; a gradient
+    out of order holds the frontier back; finish() covers the rest."""
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=0)
+    order = sorted(m.store.params, key=lambda p: p.offset)
+    mb = 0.05
+    dp, launched = _frontier_dp(m, mb, min_mb=0.001)
+    for p in order:
+        m.store.grad_ready(p)
+    dp.finish()
+    assert launched == [(b.start, b.end) for b in plan_buckets(m.store, int(mb * 2 ** 20))]
+
+    dp, launched = _frontier_dp(m, 100.0, min_mb=0.001)  # buckets never fill
+    half = len(order) // 2
+    for p in order[1:half]:  # the first gradient is late
+        m.store.grad_ready(p)
+    m.store.grad_sync()
+    assert launched == []  # nothing final from offset 0 yet
+    m.store.grad_ready(order[0])
+    m.store.grad_sync()
+    assert launched == [(0, order[half].offset)]
+    for p in order[half:]:
+        m.store.grad_ready(p)
+    dp.finish()
+    assert launched[-1] == (order[half].offset, m.store.total)
 
 
 def _cli(tmp, *sets, nproc=2):
