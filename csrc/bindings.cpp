@@ -30,7 +30,10 @@ int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* be
 int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
-               const long long* ctr, uint64_t site, int accumulate, hipStream_t st);
+               const long long* ctr, uint64_t site, int accumulate, int skip_reduce,
+               hipStream_t st);
+int tdg_reduce_partials_multi(const float* const* parts, float* const* outs, const int* nparts,
+                              int G, int N, float beta, hipStream_t st);
 int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe, void* out, int M,
                   int L, int D, float scale, float p, uint64_t seed, const long long* ctr,
                   uint64_t site, hipStream_t st);
@@ -359,7 +362,7 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
             const Tensor& gamma, const Tensor& dh, const optional<Tensor>& ds,
             const optional<Tensor>& dres, const Tensor& dgamma, const Tensor& dbeta,
             const optional<Tensor>& dbias, const Tensor& ws, double p, int64_t seed,
-            const optional<Tensor>& ctr, int64_t site, bool accumulate) {
+            const optional<Tensor>& ctr, int64_t site, bool accumulate, bool skip_reduce) {
   check_bf16(dy, "dy");
   check_contig(dy, "dy");
   const int64_t D = dy.size(-1), M = dy.numel() / D;
@@ -392,8 +395,36 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
       dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(),
       dbeta.data_ptr<float>(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
       ws.data_ptr<float>(), (int)M, (int)D, (float)p, (uint64_t)seed, ctr_ptr(ctr),
-      (uint64_t)site, accumulate, stream_of(dy));
+      (uint64_t)site, accumulate, skip_reduce, stream_of(dy));
   check_err(rc, "tdg ln_bwd");
+}
+
+// Deferred LayerNorm partial folds: outs[g] (=|+=) column sums of parts[g]
+// ([nparts[g], N] f32 each), one launch.
+void reduce_partials_multi(const std::vector<Tensor>& parts, const std::vector<Tensor>& outs,
+                           const std::vector<int64_t>& nparts, int64_t N, double beta) {
+  const size_t G = parts.size();
+  TORCH_CHECK(G >= 1 && G <= 96 && outs.size() == G && nparts.size() == G,
+              "reduce_partials_multi: 1..96 problems");
+  std::vector<const float*> pp(G);
+  std::vector<float*> oo(G);
+  std::vector<int> np(G);
+  for (size_t i = 0; i < G; ++i) {
+    check_f32(parts[i], "parts");
+    check_f32(outs[i], "outs");
+    check_contig(parts[i], "parts");
+    TORCH_CHECK(outs[i].numel() == N && outs[i].is_contiguous(), "reduce_partials_multi: out");
+    TORCH_CHECK(parts[i].numel() >= nparts[i] * N, "reduce_partials_multi: partials too small");
+    TORCH_CHECK(parts[i].device() == parts[0].device() && outs[i].device() == parts[0].device(),
+                "reduce_partials_multi: one device");
+    pp[i] = parts[i].data_ptr<float>();
+    oo[i] = outs[i].data_ptr<float>();
+    np[i] = (int)nparts[i];
+  }
+  c10::DeviceGuard g(parts[0].device());
+  check_err(tdg_reduce_partials_multi(pp.data(), oo.data(), np.data(), (int)G, (int)N, (float)beta,
+                                      stream_of(parts[0])),
+            "tdg reduce_partials_multi");
 }
 
 // ---------------------------------------------------------------- embedding
@@ -732,6 +763,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent", &xent);
   m.def("xent_stats", &xent_stats);
   m.def("adam", &adam);
+  m.def("reduce_partials_multi", &reduce_partials_multi);
   m.def("to_bf16", &to_bf16);
   m.attr("ARCH") = "gfx950";
 }

@@ -289,7 +289,7 @@ template <int D>
 void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
-              int accumulate, hipStream_t st) {
+              int accumulate, int skip_reduce, hipStream_t st) {
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
   constexpr int RPW = D >= 1024 ? 2 : 4;
   const int rpb = 4 * RPW;
@@ -300,6 +300,7 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
   hipLaunchKernelGGL((ln_bwd_kernel<D, RPW>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                      (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site);
+  if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
   hipLaunchKernelGGL(reduce_partials3_kernel, dim3(cdiv(D, 16), dbias ? 3 : 2), dim3(256), 0, st,
@@ -328,12 +329,69 @@ extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, cons
 extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                           const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,
-                          uint64_t seed, const long long* ctr, uint64_t site, int accumulate, hipStream_t st) {
+                          uint64_t seed, const long long* ctr, uint64_t site, int accumulate,
+                          int skip_reduce, hipStream_t st) {
+#define TDG_LN_B(DD)                                                                              \
+  ln_bwd_d<DD>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, \
+               ctr, site, accumulate, skip_reduce, st);                                           \
+  return 0;
   switch (D) {
-    case 128: ln_bwd_d<128>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
-    case 256: ln_bwd_d<256>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
-    case 512: ln_bwd_d<512>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
-    case 1024: ln_bwd_d<1024>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, ctr, site, accumulate, st); return 0;
+    case 128: TDG_LN_B(128)
+    case 256: TDG_LN_B(256)
+    case 512: TDG_LN_B(512)
+    case 1024: TDG_LN_B(1024)
     default: return -1;
   }
+#undef TDG_LN_B
+}
+
+// Deferred stage-2 folds of G (<= MAXR) independent column reductions
+// out[g][n] (=|+=) sum_p part[g][p][n] (nparts[g] partial rows, N columns),
+// one launch: the LayerNorm dgamma / dbeta / sublayer-bias partials of a whole
+// backward, folded together when the deferred weight gradients flush
+// instead of one small launch per LayerNorm.
+namespace tdg {
+constexpr int MAXR = 96;
+struct MultiReduce {
+  const float* part[MAXR];
+  float* out[MAXR];
+  int nparts[MAXR];
+};
+__global__ __launch_bounds__(256) void reduce_partials_multi_kernel(MultiReduce mr, int N,
+                                                                    float beta) {
+  __shared__ float red[16][17];
+  const float* part = mr.part[blockIdx.y];
+  float* out = mr.out[blockIdx.y];
+  const int P = mr.nparts[blockIdx.y];
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + c;
+  float s = 0.f;
+  if (col < N) {
+#pragma unroll 8
+    for (int q = g; q < P; q += 16) s += part[(size_t)q * N + col];
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][c];
+    out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
+  }
+}
+}  // namespace tdg
+
+extern "C" int tdg_reduce_partials_multi(const float* const* parts, float* const* outs,
+                                         const int* nparts, int G, int N, float beta,
+                                         hipStream_t st) {
+  if (G < 1 || G > MAXR) return -2;
+  MultiReduce mr{};
+  for (int i = 0; i < G; ++i) {
+    mr.part[i] = parts[i];
+    mr.out[i] = outs[i];
+    mr.nparts[i] = nparts[i];
+  }
+  hipLaunchKernelGGL(reduce_partials_multi_kernel, dim3(cdiv(N, 16), G), dim3(256), 0, st, mr, N,
+                     beta);
+  return 0;
 }

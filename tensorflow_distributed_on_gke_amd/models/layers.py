@@ -138,9 +138,12 @@ class WgradQueue:
         self.wave_tiles = wave_tiles
         self._layer_tiles = 0
         self._at_last_end = 0
+        # deferred LayerNorm dgamma/dbeta/bias partial folds (one launch per flush)
+        self.reductions = []
+        self.reduced_params = []
 
     def boundary(self) -> None:
-        if self.flush_at_boundary and self.items:
+        if self.flush_at_boundary and (self.items or self.reductions):
             self.flush()
 
     @staticmethod
@@ -164,16 +167,24 @@ class WgradQueue:
         self.items.append((dy2, x2, N, w, b, beta, rt))
 
     def flush(self) -> None:
-        if RAGGED_WGRAD and self._flush_ragged():
-            pass
-        else:
-            self._flush_grouped()
-        self._flush_bias()
+        if self.items:
+            if RAGGED_WGRAD and self._flush_ragged():
+                pass
+            else:
+                self._flush_grouped()
+            self._flush_bias()
+        if self.reductions:
+            K.reduce_partials_multi(self.reductions)
         for dy2, x2, N, w, b, beta, rt in self.items:
             _ready(rt, w, *([b] if b is not None else []))
-        if self.items and self.items[0][6].store is not None:
-            self.items[0][6].store.grad_sync()
+        for rt, p in self.reduced_params:
+            _ready(rt, p)
+        rts = [it[6] for it in self.items] + [rp[0] for rp in self.reduced_params]
+        if rts and rts[0].store is not None:
+            rts[0].store.grad_sync()
         self.items = []
+        self.reductions = []
+        self.reduced_params = []
         self._at_last_end = 0
 
     def _flush_ragged(self) -> bool:
@@ -267,9 +278,13 @@ def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt
     bias gradient (sum of ds over rows)."""
     h, mean, rstd, ks = saved
     if dy.is_cuda:
+        q = rt.wgrad
         dh, ds = K.ln_bwd(dy.contiguous(), h, mean, rstd, gamma.master, gamma.grad, beta.grad,
                           sub_bias.grad, rt.p, rt.seed, rt.ctr, site, want_ds=True,
-                          accumulate=rt.accumulate)
+                          accumulate=rt.accumulate, defer=q.reductions if q is not None else None)
+        if q is not None:  # folded (and reported ready) with the next wgrad flush
+            q.reduced_params += [(rt, gamma), (rt, beta), (rt, sub_bias)]
+            return dh, ds
     else:
         xhat = (h - mean) * rstd
         D = h.shape[-1]

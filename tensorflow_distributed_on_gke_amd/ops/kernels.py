@@ -369,18 +369,42 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
-           dres=None, accumulate=False):
+           dres=None, accumulate=False, defer=None):
+    """`defer` (a list): leave the dgamma / dbeta / dbias partial sums in a
+    per-site workspace and append their fold to `defer` (run later, all
+    LayerNorms of a backward in one launch, by reduce_partials_multi)."""
     D = dy.shape[-1]
     M = dy.numel() // D
     dh = torch.empty_like(dy)
     need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
     ds = torch.empty_like(dy) if need_ds else None
-    ws = workspace("ln_bwd", 3 * math.ceil(M / 8) * D, dy.device)
+    if defer is None:
+        ws = workspace("ln_bwd", 3 * math.ceil(M / 8) * D, dy.device)
+    else:  # partials must survive until the fold: one workspace per site
+        ws = workspace(f"ln_bwd_part_{site}", 3 * math.ceil(M / 8) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
-               accumulate)
+               accumulate, defer is not None)
+    if defer is not None:
+        nb = math.ceil(M / (4 * (2 if D >= 1024 else 4)))  # rows per ln_bwd block (norm.hip)
+        outs = [dgamma, dbeta] + ([dbias] if dbias is not None else [])
+        for i, o in enumerate(outs):
+            defer.append((ws[i * nb * D:(i + 1) * nb * D], o, nb, D, 1.0 if accumulate else 0.0))
     if ds is None:
         ds = dh
     return dh, ds
+
+
+def reduce_partials_multi(items) -> None:
+    """Fold deferred (partials, out, nparts, N, beta) column reductions; one
+    launch per (N, beta) group of up to 96."""
+    groups = {}
+    for part, out, nparts, N, beta in items:
+        groups.setdefault((N, beta), []).append((part, out, nparts))
+    for (N, beta), its in groups.items():
+        for c0 in range(0, len(its), 96):
+            ch = its[c0:c0 + 96]
+            C().reduce_partials_multi([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
+                                      N, beta)
 
 
 # ------------------------------------------------------------------ embedding / loss / optim

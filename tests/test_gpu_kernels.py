@@ -266,6 +266,16 @@ def test_add_ln_fwd_bwd(D, p):
     _close(dg, gr.grad, 2e-2, "ln dgamma")
     _close(db, br.grad, 1e-2, "ln dbeta")
     _close(dbias, sr.grad.sum(0), 2e-2, "ln fused dbias")
+    # deferred fold (partials kept per site, all folded in one launch later):
+    # bitwise the same column sums, also when accumulating
+    defer = []
+    dg2, db2, dbias2 = (torch.full((D,), 2.0, device=DEV) for _ in range(3))
+    kk.ln_bwd(dy.to(DEV), h, mean, rstd, gamma.to(DEV), dg2, db2, dbias2, p, seed, ctr.to(DEV),
+              site, accumulate=True, defer=defer)
+    assert len(defer) == 3 and torch.equal(dg2, torch.full((D,), 2.0, device=DEV))
+    kk.reduce_partials_multi(defer)
+    for got, want in ((dg2, dg), (db2, db), (dbias2, dbias)):
+        torch.testing.assert_close(got, want + 2.0, rtol=0, atol=1e-5)
 
 
 # --------------------------------------------------------------------------- embedding
