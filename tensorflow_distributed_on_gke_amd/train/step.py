@@ -27,6 +27,8 @@ from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 # data parallel: weight gradients flushed in wave-sized chunks at layer ends
 CHUNKED_WGRAD = os.environ.get("TDG_DP_CHUNKED_WGRAD", "1") != "0"
+# skip the optimizer's gradient zeroing (all GPU gradient writers overwrite)
+ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 
 
 class TrainStep:
@@ -52,6 +54,8 @@ class TrainStep:
             self.rt.wgrad = WgradQueue(flush_at_boundary=dp,
                                        wave_tiles=K.NUM_CU if dp and CHUNKED_WGRAD else 0)
         self.fp8 = fp8_state
+        if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
+            opt.zero_grad = False  # every GPU gradient writer overwrites
         # data parallel: each bucket's Adam runs as soon as its all-reduce is
         # done (decoder side during the encoder's backward)
         # (opt-in: on one MI355X with --force-dp the concurrent Adam contended

@@ -90,3 +90,31 @@ def test_gpu_backward_bitwise_deterministic():
         grads.append((out.clone(), m.store.flat_grad.clone()))
     assert torch.equal(grads[1][0], grads[2][0])
     assert torch.equal(grads[1][1], grads[2][1])
+
+
+def test_gpu_gradients_fully_overwritten():
+    """TrainStep skips the optimizer's gradient zeroing on the GPU: every
+    gradient writer of a non-accumulating backward must overwrite. Poison
+    every parameter gradient with NaN before a step: the update must come out
+    finite and bitwise equal to the zeroing optimizer's."""
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+    cfg = model_config("tiny", src_vocab=300, tgt_vocab=250, dropout=0.1)
+    src, tgt = _batch(8, 40, 33, cfg.src_vocab, cfg.tgt_vocab, seed=9)
+    src, tgt = src.cuda(), tgt.cuda()
+    flats = []
+    for poison in (False, True):
+        m = Transformer(cfg).build("cuda", seed=3)
+        opt = Adam(m.store, cfg.d_model, lr=1e-3)
+        step = TrainStep(m, opt, None, workers=1.0, seed=5)
+        assert opt.zero_grad is False
+        if not poison:
+            opt.zero_grad = True
+        for i in range(3):
+            if poison:
+                for p in m.store.params:
+                    p.grad.fill_(float("nan"))
+            step(src, tgt)
+        torch.cuda.synchronize()
+        assert torch.isfinite(m.store.flat).all()
+        flats.append(m.store.flat.clone())
+    assert torch.equal(flats[0], flats[1])
