@@ -1027,6 +1027,9 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
     TDG_CFG(9, 256, 128, 4, 2, 3)
     TDG_CFG(10, 128, 256, 2, 4, 3)
     TDG_CFG(11, 128, 128, 2, 2, 4)
+    // deeper pipelines for the latency-bound one-tile-per-CU shapes (8 waves)
+    TDG_CFG(13, 128, 128, 2, 4, 4)
+    TDG_CFG(14, 128, 128, 2, 4, 5)
     default:
       TDG_CFG(8, 64, 64, 2, 2, 2)
   }

@@ -25,7 +25,7 @@ from tensorflow_distributed_on_gke_amd.ops import kernels as kk  # noqa: E402
 from tensorflow_distributed_on_gke_amd.train.optim import Adam  # noqa: E402
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep  # noqa: E402
 
-CANDS = [(c, 1) for c in (0, 1, 2, 4, 7, 8, 11, 12)]
+CANDS = [(c, 1) for c in (0, 1, 2, 4, 7, 8, 11, 12, 13, 14)]
 
 
 def main():
