@@ -51,7 +51,7 @@ int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
 int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                     const int* shapes, int K, int a_kc, int b_kc, int out_f32, float alpha,
-                    float beta, hipStream_t st);
+                    float beta, float* const* bias_out, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
@@ -531,7 +531,8 @@ void gemm_grouped(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
 // shapes[i] = (M, N, lda, ldb, ldc), sharing K and the operand layouts.
 void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
                  const std::vector<Tensor>& Cs, const std::vector<int64_t>& shapes, int64_t K,
-                 bool a_kc, bool b_kc, double alpha, double beta) {
+                 bool a_kc, bool b_kc, double alpha, double beta,
+                 const std::vector<c10::optional<Tensor>>& bias_out) {
   const size_t P = As.size();
   TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && shapes.size() == 5 * P,
               "gemm_ragged: 1..64 problems, 5 shape values each");
@@ -563,9 +564,24 @@ void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
     c[i] = Cs[i].data_ptr();
     for (int j = 0; j < 5; ++j) sh[5 * i + j] = (int)shapes[5 * i + j];
   }
+  // optional fused bias gradients: bias_out[i][M_i] = alpha * row sums of A_i (+ beta * old)
+  TORCH_CHECK(bias_out.empty() || bias_out.size() == P, "gemm_ragged: bias_out must be empty or P long");
+  std::vector<float*> bo(P, nullptr);
+  bool any_bias = false;
+  for (size_t i = 0; i < bias_out.size(); ++i) {
+    if (!bias_out[i].has_value()) continue;
+    const Tensor& t = *bias_out[i];
+    TORCH_CHECK(!a_kc, "gemm_ragged: fused bias sums need an MN-contiguous A");
+    check_f32(t, "bias_out");
+    TORCH_CHECK(t.is_contiguous() && t.numel() == shapes[5 * i], "gemm_ragged: bias_out[", i,
+                "] must hold M floats");
+    bo[i] = t.data_ptr<float>();
+    any_bias = true;
+  }
   c10::DeviceGuard g(As[0].device());
   const int rc = tdg_gemm_ragged(a.data(), b.data(), c.data(), (int)P, sh.data(), (int)K, a_kc,
-                                 b_kc, f32, (float)alpha, (float)beta, stream_of(As[0]));
+                                 b_kc, f32, (float)alpha, (float)beta,
+                                 any_bias ? bo.data() : nullptr, stream_of(As[0]));
   check_err(rc, "tdg gemm_ragged");
 }
 
@@ -744,7 +760,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
   m.def("gemm_grouped", &gemm_grouped);
-  m.def("gemm_ragged", &gemm_ragged);
+  m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
+        py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),
+        py::arg("bias_out") = std::vector<c10::optional<Tensor>>{});
   m.def("colsum_grouped", &colsum_grouped);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);

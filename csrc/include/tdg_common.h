@@ -13,6 +13,8 @@ typedef uint16_t bf16_t;  // raw bf16 bits in memory
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef short short2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 

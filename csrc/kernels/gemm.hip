@@ -502,6 +502,9 @@ struct R256Args {
   const bf16_t* A[R256_MAXP];
   const bf16_t* B[R256_MAXP];
   void* C[R256_MAXP];
+  // optional fused bias gradient of problem i: bias_out[i][m] (=|+=) sum_k A[m][k]
+  // (row sums of the A operand over the whole K; only for A MN-contiguous)
+  float* bias_out[R256_MAXP];
   R256Class cls[R256_MAXC];
   int ncls;
 };
@@ -546,6 +549,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     tm = t % cl.tiles_m;
     tn = t / cl.tiles_m;
   }
+  // Fused bias gradient (weight-gradient launches): the tiles of the first
+  // N-column also sum their A fragments over K -- the A operand is dY^T, so
+  // its row sums are the bias gradient, read here from registers the MFMAs
+  // already hold instead of a second pass over dY. Wave wn sums fragments
+  // wn (rows 16wn.., half 0) and 4+wn (half 1) with v_dot2 against ones.
+  float* __restrict__ bias_out = A_KC ? nullptr : args.bias_out[p];
+  const bool do_bsum = bias_out != nullptr && tn == 0;
+  float bsum0 = 0.f, bsum1 = 0.f;
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = K / BK;  // host guarantees K % 64 == 0
 
@@ -671,6 +682,37 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
           for (int j = 0; j < 2; ++j)
             acc[i0 + i][j0 + j] = mfma16(fa[i0 + i][s2], fb[j0 + j][s2], acc[i0 + i][j0 + j]);
       __builtin_amdgcn_s_setprio(0);
+      if (do_bsum && (ph == 0 || ph == 2)) {
+        const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3f803f80);
+        float bs = ph == 0 ? bsum0 : bsum1;
+        // constant fragment indices only (a wave-uniform branch per candidate):
+        // a runtime index would move fa[] to scratch
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (i != wn) continue;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const short8_t f = ph == 0 ? fa[i][s2] : fa[4 + i][s2];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              bs = __builtin_amdgcn_fdot2_f32_bf16(
+                  __builtin_bit_cast(bf16x2_t, (short2_t){f[2 * e], f[2 * e + 1]}), one, bs, false);
+          }
+        }
+        if (ph == 0) bsum0 = bs;
+        else bsum1 = bs;
+      }
+    }
+  }
+  if (do_bsum) {  // lanes l, l+16, l+32, l+48 hold disjoint K subsets of row l&15
+    bsum0 += __shfl_xor(bsum0, 16, 64);
+    bsum0 += __shfl_xor(bsum0, 32, 64);
+    bsum1 += __shfl_xor(bsum1, 16, 64);
+    bsum1 += __shfl_xor(bsum1, 32, 64);
+    if (lane < 16) {
+      const int mA = m0 + wm * 128 + 16 * wn + lane, mB = mA + 64;
+      if (mA < M) bias_out[mA] = alpha * bsum0 + (beta != 0.f ? beta * bias_out[mA] : 0.f);
+      if (mB < M) bias_out[mB] = alpha * bsum1 + (beta != 0.f ? beta * bias_out[mB] : 0.f);
     }
   }
 
@@ -1111,7 +1153,7 @@ extern "C" int tdg_gemm_grouped(const void* const* A, const void* const* B, void
 // success.
 extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                                const int* shapes, int K, int a_kc, int b_kc, int out_f32,
-                               float alpha, float beta, hipStream_t st) {
+                               float alpha, float beta, float* const* bias_out, hipStream_t st) {
   if (P < 1 || P > R256_MAXP) return -2;
   R256Args args{};
   int ncls = 0, tiles = 0;
@@ -1133,6 +1175,8 @@ extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void*
     args.A[i] = (const bf16_t*)A[i];
     args.B[i] = (const bf16_t*)B[i];
     args.C[i] = C[i];
+    args.bias_out[i] = bias_out ? bias_out[i] : nullptr;
+    if (args.bias_out[i] && a_kc) return -7;  // row sums need the MN-contiguous A path
   }
   args.ncls = ncls;
 #define TDG_RG(AK, BKc, F) \

@@ -169,10 +169,10 @@ class WgradQueue:
     def flush(self) -> None:
         if self.items:
             if RAGGED_WGRAD and self._flush_ragged():
-                pass
+                pass  # bias gradients fused into the ragged launch
             else:
                 self._flush_grouped()
-            self._flush_bias()
+                self._flush_bias()
         if self.reductions:
             K.reduce_partials_multi(self.reductions)
         for dy2, x2, N, w, b, beta, rt in self.items:
@@ -205,7 +205,8 @@ class WgradQueue:
                 for c0 in range(0, len(chunk), K.RAGGED_MAX_PROBLEMS):
                     part = chunk[c0:c0 + K.RAGGED_MAX_PROBLEMS]
                     K.wgrad_ragged([i[0] for i in part], [i[1] for i in part],
-                                   [i[3].grad for i in part], beta)
+                                   [i[3].grad for i in part], beta,
+                                   [i[4].grad if i[4] is not None else None for i in part])
         return True
 
     def _flush_grouped(self) -> None:

@@ -142,9 +142,21 @@ def test_wgrad_ragged():
         dys.append(dy[:, :n_out] if n_out == 7010 else dy)
         xs.append(x)
         dws.append(dw)
-    kk.wgrad_ragged(dys, xs, dws, beta=1.0)
+    # fused bias gradients on every other problem (row sums of dy^T over tokens)
+    biases, brefs = [], []
+    for i, (n_out, _) in enumerate(spec):
+        if i % 2 == 0:
+            b = _rand(n_out, seed=400 + i).to(DEV)
+            brefs.append(dys[i].float().sum(0) + b)
+            biases.append(b)
+        else:
+            biases.append(None)
+            brefs.append(None)
+    kk.wgrad_ragged(dys, xs, dws, beta=1.0, biases=biases)
     for i in range(len(spec)):
         _close(dws[i], refs[i], 2e-3, f"ragged wgrad {i} {spec[i]}")
+        if brefs[i] is not None:
+            _close(biases[i], brefs[i], 1e-4, f"ragged fused bias {i} {spec[i]}")
 
 
 def test_linear_wrappers_padded_vocab():
