@@ -43,7 +43,14 @@ int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, i
 int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable, long long* acc,
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
+int tdg_gemm_ln(const void* A, int lda, const void* W, int ldw, const float* bias, const void* X,
+                int ldx, const float* gamma, const float* beta, void* Y, void* H, float* mean,
+                float* rstd, int M, int K, int D, float p, uint64_t seed, const long long* ctr,
+                uint64_t site, float eps, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
+int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, int B, int lab64, void* tgt_in,
+                   void* labels, int* src_len, int* tgt_len, float* ntok, long long* ctr,
+                   int* row_lab, unsigned* ticket, hipStream_t st);
 int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* part, int M, int N,
                        int ld, int rows_per_block, float beta, hipStream_t st);
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
@@ -356,6 +363,40 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
                             y8 ? y8->data_ptr() : nullptr, s8 ? s8->data_ptr<float>() : nullptr,
                             amax_ptr(amax8), stream_of(x));
   check_err(rc, "tdg ln_fwd");
+}
+
+// Fused output projection + bias + dropout + residual + LayerNorm:
+// y = LN(x + dropout(a @ w^T + bias)). Returns 0, or a negative code when the
+// shape is not covered (nothing launched; the caller runs GEMM + ln_fwd).
+int64_t gemm_ln(const Tensor& a, const Tensor& w, const Tensor& bias, const Tensor& x,
+                const Tensor& gamma, const Tensor& beta, const Tensor& y, const Tensor& hsave,
+                const Tensor& mean, const Tensor& rstd, double p, int64_t seed,
+                const optional<Tensor>& ctr, int64_t site, double eps) {
+  check_bf16(a, "a");
+  check_bf16(w, "w");
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  check_bf16(hsave, "hsave");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && x.dim() == 2, "gemm_ln: 2-D a, w, x");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && x.stride(1) == 1, "gemm_ln: row-major");
+  const int64_t M = a.size(0), K = a.size(1), D = w.size(0);
+  TORCH_CHECK(w.size(1) == K && x.size(0) == M && x.size(1) == D, "gemm_ln: shapes");
+  TORCH_CHECK(y.is_contiguous() && hsave.is_contiguous() && y.numel() == M * D &&
+                  hsave.numel() == M * D, "gemm_ln: y / hsave must be contiguous [M, D]");
+  for (const Tensor* t : {&bias, &gamma, &beta}) {
+    check_f32(*t, "bias/gamma/beta");
+    TORCH_CHECK(t->numel() == D && t->is_contiguous(), "gemm_ln: vectors must hold D floats");
+  }
+  for (const Tensor* t : {&mean, &rstd}) {
+    check_f32(*t, "mean/rstd");
+    TORCH_CHECK(t->numel() == M, "gemm_ln: mean/rstd shape");
+  }
+  c10::DeviceGuard g(a.device());
+  return tdg_gemm_ln(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0),
+                     bias.data_ptr<float>(), x.data_ptr(), (int)x.stride(0), gamma.data_ptr<float>(),
+                     beta.data_ptr<float>(), y.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), (int)M, (int)K, (int)D, (float)p, (uint64_t)seed,
+                     ctr_ptr(ctr), (uint64_t)site, (float)eps, stream_of(a));
 }
 
 void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Tensor& rstd,
@@ -679,6 +720,42 @@ void count_tokens(const Tensor& labels, const Tensor& out) {
             "tdg count_tokens");
 }
 
+// tgt_in, labels [B, T] (token dtype), src_len, tgt_len [B] int32, ntok [1] f32,
+// ctr (optional int64 [1], += 1)
+void prep_batch(const Tensor& src, const Tensor& tgt, const Tensor& tgt_in, const Tensor& labels,
+                const Tensor& src_len, const Tensor& tgt_len, const Tensor& ntok,
+                const c10::optional<Tensor>& ctr, const Tensor& scratch) {
+  TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous(), "prep_batch: src");
+  TORCH_CHECK(tgt.is_cuda() && tgt.dim() == 2 && tgt.is_contiguous() && tgt.size(0) == src.size(0),
+              "prep_batch: tgt");
+  const auto dt = src.scalar_type();
+  TORCH_CHECK((dt == at::kLong || dt == at::kInt) && tgt.scalar_type() == dt,
+              "prep_batch: tokens must be int64 or int32 (both)");
+  const int64_t B = src.size(0), S = src.size(1), T1 = tgt.size(1);
+  TORCH_CHECK(T1 >= 2, "prep_batch: target needs >= 2 tokens");
+  for (const Tensor* t : {&tgt_in, &labels})
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == dt &&
+                    t->numel() == B * (T1 - 1), "prep_batch: tgt_in / labels");
+  for (const Tensor* t : {&src_len, &tgt_len})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() == B, "prep_batch: lengths");
+  check_f32(ntok, "ntok");
+  // scratch: int32 [B + 1] -- per-row label counts + a zero-initialised ticket
+  TORCH_CHECK(scratch.is_cuda() && scratch.scalar_type() == at::kInt && scratch.numel() >= B + 1,
+              "prep_batch: scratch must be int32 [B + 1], last word zero");
+  long long* c = nullptr;
+  if (ctr.has_value()) {
+    TORCH_CHECK(ctr->is_cuda() && ctr->scalar_type() == at::kLong, "prep_batch: ctr");
+    c = reinterpret_cast<long long*>(ctr->data_ptr<int64_t>());
+  }
+  c10::DeviceGuard g(src.device());
+  check_err(tdg_prep_batch(src.data_ptr(), (int)S, tgt.data_ptr(), (int)T1, (int)B, dt == at::kLong,
+                           tgt_in.data_ptr(), labels.data_ptr(), src_len.data_ptr<int>(),
+                           tgt_len.data_ptr<int>(), ntok.data_ptr<float>(), c,
+                           scratch.data_ptr<int>(),
+                           reinterpret_cast<unsigned*>(scratch.data_ptr<int>() + B), stream_of(src)),
+            "tdg prep_batch");
+}
+
 void xent(const Tensor& logits, int64_t V, const Tensor& labels, const Tensor& ntok,
           double workers, double smoothing, const Tensor& row_loss, const Tensor& row_correct,
           bool write_grad) {
@@ -773,11 +850,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_probs", &attn_probs);
   m.def("ln_fwd", &ln_fwd);
+  m.def("gemm_ln", &gemm_ln);
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("embed_bwd_det", &embed_bwd_det);
   m.def("count_tokens", &count_tokens);
+  m.def("prep_batch", &prep_batch);
   m.def("xent", &xent);
   m.def("xent_stats", &xent_stats);
   m.def("adam", &adam);

@@ -125,6 +125,55 @@ __global__ void count_tokens_kernel(const LabT* __restrict__ labels, int M, floa
   if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Batch preparation in one launch (replaces ~10 small framework kernels at the
+// head of every step): teacher forcing tgt_in = tgt[:, :-1], labels =
+// tgt[:, 1:] (reference: __main__.py:106-107), non-PAD lengths of src and
+// tgt_in (the padding masks, transformer_model.py:56-62, as key lengths), the
+// non-PAD label count, and the dropout RNG step counter bump. One workgroup,
+// one wave per row at a time.
+template <typename LabT>
+__global__ __launch_bounds__(64) void prep_batch_kernel(
+    const LabT* __restrict__ src, int S, const LabT* __restrict__ tgt, int T1, int B,
+    LabT* __restrict__ tgt_in, LabT* __restrict__ labels, int* __restrict__ src_len,
+    int* __restrict__ tgt_len, float* __restrict__ ntok, long long* __restrict__ ctr,
+    int* __restrict__ row_lab, unsigned* __restrict__ ticket) {
+  // one wave per row; the last wave to finish folds the label counts
+  const int lane = threadIdx.x, b = blockIdx.x, T = T1 - 1;
+  int cs = 0, ct = 0, cl = 0;
+  for (int j = lane; j < S; j += 64) cs += src[(long long)b * S + j] != 0;
+  for (int j = lane; j < T1; j += 64) {
+    const LabT v = tgt[(long long)b * T1 + j];
+    if (j < T) {
+      tgt_in[(long long)b * T + j] = v;
+      ct += v != 0;
+    }
+    if (j > 0) {
+      labels[(long long)b * T + j - 1] = v;
+      cl += v != 0;
+    }
+  }
+  const float fs = wave_sum((float)cs), ft = wave_sum((float)ct), fl = wave_sum((float)cl);
+  __shared__ bool last;
+  if (lane == 0) {
+    src_len[b] = (int)fs;
+    tgt_len[b] = (int)ft;
+    row_lab[b] = (int)fl;
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == (unsigned)(B - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  int n = 0;  // integer counts: exact and order-independent
+  for (int i = lane; i < B; i += 64) n += __atomic_load_n(row_lab + i, __ATOMIC_RELAXED);
+  const float tot = wave_sum((float)n);
+  if (lane == 0) {
+    ntok[0] = tot;
+    if (ctr) ctr[0] += 1;
+    *ticket = 0u;  // re-armed for the next launch (graph replay)
+  }
+}
+
 // stats[0] += sum(row_loss)/(ntok*workers), stats[1] += correct/ntok (accuracy
 // ratio), stats[2] += 1 (batches), stats[3] += ntok; single block.
 __global__ void xent_stats_kernel(const float* __restrict__ row_loss,
@@ -172,6 +221,22 @@ extern "C" int tdg_count_tokens(const void* labels, int lab64, int M, float* out
   else
     hipLaunchKernelGGL(count_tokens_kernel<int>, dim3(1), dim3(256), 0, st, (const int*)labels, M,
                        out);
+  return 0;
+}
+
+extern "C" int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, int B, int lab64,
+                               void* tgt_in, void* labels, int* src_len, int* tgt_len,
+                               float* ntok, long long* ctr, int* row_lab, unsigned* ticket,
+                               hipStream_t st) {
+  if (S < 1 || T1 < 2 || B < 1) return -1;
+  if (lab64)
+    hipLaunchKernelGGL(prep_batch_kernel<long long>, dim3(B), dim3(64), 0, st,
+                       (const long long*)src, S, (const long long*)tgt, T1, B, (long long*)tgt_in,
+                       (long long*)labels, src_len, tgt_len, ntok, ctr, row_lab, ticket);
+  else
+    hipLaunchKernelGGL(prep_batch_kernel<int>, dim3(B), dim3(64), 0, st, (const int*)src, S,
+                       (const int*)tgt, T1, B, (int*)tgt_in, (int*)labels, src_len, tgt_len, ntok,
+                       ctr, row_lab, ticket);
   return 0;
 }
 

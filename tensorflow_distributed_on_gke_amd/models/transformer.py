@@ -231,9 +231,8 @@ class Transformer:
             x = layer(x, kv_all, kvh, src_len, tgt_len, rt)
         return x
 
-    def features(self, src, tgt_in, rt: RunCtx):
-        src_len = seq_lengths(src)
-        tgt_len = seq_lengths(tgt_in)
+    def features(self, src, tgt_in, rt: RunCtx, lengths=None):
+        src_len, tgt_len = lengths if lengths is not None else (seq_lengths(src), seq_lengths(tgt_in))
         enc = self.encode(src, src_len, rt)
         return self.decode(tgt_in, enc, src_len, tgt_len, rt)
 
@@ -259,27 +258,35 @@ class Transformer:
     # ------------------------------------------------------------------ training
     def loss_and_backward(self, src, tgt, rt: RunCtx, workers: float,
                           accum: Optional[torch.Tensor] = None, backward: bool = True,
-                          step_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                          step_out: Optional[torch.Tensor] = None,
+                          bump_ctr: bool = False) -> torch.Tensor:
         """Teacher-forced forward, masked CE / accuracy, and (if `backward`)
         the full backward into the flat gradient buffer. Returns a device
         tensor [local_loss, accuracy] (loss already / workers, as the
-        reference's local_loss_function). No host synchronisation."""
+        reference's local_loss_function). No host synchronisation.
+        bump_ctr: advance the dropout RNG step counter rt.ctr first."""
         cfg = self.cfg
-        tgt_in = tgt[:, :-1].contiguous()
-        labels = tgt[:, 1:].contiguous()
+        dev = src.device
+        if dev.type == "cuda":  # split / lengths / token count / ctr: one launch
+            tgt_in, labels, src_len, tgt_len, ntok = K.prep_batch(
+                src, tgt, rt.ctr if bump_ctr else None)
+            lengths = (src_len, tgt_len)
+        else:
+            if bump_ctr:
+                rt.ctr.add_(1)
+            tgt_in = tgt[:, :-1].contiguous()
+            labels = tgt[:, 1:].contiguous()
+            lengths = None
         B, T = tgt_in.shape
         M = B * T
-        dev = src.device
         if step_out is None:
             step_out = torch.zeros(2, dtype=torch.float32, device=dev)
         grad_ctx = torch.enable_grad() if backward else torch.no_grad()
         with grad_ctx:
-            dec = self.features(src, tgt_in, rt)
+            dec = self.features(src, tgt_in, rt, lengths)
         dec2 = dec.detach().reshape(M, cfg.d_model)
         if dev.type == "cuda":
             logits = self.project(dec.detach())
-            ntok = K.workspace("ntok", 1, dev)[:1]
-            K.count_tokens(labels, ntok)
             row_loss = K.workspace("row_loss", M, dev)[:M]
             row_cor = K.workspace("row_correct", M, dev)[:M]
             K.xent(logits, cfg.tgt_vocab, labels, ntok, workers, cfg.label_smoothing, row_loss,

@@ -371,6 +371,34 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
     return y, h, mean, rstd
 
 
+# Fused projection + LayerNorm (csrc/kernels/gemm_ln.hip) is opt-in: with one
+# workgroup per 32 full rows every workgroup streams all of W, and on MI355X
+# that measured slower than the 128x128-tile GEMM + standalone LayerNorm
+# (8192 rows: 35 vs 25 us at K=512, 97 vs 39 us at K=2048; profiles/
+# pmc_gemm_ln_v1.txt: 2.3x the L2 requests of the tiled GEMM).
+GEMM_LN = os.environ.get("TDG_GEMM_LN", "0") != "0"
+
+
+def gemm_ln_ok(a2, w, x2) -> bool:
+    """Shapes the fused projection + LayerNorm kernel covers (d_model 512)."""
+    return (GEMM_LN and w.shape[0] == 512 and a2.shape[1] % 64 == 0 and a2.stride(1) == 1
+            and x2.stride(1) == 1 and a2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and w.stride(0) % 8 == 0)
+
+
+def gemm_ln(a2, w, bias, x2, gamma, beta, p, seed, ctr, site, eps=1e-6):
+    """y = LN(x + dropout(a @ w^T + bias)) in one launch (csrc/kernels/gemm_ln.hip).
+    Returns (y, h, mean, rstd) like ln_fwd, or None if the shape is not covered."""
+    M, D = x2.shape
+    y = torch.empty(M, D, dtype=torch.bfloat16, device=x2.device)
+    h = torch.empty_like(y)
+    stats = torch.empty(2, M, dtype=torch.float32, device=x2.device)
+    rc = C().gemm_ln(a2, w, bias, x2, gamma, beta, y, h, stats[0], stats[1], p, seed, ctr, site, eps)
+    if rc != 0:
+        return None
+    return y, h, stats[0], stats[1]
+
+
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
            dres=None, accumulate=False, defer=None):
     """`defer` (a list): leave the dgamma / dbeta / dbias partial sums in a
@@ -435,6 +463,28 @@ def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False):
 
 def count_tokens(labels, out):
     C().count_tokens(labels, out)
+
+
+_PREP_SCRATCH: Dict[tuple, torch.Tensor] = {}
+
+
+def prep_batch(src, tgt, ctr=None):
+    """One launch: (tgt_in, labels, src_len, tgt_len, ntok) of a teacher-forced
+    batch -- tgt[:, :-1], tgt[:, 1:], int32 non-PAD lengths, f32 [1] non-PAD
+    label count -- and ctr += 1 when given (the dropout RNG step)."""
+    src = src.contiguous()
+    tgt = tgt.contiguous()
+    B, T1 = tgt.shape
+    tgt_in = torch.empty(B, T1 - 1, dtype=tgt.dtype, device=tgt.device)
+    labels = torch.empty(B, T1 - 1, dtype=tgt.dtype, device=tgt.device)
+    lens = torch.empty(2, B, dtype=torch.int32, device=tgt.device)
+    ntok = torch.empty(1, dtype=torch.float32, device=tgt.device)
+    key = (tgt.device, B)
+    scratch = _PREP_SCRATCH.get(key)
+    if scratch is None:  # [B] label counts + ticket (zero; the kernel re-arms it)
+        scratch = _PREP_SCRATCH[key] = torch.zeros(B + 1, dtype=torch.int32, device=tgt.device)
+    C().prep_batch(src, tgt, tgt_in, labels, lens[0], lens[1], ntok, ctr, scratch)
+    return tgt_in, labels, lens[0], lens[1], ntok
 
 
 def xent(logits, V, labels, ntok, workers, smoothing, row_loss, row_correct, write_grad=True):

@@ -70,9 +70,8 @@ class TrainStep:
         self._static: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     def eager(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
-        self.rt.ctr.add_(1)
         self.model.loss_and_backward(src, tgt, self.rt, self.workers, accum=self.accum,
-                                     step_out=self.last)
+                                     step_out=self.last, bump_ctr=True)
         if self.ddp is not None:
             self.ddp.finish()
         else:

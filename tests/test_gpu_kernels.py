@@ -403,3 +403,58 @@ def test_gemm_library_beta_accumulate():
         C = C0.clone()
         kk.gemm(A, B, C, M, N, Kd, Kd, N, N, True, False, beta=1.0, cfg=cfg)
         _close(C, ref, 2e-2, f"beta=1 {cfg}")
+
+
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_prep_batch(dtype):
+    """Fused batch preparation: teacher-forcing split, non-PAD lengths, label
+    count and the RNG step bump, vs plain torch."""
+    g = torch.Generator().manual_seed(5)
+    B, S, T1 = 37, 71, 130
+    src = torch.randint(1, 100, (B, S), generator=g, dtype=dtype)
+    tgt = torch.randint(1, 100, (B, T1), generator=g, dtype=dtype)
+    for b in range(B):  # right padding with PAD = 0
+        src[b, torch.randint(1, S + 1, (1,), generator=g).item():] = 0
+        tgt[b, torch.randint(2, T1 + 1, (1,), generator=g).item():] = 0
+    ctr = torch.tensor([41], dtype=torch.int64, device=DEV)
+    tgt_in, labels, sl, tl, ntok = kk.prep_batch(src.to(DEV), tgt.to(DEV), ctr)
+    assert torch.equal(tgt_in.cpu(), tgt[:, :-1])
+    assert torch.equal(labels.cpu(), tgt[:, 1:])
+    assert torch.equal(sl.cpu(), (src != 0).sum(1).to(torch.int32))
+    assert torch.equal(tl.cpu(), (tgt[:, :-1] != 0).sum(1).to(torch.int32))
+    assert ntok.item() == float((tgt[:, 1:] != 0).sum())
+    assert ctr.item() == 42
+
+
+@pytest.mark.parametrize("M,K", [(300, 512), (8192, 512), (1000, 2048)])
+def test_gemm_ln_matches_unfused(M, K):
+    """Fused projection + bias + dropout + residual + LayerNorm (one launch)
+    vs the GEMM then the standalone LayerNorm: the fused epilogue runs the same
+    row code on the same bf16 s, so the outputs must agree bitwise; and both
+    against an fp32 torch reference."""
+    D, p, seed, site = 512, 0.1, 1234, 9
+    a = _bf(_rand(M, K, seed=61)).to(DEV)
+    w = _bf(_rand(D, K, scale=1.0 / math.sqrt(K), seed=62)).to(DEV)
+    b = _rand(D, scale=0.1, seed=63).to(DEV)
+    x = _bf(_rand(M, D, seed=64)).to(DEV)
+    gamma = (1.0 + 0.1 * _rand(D, seed=65)).to(DEV)
+    beta = (0.1 * _rand(D, seed=66)).to(DEV)
+    ctr = torch.tensor([7], dtype=torch.int64, device=DEV)
+    r = kk.gemm_ln(a, w, b, x, gamma, beta, p, seed, ctr, site)
+    assert r is not None
+    y, h, mean, rstd = r
+    s = kk.linear_fwd(a, w, b)
+    y2, h2, mean2, rstd2 = kk.ln_fwd(x, s, gamma, beta, p, seed, ctr, site)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h2), "hsave differs from GEMM + ln_fwd"
+    assert torch.equal(y, y2), "y differs from GEMM + ln_fwd"
+    assert torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    # fp32 reference with the same dropout keep mask (dropped s -> h == x exactly where masked)
+    sf = (a.float() @ w.float().t() + b).to(torch.bfloat16).float()
+    keep = (h.float() - x.float()).abs() > 0
+    hf = x.float() + torch.where(keep, sf / (1 - p), torch.zeros_like(sf))
+    mu = hf.mean(-1, keepdim=True)
+    yf = (hf - mu) * torch.rsqrt(((hf - mu) ** 2).mean(-1, keepdim=True) + 1e-6) * gamma + beta
+    _close(y, yf, 3e-2, "gemm_ln vs fp32")
+    frac = keep.float().mean().item()
+    assert 0.85 < frac < 0.95, f"dropout keep fraction {frac}"
