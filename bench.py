@@ -48,7 +48,8 @@ def main() -> None:
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype (bf16 halves xGMI bytes)")
-    ap.add_argument("--graph", type=int, default=-1, help="1: capture step in a HIP graph (default: on for 1 GPU)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1: capture step in a HIP graph (default: on for 1 GPU without data parallelism)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--defer-wgrad", type=int, default=-1,
                     help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
@@ -88,7 +89,9 @@ def main() -> None:
         s, t = data.batch(i)
         batches.append((s.to(dev, non_blocking=True), t.to(dev, non_blocking=True)))
 
-    use_graph = args.graph if args.graph >= 0 else int(world == 1 and dev.type == "cuda")
+    # HIP graph on one GPU only: the data-parallel path (also the --force-dp
+    # single-rank rehearsal of it) runs eager, its collectives outside capture
+    use_graph = args.graph if args.graph >= 0 else int(ddp is None and dev.type == "cuda")
     if use_graph:
         step.capture(*batches[0])
     for i in range(args.warmup):

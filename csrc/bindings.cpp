@@ -575,17 +575,18 @@ void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
                  bool a_kc, bool b_kc, double alpha, double beta,
                  const std::vector<c10::optional<Tensor>>& bias_out) {
   const size_t P = As.size();
-  TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && shapes.size() == 5 * P,
-              "gemm_ragged: 1..64 problems, 5 shape values each");
+  TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && shapes.size() == 7 * P,
+              "gemm_ragged: 1..64 problems, 7 shape values each (M, N, lda, ldb, ldc, t_first, "
+              "t_count)");
   TORCH_CHECK(K > 0 && K % 64 == 0, "gemm_ragged: K must be a multiple of 64");
   auto r8 = [](int64_t v) { return (v + 7) / 8 * 8; };
   const bool f32 = Cs[0].scalar_type() == at::kFloat;
   std::vector<const void*> a(P), b(P);
   std::vector<void*> c(P);
-  std::vector<int> sh(5 * P);
+  std::vector<int> sh(7 * P);
   for (size_t i = 0; i < P; ++i) {
-    const int64_t M = shapes[5 * i], N = shapes[5 * i + 1], lda = shapes[5 * i + 2],
-                  ldb = shapes[5 * i + 3], ldc = shapes[5 * i + 4];
+    const int64_t M = shapes[7 * i], N = shapes[7 * i + 1], lda = shapes[7 * i + 2],
+                  ldb = shapes[7 * i + 3], ldc = shapes[7 * i + 4];
     TORCH_CHECK(M > 0 && N > 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc >= N, "gemm_ragged: shape");
     check_bf16(As[i], "A");
     check_bf16(Bs[i], "B");
@@ -603,7 +604,7 @@ void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
     a[i] = As[i].data_ptr();
     b[i] = Bs[i].data_ptr();
     c[i] = Cs[i].data_ptr();
-    for (int j = 0; j < 5; ++j) sh[5 * i + j] = (int)shapes[5 * i + j];
+    for (int j = 0; j < 7; ++j) sh[7 * i + j] = (int)shapes[7 * i + j];
   }
   // optional fused bias gradients: bias_out[i][M_i] = alpha * row sums of A_i (+ beta * old)
   TORCH_CHECK(bias_out.empty() || bias_out.size() == P, "gemm_ragged: bias_out must be empty or P long");
@@ -614,7 +615,7 @@ void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
     const Tensor& t = *bias_out[i];
     TORCH_CHECK(!a_kc, "gemm_ragged: fused bias sums need an MN-contiguous A");
     check_f32(t, "bias_out");
-    TORCH_CHECK(t.is_contiguous() && t.numel() == shapes[5 * i], "gemm_ragged: bias_out[", i,
+    TORCH_CHECK(t.is_contiguous() && t.numel() == shapes[7 * i], "gemm_ragged: bias_out[", i,
                 "] must hold M floats");
     bo[i] = t.data_ptr<float>();
     any_bias = true;

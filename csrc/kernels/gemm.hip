@@ -338,7 +338,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 // 128 FLOP per LDS byte vs 64 for 128x128 tiles.
 constexpr int R256_MAXP = 64, R256_MAXC = 8;
 struct R256Class {
-  int M, N, lda, ldb, ldc, tiles_m, tiles_n, tile_start, prob_start;
+  // t_first: tile index (within the problem) of the class's first tile -- a
+  // class may cover a tile sub-range of a single problem, so a long list of
+  // weight gradients can be cut into launches of exactly one wave of tiles
+  int M, N, lda, ldb, ldc, tiles_m, tiles_n, tile_start, prob_start, t_first;
 };
 struct R256Args {
   const bf16_t* A[R256_MAXP];
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     if (i < args.ncls && t0 >= args.cls[i].tile_start) cl = args.cls[i];
   const int M = cl.M, N = cl.N, lda = cl.lda, ldb = cl.ldb, ldc = cl.ldc;
   const int tpp = cl.tiles_m * cl.tiles_n;
-  const int lt = t0 - cl.tile_start;
+  const int lt = t0 - cl.tile_start + cl.t_first;
   const int p = cl.prob_start + lt / tpp;
   const int t = lt % tpp;
   const bf16_t* __restrict__ A = args.A[p];
@@ -867,7 +870,7 @@ inline int r256_single(R256Args& a, const bf16_t* const* A, const bf16_t* const*
   R256Class& c = a.cls[0];
   c.M = M; c.N = N; c.lda = lda; c.ldb = ldb; c.ldc = ldc;
   c.tiles_m = cdiv(M, 256); c.tiles_n = cdiv(N, 256);
-  c.tile_start = 0; c.prob_start = 0;
+  c.tile_start = 0; c.prob_start = 0; c.t_first = 0;
   return G * c.tiles_m * c.tiles_n;
 }
 
@@ -990,30 +993,36 @@ extern "C" int tdg_gemm_grouped(const void* const* A, const void* const* B, void
 }
 
 // Ragged grouped GEMM: P (<= 64) problems sharing K and layout, in runs of
-// equal shape (<= 8 distinct shapes), plain epilogue, ONE launch of 256x256
-// tiles. shapes[5*i..] = (M, N, lda, ldb, ldc) of problem i. Returns 0 on
-// success.
+// equal shape (<= 8 runs), plain epilogue, ONE launch of 256x256 tiles.
+// shapes[7*i..] = (M, N, lda, ldb, ldc, t_first, t_count) of problem i:
+// tiles [t_first, t_first + t_count) of it (t_count < 0: all; a partial
+// problem is a run of its own). Returns 0 on success.
 extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                                const int* shapes, int K, int a_kc, int b_kc, int out_f32,
                                float alpha, float beta, float* const* bias_out, hipStream_t st) {
   if (P < 1 || P > R256_MAXP) return -2;
   R256Args args{};
   int ncls = 0, tiles = 0;
+  bool prev_partial = false;
   for (int i = 0; i < P; ++i) {
-    const int* s = shapes + 5 * i;
-    const bool same = ncls > 0 && args.cls[ncls - 1].M == s[0] && args.cls[ncls - 1].N == s[1] &&
-                      args.cls[ncls - 1].lda == s[2] && args.cls[ncls - 1].ldb == s[3] &&
-                      args.cls[ncls - 1].ldc == s[4];
+    const int* s = shapes + 7 * i;
+    const int tpp = cdiv(s[0], 256) * cdiv(s[1], 256);
+    const int first = s[5], count = s[6] < 0 ? tpp - s[5] : s[6];
+    if (first < 0 || count <= 0 || first + count > tpp) return -8;
+    const bool partial = count != tpp;
+    const bool same = ncls > 0 && !partial && !prev_partial && args.cls[ncls - 1].M == s[0] &&
+                      args.cls[ncls - 1].N == s[1] && args.cls[ncls - 1].lda == s[2] &&
+                      args.cls[ncls - 1].ldb == s[3] && args.cls[ncls - 1].ldc == s[4];
     if (!same) {
       if (ncls == R256_MAXC) return -5;
       R256Class& c = args.cls[ncls++];
       c.M = s[0]; c.N = s[1]; c.lda = s[2]; c.ldb = s[3]; c.ldc = s[4];
       c.tiles_m = cdiv(s[0], 256); c.tiles_n = cdiv(s[1], 256);
-      c.tile_start = tiles; c.prob_start = i;
+      c.tile_start = tiles; c.prob_start = i; c.t_first = first;
       if ((!a_kc && s[2] % 8) || (!b_kc && s[3] % 8)) return -6;
     }
-    const R256Class& c = args.cls[ncls - 1];
-    tiles += c.tiles_m * c.tiles_n;
+    prev_partial = partial;
+    tiles += count;
     args.A[i] = (const bf16_t*)A[i];
     args.B[i] = (const bf16_t*)B[i];
     args.C[i] = C[i];

@@ -299,19 +299,24 @@ def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
 RAGGED_MAX_PROBLEMS, RAGGED_MAX_SHAPES = 64, 8
 
 
-def wgrad_ragged(dys, xs, dws, beta: float = 0.0, biases=None) -> None:
+def wgrad_ragged(dys, xs, dws, beta: float = 0.0, biases=None, ranges=None) -> None:
     """dws[i][N_i,K_i] (f32) (+)= dys[i][M,N_i]^T @ xs[i][M,K_i] for up to 64
     problems of up to 8 shapes sharing the token count M, as ONE launch of
     256x256 tiles (ragged grouping, csrc/kernels/gemm.hip gemm256_kernel).
     Problems of equal shape must be adjacent. biases[i] (f32 [N_i] or None):
     the bias gradient sum_m dys[i][m] (+ beta * old), summed inside the same
-    launch from the dY fragments the MFMAs consume (no second pass over dY)."""
+    launch from the dY fragments the MFMAs consume (no second pass over dY).
+    ranges[i] = (t_first, t_count) or None: only those 256x256 tiles of
+    problem i (in the kernel's enumeration of its tile grid); a cut problem
+    gets a shape class of its own."""
     M = xs[0].shape[0]
     shapes = []
-    for dy, x, dw in zip(dys, xs, dws):
+    for i, (dy, x, dw) in enumerate(zip(dys, xs, dws)):
         if x.shape[0] != M or dy.shape[0] != M:
             raise ValueError("wgrad_ragged: all problems must share the token count")
+        r = ranges[i] if ranges is not None else None
         shapes += [dw.shape[0], x.shape[1], dy.stride(0), x.stride(0), dw.stride(0)]
+        shapes += [0, -1] if r is None else [int(r[0]), int(r[1])]
     C().gemm_ragged(list(dys), list(xs), list(dws), shapes, M, False, False, 1.0, beta,
                     list(biases) if biases is not None else [])
 

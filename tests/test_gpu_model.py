@@ -118,3 +118,38 @@ def test_gpu_gradients_fully_overwritten():
         assert torch.isfinite(m.store.flat).all()
         flats.append(m.store.flat.clone())
     assert torch.equal(flats[0], flats[1])
+
+
+@pytest.mark.parametrize("wave", [7, 64])
+def test_gpu_wgrad_wave_chunks_bitwise(wave):
+    """Data-parallel weight-gradient schedule: the deferred ragged wgrad queue
+    launched in exact waves of `wave` tiles at layer ends (problems cut by
+    tile range across launches) must give bitwise the gradients of one launch
+    at the end of backward, and report every parameter ready exactly once."""
+    from tensorflow_distributed_on_gke_amd.models.layers import WgradQueue
+    cfg = model_config("tiny", d_model=512, heads=8, d_ff=2048, src_vocab=1000, tgt_vocab=1000,
+                       dropout=0.1)
+    m = Transformer(cfg).build("cuda", seed=21)
+    src, tgt = _batch(8, 64, 65, cfg.src_vocab, cfg.tgt_vocab, seed=3)
+    src, tgt = src.cuda(), tgt.cuda()
+    grads, ready = [], []
+    for wt in (0, wave):
+        seen = []
+        m.store.clear_grad_hooks()
+        m.store.on_grad_ready(lambda p: seen.append(p.index))
+        rt = RunCtx(training=True, dropout=0.1, seed=5,
+                    ctr=torch.tensor([4], dtype=torch.int64, device="cuda"), store=m.store)
+        rt.wgrad = WgradQueue(flush_at_boundary=True, wave_tiles=wt)
+        for p in m.store.params:  # (the flat buffer's alignment padding is never written)
+            p.grad.fill_(float("nan"))
+        m.loss_and_backward(src, tgt, rt, workers=1.0)
+        rt.wgrad.flush()
+        torch.cuda.synchronize()
+        assert not rt.wgrad.items and rt.wgrad._cursor == 0
+        grads.append(torch.cat([p.grad.reshape(-1) for p in m.store.params]))
+        ready.append(sorted(seen))
+    m.store.clear_grad_hooks()
+    assert torch.isfinite(grads[0]).all()
+    assert torch.equal(grads[0], grads[1])
+    assert ready[0] == ready[1] == sorted(set(ready[1])), "each parameter reported ready once"
+    assert ready[1] == [p.index for p in m.store.params], "every parameter reported ready"
