@@ -74,10 +74,21 @@ def cmd_test(args) -> int:
 
     settings = load_settings(args.config if os.path.exists(args.config) else None, args.set)
     dev = args.device if args.device != "auto" else ("cuda:0" if torch.cuda.is_available() else "cpu")
+    if settings.src_tokenizer and settings.tgt_tokenizer:
+        # the WordPiece pair a text-data training run saved (data/text.py); like
+        # the reference, the vocabulary sizes come from the tokenizers
+        from types import SimpleNamespace
+
+        from tensorflow_distributed_on_gke_amd.data.text import WordPieceTokenizer
+        pt = WordPieceTokenizer.load(settings.src_tokenizer)
+        en = WordPieceTokenizer.load(settings.tgt_tokenizer)
+        settings.src_vocab, settings.tgt_vocab = pt.vocab_size, en.vocab_size
+        tok = SimpleNamespace(pt=pt, en=en)
+    else:
+        tok = ByteTokenizer(min(settings.src_vocab, settings.tgt_vocab))
     model = build_model(settings, dev)
     if args.weights:
         bundle.load_weights(model.store, args.weights)
-    tok = ByteTokenizer(min(settings.src_vocab, settings.tgt_vocab))
     tester = Tester(tok, model)
     text, tokens, attn = tester(list(args.sentence), max_length=args.max_length)
     for s, t in zip(args.sentence, text):

@@ -51,8 +51,15 @@ class Settings:
     validation_steps: int = 20
     log_every: int = 50
     snapshot_every_epochs: int = 5
-    # --- data
+    # --- data: "synthetic" token pairs, or "text": TSV source<TAB>target files
+    # (data/text.py, the reference's TED pipeline on local files; an epoch is
+    # one pass over train_file, steps_per_epoch / validation_steps ignored)
     data: str = "synthetic"
+    train_file: Optional[str] = None
+    validation_file: Optional[str] = None
+    src_tokenizer: Optional[str] = None  # WordPiece JSON; None: trained on train_file
+    tgt_tokenizer: Optional[str] = None
+    shuffle_buffer: int = 20000
     src_len: int = 40
     tgt_len: int = 40
     min_len: int = 4

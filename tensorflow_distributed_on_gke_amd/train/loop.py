@@ -83,6 +83,18 @@ class Trainer:
             # divisor; the runtime world size wins
             self.log(f"note: settings.worker_count={s.worker_count} but world size is {info.world}; "
                      f"using {info.world}")
+        self.tokenizers = None
+        if s.data == "text":
+            # vocabulary sizes come from the tokenizers (reference __main__.py:32-35)
+            from tensorflow_distributed_on_gke_amd.data.text import build_tokenizers
+            if not s.train_file:
+                raise ValueError("data=text needs train_file")
+            self.tokenizers = build_tokenizers(s.train_file, s.src_vocab, s.tgt_vocab,
+                                               cache_dir=s.temporary_directory if info.chief else None,
+                                               src_path=s.src_tokenizer, tgt_path=s.tgt_tokenizer)
+            s.src_vocab, s.tgt_vocab = self.tokenizers[0].vocab_size, self.tokenizers[1].vocab_size
+        elif s.data != "synthetic":
+            raise ValueError(f"unknown data source {s.data!r} (synthetic | text)")
         self.model = build_model(s, info.device)
         self.opt = Adam(self.model.store, self.model.cfg.d_model, warmup=s.warmup_steps, beta1=s.beta1,
                         beta2=s.beta2, eps=s.epsilon, lr=s.learning_rate)
@@ -95,12 +107,25 @@ class Trainer:
             self.fp8 = Fp8State(self.model)
         self.step_fn = TrainStep(self.model, self.opt, self.ddp, workers=info.world, seed=s.seed + 17,
                                  fp8_state=self.fp8)
-        self.train_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab, s.tgt_vocab,
-                                         seed=s.seed, rank=info.rank, world=info.world, min_len=s.min_len,
-                                         copy_task=s.copy_task, pin=info.device.type == "cuda")
-        self.val_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab, s.tgt_vocab,
-                                       seed=s.seed + 1_000_003, rank=info.rank, world=info.world,
-                                       min_len=s.min_len, copy_task=s.copy_task)
+        if self.tokenizers is not None:
+            from tensorflow_distributed_on_gke_amd.data.text import TextPairs
+            st, tt = self.tokenizers
+            self.train_data = TextPairs(s.train_file, st, tt, s.local_batch_size, info.rank, info.world,
+                                        seed=s.seed, shuffle_buffer=s.shuffle_buffer, max_len=s.max_len,
+                                        pin=info.device.type == "cuda")
+            self.val_data = TextPairs(s.validation_file or s.train_file, st, tt, s.local_batch_size,
+                                      info.rank, info.world, seed=s.seed, shuffle=False,
+                                      max_len=s.max_len)
+            s.steps_per_epoch = self.train_data.steps_per_epoch  # one pass per epoch
+            s.validation_steps = self.val_data.steps_per_epoch
+        else:
+            self.train_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab,
+                                             s.tgt_vocab, seed=s.seed, rank=info.rank, world=info.world,
+                                             min_len=s.min_len, copy_task=s.copy_task,
+                                             pin=info.device.type == "cuda")
+            self.val_data = SyntheticPairs(s.local_batch_size, s.src_len, s.tgt_len + 1, s.src_vocab,
+                                           s.tgt_vocab, seed=s.seed + 1_000_003, rank=info.rank,
+                                           world=info.world, min_len=s.min_len, copy_task=s.copy_task)
         self.start_epoch = 0
         self.uploader: Optional[ModelUploader] = None
         self.global_step = 0
@@ -188,13 +213,14 @@ class Trainer:
         self.global_step = self.start_epoch * steps
         self.train_data.seek(self.global_step)
         captured = False
-        tok_per_step = s.local_batch_size * (s.src_len + s.tgt_len) * info.world
         for epoch in range(self.start_epoch, s.epochs):
             t0 = time.time()
             self.step_fn.accum.zero_()
+            epoch_tokens = 0
             for batch in range(steps):
                 src, tgt = self._to_dev(self.train_data.next())
-                if s.hip_graph and info.device.type == "cuda" and not captured:
+                epoch_tokens += (src.shape[1] + tgt.shape[1] - 1) * src.shape[0] * info.world
+                if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured:
                     self.step_fn.capture(src, tgt)
                     captured = True
                 self.timer.start()
@@ -234,7 +260,7 @@ class Trainer:
                 self.save_resume_state(epoch + 1)
             dt = time.time() - t0
             st = EpochStats(epoch + 1, train_loss, train_acc, val["loss"], val["acc"], dt,
-                            tok_per_step * steps / max(train_time, 1e-9))
+                            epoch_tokens / max(train_time, 1e-9))
             self.history.append(st)
             self.timer.drain()
             self.metrics.write(kind="epoch", **st.__dict__)
