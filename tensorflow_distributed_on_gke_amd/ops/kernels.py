@@ -171,6 +171,10 @@ def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc, beta=0.0):
         torch.mm(a, b, out_dtype=torch.float32, out=c)
 
 
+def _tok_bucket(v: int) -> int:
+    return -(-v // 1024) * 1024
+
+
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
          ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
     blas_ok = _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N)
@@ -187,7 +191,11 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None
                  beta, tile, splits, ws)
 
     if cfg is None:
-        key = (M, N, K, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0, beta != 0.0)
+        # token-count dimensions (M of forward / dgrad, K of wgrad) are bucketed
+        # to multiples of 1024 for the tuning key, so variable-length text
+        # batches reuse a handful of tunings instead of re-tuning every length
+        Mk, Kk = (M, _tok_bucket(K)) if (not a_kc and not b_kc) else (_tok_bucket(M), K)
+        key = (Mk, N, Kk, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0, beta != 0.0)
         ent = _TUNED.get(key)
         if ent is None:
             o = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
