@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--min-flops", type=float, default=2e9)
     ap.add_argument("--out", default="gpurun_out/tuned_inmodel.json")
+    ap.add_argument("--epi", type=lambda v: [int(x) for x in v.split(",")], default=None,
+                    help="only GEMMs with these epilogues (e.g. 1,2: bias, bias+relu)")
     args = ap.parse_args()
 
     dev = torch.device("cuda", 0)
@@ -54,11 +56,14 @@ def main():
     orig = kk.gemm
 
     def spy(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=kk.EPI_NONE, bias=None, aux=None,
-            ldaux=0, alpha=1.0, beta=0.0, cfg=None):
-        key = (M, N, K, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0, beta != 0.0)
-        if cfg is None:
-            seen.setdefault(key, [0, kk._blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N)])[0] += 1
-        return orig(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi, bias, aux, ldaux, alpha, beta, cfg)
+            ldaux=0, alpha=1.0, beta=0.0, cfg=None, bias_lp=None):
+        Mk, Kk = (M, kk._tok_bucket(K)) if (not a_kc and not b_kc) else (kk._tok_bucket(M), K)
+        key = (Mk, N, Kk, a_kc, b_kc, epi, Cout.dtype, ldc % 8 == 0, beta != 0.0)
+        if cfg is None and (not args.epi or epi in args.epi):
+            seen.setdefault(key, [0, kk._blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N,
+                                                 bias_lp)])[0] += 1
+        return orig(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi, bias, aux, ldaux, alpha, beta,
+                    cfg, bias_lp)
 
     kk.gemm = spy
     for _ in range(3):

@@ -300,7 +300,7 @@ def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int
             if r is not None:
                 y, h, mean, rstd = r
                 return y.view(x.shape), (h.view(x.shape), mean, rstd, None)
-    s = K.linear_fwd(a2, w.compute, b.master)
+    s = K.linear_fwd(a2, w.compute, b.master, bias_lp=b.compute)
     return _ln_fwd(x, s.view(x.shape), gamma, beta, site, rt)
 
 
@@ -438,7 +438,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ctx.meta = (heads, causal, scale, site, rt)
         x2 = x.reshape(B * L, d)
         if x.is_cuda:
-            qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
+            qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master, bias_lp=bqkv.compute)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
             o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
             s = None  # projection fused with the LayerNorm below
@@ -506,7 +506,7 @@ class CrossKVFn(torch.autograd.Function):
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
         ctx.save_for_backward(e2)
         if enc.is_cuda:
-            kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
+            kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master, bias_lp=bkv.compute)
         else:
             kv = e2 @ wkv.master.t() + bkv.master
         return kv.view(B, S, -1)
@@ -559,7 +559,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
         if kv5 is None:
             raise ValueError("kv_all must be contiguous")
         if x.is_cuda:
-            q = K.linear_fwd(x2, wq.compute, bq.master)
+            q = K.linear_fwd(x2, wq.compute, bq.master, bias_lp=bq.compute)
             o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
                                 False)
             s = None  # projection fused with the LayerNorm below
@@ -644,7 +644,7 @@ class FFNBlockFn(torch.autograd.Function):
             h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs)
             f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2)
         elif x.is_cuda:
-            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
+            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True, bias_lp=b1.compute)
             f = None  # second projection fused with the LayerNorm below
         else:
             h = torch.relu(x2 @ w1.master.t() + b1.master)

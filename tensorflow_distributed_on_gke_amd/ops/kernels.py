@@ -148,10 +148,16 @@ BLAS = (-1, 1)  # "config" meaning: plain library GEMM (hipBLASLt via torch)
 ALLOW_BLAS = True
 
 
-def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N) -> bool:
-    """Plain GEMMs only (no fused epilogue): dgrad (KC x MC, bf16 out) and
-    wgrad (MC x MC, f32 out) may go to hipBLASLt if it is faster."""
-    if not ALLOW_BLAS or epi != EPI_NONE or alpha != 1.0 or beta not in (0.0, 1.0) or ldc != N:
+def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N, bias_lp=None) -> bool:
+    """Library candidates (hipBLASLt through torch): plain dgrad (KC x MC, bf16
+    out) and wgrad (MC x MC, f32 out), and forward (KC x KC, bf16 out) with the
+    bias / bias+ReLU epilogue when the bias's bf16 copy is supplied."""
+    if not ALLOW_BLAS or alpha != 1.0 or beta not in (0.0, 1.0) or ldc != N:
+        return False
+    if epi in (EPI_BIAS, EPI_BIAS_RELU):
+        return (bias_lp is not None and a_kc and b_kc and beta == 0.0
+                and Cout.dtype == torch.bfloat16 and bias_lp.dtype == torch.bfloat16)
+    if epi != EPI_NONE:
         return False
     if beta == 1.0:  # C += A B (standard GEMM beta; residual-gradient accumulation)
         return a_kc and not b_kc and Cout.dtype == torch.bfloat16
@@ -159,10 +165,17 @@ def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N) -> bool:
         (not a_kc and not b_kc and Cout.dtype == torch.float32)
 
 
-def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc, beta=0.0):
+def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc, beta=0.0, epi=EPI_NONE, bias_lp=None):
     a = A.as_strided((M, K), (lda, 1)) if a_kc else A.as_strided((K, M), (lda, 1)).t()
-    b = B.as_strided((K, N), (ldb, 1))
     c = Cout.as_strided((M, N), (N, 1))
+    if epi in (EPI_BIAS, EPI_BIAS_RELU):  # forward: B is the [N, K] weight
+        wt = B.as_strided((N, K), (ldb, 1)).t()
+        if epi == EPI_BIAS_RELU:
+            torch._addmm_activation(bias_lp, a, wt, use_gelu=False, out=c)
+        else:
+            torch.addmm(bias_lp, a, wt, out=c)
+        return
+    b = B.as_strided((K, N), (ldb, 1))
     if beta == 1.0:
         c.addmm_(a, b)
     elif Cout.dtype == torch.bfloat16:
@@ -176,14 +189,15 @@ def _tok_bucket(v: int) -> int:
 
 
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
-         ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    blas_ok = _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N)
+         ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None,
+         bias_lp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    blas_ok = _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N, bias_lp)
 
     def run(c, out=Cout):
         if c == BLAS:
             if not blas_ok:
                 raise RuntimeError("library GEMM not applicable")
-            _blas(A, B, out, M, N, K, lda, ldb, a_kc, beta)
+            _blas(A, B, out, M, N, K, lda, ldb, a_kc, beta, epi, bias_lp)
             return
         tile, splits = c
         ws = workspace("splitk", splits * M * ldc, A.device) if splits > 1 else None
@@ -225,15 +239,18 @@ def tuned_table() -> Dict[str, str]:
 
 
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
-               out: Optional[torch.Tensor] = None, ldc: Optional[int] = None) -> torch.Tensor:
-    """y[M,N] = x[M,K] @ w[N,K]^T + bias (bf16 out)."""
+               out: Optional[torch.Tensor] = None, ldc: Optional[int] = None,
+               bias_lp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[M,N] = x[M,K] @ w[N,K]^T + bias (bf16 out). bias_lp: the bias's bf16
+    compute copy -- lets the tuner also try hipBLASLt's bias(+ReLU) epilogue."""
     M, K = x2.shape
     N = w.shape[0]
     ldc = ldc or N
     if out is None:
         out = torch.empty(M, ldc, dtype=torch.bfloat16, device=x2.device)
     epi = EPI_BIAS_RELU if relu else (EPI_BIAS if bias is not None else EPI_NONE)
-    return gemm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), ldc, True, True, epi, bias=bias)
+    return gemm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), ldc, True, True, epi, bias=bias,
+                bias_lp=bias_lp)
 
 
 def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor, N: int, relu_aux: Optional[torch.Tensor] = None,

@@ -458,3 +458,24 @@ def test_gemm_ln_matches_unfused(M, K):
     _close(y, yf, 3e-2, "gemm_ln vs fp32")
     frac = keep.float().mean().item()
     assert 0.85 < frac < 0.95, f"dropout keep fraction {frac}"
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_linear_fwd_library_bias_epilogue(relu):
+    """The hipBLASLt bias(+ReLU) candidate (bf16 bias copy) agrees with the
+    in-tree epilogue GEMM to bf16 rounding."""
+    M, N, K = 1000, 768, 512
+    x = _bf(_rand(M, K, seed=71)).to(DEV)
+    w = _bf(_rand(N, K, scale=1.0 / math.sqrt(K), seed=72)).to(DEV)
+    b = _rand(N, scale=0.5, seed=73).to(DEV)
+    out_lib = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out_own = torch.empty_like(out_lib)
+    epi = kk.EPI_BIAS_RELU if relu else kk.EPI_BIAS
+    kk.gemm(x, w, out_lib, M, N, K, K, K, N, True, True, epi, bias=b, cfg=kk.BLAS,
+            bias_lp=b.to(torch.bfloat16))
+    kk.gemm(x, w, out_own, M, N, K, K, K, N, True, True, epi, bias=b, cfg=(0, 1))
+    ref = x.float() @ w.float().t() + b
+    if relu:
+        ref = torch.relu(ref)
+    _close(out_lib, ref, 1e-2, "hipBLASLt bias epilogue")
+    _close(out_own, ref, 1e-2, "in-tree bias epilogue")
