@@ -37,8 +37,9 @@ def init_distributed(device: str = "auto", timeout_s: float = 900.0, force: bool
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_cuda = torch.cuda.is_available() if device == "auto" else device.startswith("cuda")
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # (more ranks than GPUs only for rehearsals with TDG_DIST_BACKEND=gloo)
+        dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
     if (world > 1 or force) and not dist.is_initialized():
@@ -47,9 +48,12 @@ def init_distributed(device: str = "auto", timeout_s: float = 900.0, force: bool
         # RCCL async error handling: a dead peer aborts collectives instead of
         # hanging (failure detection; the reference relied on MWMS defaults).
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-        kw = dict(backend="nccl" if use_cuda else "gloo", init_method="env://", rank=rank,
+        # TDG_DIST_BACKEND=gloo: a multi-rank rehearsal of the GPU data-parallel
+        # path on ONE GPU (RCCL needs a device per rank); production is RCCL
+        backend = os.environ.get("TDG_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+        kw = dict(backend=backend, init_method="env://", rank=rank,
                   world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda:
+        if use_cuda and backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
     return DistInfo(rank, world, local_rank, dev)

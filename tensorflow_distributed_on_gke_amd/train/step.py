@@ -27,6 +27,9 @@ from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 # data parallel: weight gradients flushed in wave-sized chunks at layer ends
 CHUNKED_WGRAD = os.environ.get("TDG_DP_CHUNKED_WGRAD", "1") != "0"
+# tiles per wave of the chunked schedule (one whole-K 256x256 tile per CU);
+# overridable so tests can force problems to be cut across launches
+WAVE_TILES = int(os.environ.get("TDG_DP_WAVE_TILES", "0"))
 # skip the optimizer's gradient zeroing (all GPU gradient writers overwrite)
 ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 
@@ -52,7 +55,7 @@ class TrainStep:
         if defer_wgrad and dev.type == "cuda":
             dp = ddp is not None and ddp.active
             self.rt.wgrad = WgradQueue(flush_at_boundary=dp,
-                                       wave_tiles=K.NUM_CU if dp and CHUNKED_WGRAD else 0)
+                                       wave_tiles=(WAVE_TILES or K.NUM_CU) if dp and CHUNKED_WGRAD else 0)
         self.fp8 = fp8_state
         if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
             opt.zero_grad = False  # every GPU gradient writer overwrites
