@@ -113,6 +113,101 @@ __global__ __launch_bounds__(256) void xent_kernel(bf16_t* __restrict__ logits, 
   }
 }
 
+// Register-resident variant for padded rows of <= 256 * 8 * NCH columns
+// (ldl % 8 == 0): every thread loads its NCH 16-byte chunks once, so max /
+// argmax / sum-exp / dlogits are computed from registers (no second pass over
+// the row, no per-element online-softmax dependency chain); two block
+// reductions (max+argmax+sum, then sum-exp). Same results as xent_kernel up to
+// the order of the f32 sums (deterministic).
+template <typename LabT, int NCH>
+__global__ __launch_bounds__(256) void xent_reg_kernel(bf16_t* __restrict__ logits, int V, int ldl,
+                                                       const LabT* __restrict__ labels,
+                                                       const float* __restrict__ ntok,
+                                                       float workers, float smoothing,
+                                                       float* __restrict__ row_loss,
+                                                       float* __restrict__ row_correct,
+                                                       int write_grad) {
+  __shared__ float r_m[4], r_x[4], r_s[4];
+  __shared__ int r_i[4];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16_t* x = logits + (size_t)row * ldl;
+  const int lab = (int)labels[row];
+  const int nch = ldl >> 3;
+  short8_t raw[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = tid + 256 * k;
+    if (ch < nch) raw[k] = *reinterpret_cast<const short8_t*>(x + 8 * ch);
+  }
+  const float xl = bf2f(x[lab]);  // read before any thread overwrites the row
+  float m = -INFINITY, sumx = 0.f;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c0 = 8 * (tid + 256 * k);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (c0 + e < V) {
+        const float v = bf2f((bf16_t)raw[k][e]);
+        sumx += v;
+        if (v > m) { m = v; bi = c0 + e; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (m2 > m || (m2 == m && i2 < bi)) { m = m2; bi = i2; }
+    sumx += __shfl_xor(sumx, o, 64);
+  }
+  if (lane == 0) { r_m[w] = m; r_i[w] = bi; r_x[w] = sumx; }
+  __syncthreads();
+  m = r_m[0]; bi = r_i[0]; sumx = r_x[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    if (r_m[k] > m || (r_m[k] == m && r_i[k] < bi)) { m = r_m[k]; bi = r_i[k]; }
+    sumx += r_x[k];
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c0 = 8 * (tid + 256 * k);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (c0 + e < V) se += __expf(bf2f((bf16_t)raw[k][e]) - m);
+  }
+  se = wave_sum(se);
+  if (lane == 0) r_s[w] = se;
+  __syncthreads();
+  const float lse = m + __logf(r_s[0] + r_s[1] + r_s[2] + r_s[3]);
+  const bool valid = lab != 0;
+  if (tid == 0) {
+    row_loss[row] = valid ? (1.f - smoothing) * (lse - xl) + smoothing * (lse - sumx / (float)V) : 0.f;
+    row_correct[row] = (valid && bi == lab) ? 1.f : 0.f;
+  }
+  if (!write_grad) return;
+  const float scale = valid ? 1.f / (fmaxf(ntok[0], 1.f) * workers) : 0.f;
+  const float off = smoothing / (float)V;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = tid + 256 * k;
+    if (ch >= nch) continue;
+    const int c0 = 8 * ch;
+    short8_t g;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      float gv = 0.f;
+      if (c < V && valid)
+        gv = (__expf(bf2f((bf16_t)raw[k][e]) - lse) - off - (c == lab ? 1.f - smoothing : 0.f)) * scale;
+      g[e] = (short)f2bf(gv);
+    }
+    *reinterpret_cast<short8_t*>(x + c0) = g;
+  }
+}
+
 // ntok = number of non-pad labels
 template <typename LabT>
 __global__ void count_tokens_kernel(const LabT* __restrict__ labels, int M, float* __restrict__ out) {
@@ -243,6 +338,25 @@ extern "C" int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, i
 extern "C" int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64,
                         const float* ntok, float workers, float smoothing, float* row_loss,
                         float* row_correct, int write_grad, hipStream_t st) {
+  const bool aligned = (ldl % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
+  if (aligned && ldl <= 256 * 8 * 4) {
+#define TDG_XR(NCH)                                                                              \
+  if (lab64)                                                                                    \
+    hipLaunchKernelGGL((xent_reg_kernel<long long, NCH>), dim3(M), dim3(256), 0, st,           \
+                       (bf16_t*)logits, V, ldl, (const long long*)labels, ntok, workers,        \
+                       smoothing, row_loss, row_correct, write_grad);                           \
+  else                                                                                          \
+    hipLaunchKernelGGL((xent_reg_kernel<int, NCH>), dim3(M), dim3(256), 0, st, (bf16_t*)logits, \
+                       V, ldl, (const int*)labels, ntok, workers, smoothing, row_loss,          \
+                       row_correct, write_grad);                                                \
+  return 0;
+    const int nch = cdiv(ldl / 8, 256);
+    if (nch <= 1) { TDG_XR(1) }
+    if (nch == 2) { TDG_XR(2) }
+    if (nch == 3) { TDG_XR(3) }
+    TDG_XR(4)
+#undef TDG_XR
+  }
   if (lab64)
     hipLaunchKernelGGL(xent_kernel<long long>, dim3(M), dim3(256), 0, st, (bf16_t*)logits, V, ldl,
                        (const long long*)labels, ntok, workers, smoothing, row_loss, row_correct,
