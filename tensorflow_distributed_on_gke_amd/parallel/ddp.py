@@ -93,25 +93,29 @@ class DataParallel:
         self._upd_stream = None
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
+        self._stream_ordered = (self.active and store.flat.is_cuda
+                                and dist.get_backend(group) == "nccl")
         if self.active:
             store.on_grad_ready(self._on_ready)
             store.on_grad_sync(self._on_sync)
         self.reset()
 
-    def attach_optimizer(self, opt) -> None:
-        """Overlap the optimizer with backward: a bucket is updated (Adam over
-        its flat range) as soon as its all-reduce is done AND the model has
-        passed a release point (ParamStore.release_point: no later backward
-        kernel reads those weights) -- for the Transformer, the decoder side
-        is updated while the encoder's backward runs. finish() updates the
-        rest and advances the step. The optimizer must offer
-        apply_range(start, end, inc_step) / advance_step()."""
+    def attach_optimizer(self, opt, release: bool = True) -> None:
+        """Run the optimizer per bucket (Adam over its flat range) instead of
+        once after every all-reduce. finish() updates each bucket as soon as
+        ITS all-reduce is done, so the Adam of the early buckets overlaps the
+        all-reduce of the last one (the exposed tail). release=True also
+        updates buckets mid-backward, once the model passed a release point
+        (ParamStore.release_point: no later backward kernel reads those
+        weights) -- the decoder side during the encoder's backward. The
+        optimizer must offer apply_range(start, end, inc_step) / advance_step()."""
         if not self.active:
             return
         self.opt = opt
-        if self.store.flat.is_cuda:
-            self._upd_stream = torch.cuda.Stream(self.store.flat.device)
-        self.store.on_release(self._on_release)
+        if release:
+            if self.store.flat.is_cuda:
+                self._upd_stream = torch.cuda.Stream(self.store.flat.device)
+            self.store.on_release(self._on_release)
 
     # ------------------------------------------------------------------ init
     def broadcast_params(self, src: int = 0) -> None:
@@ -213,11 +217,18 @@ class DataParallel:
         self._launch_span(self.store.total)
         if self._upd_stream is not None:
             torch.cuda.current_stream(self._upd_stream.device).wait_stream(self._upd_stream)
-        for b in self.buckets:
-            if not b.updated:
-                self._complete(b)
-                if self.opt is not None:
-                    self.opt.apply_range(b.start, b.end, inc_step=False)
+        # RCCL: Work.wait() orders the current stream after the collective, so
+        # each bucket's Adam is queued right behind ITS wait and runs while the
+        # later buckets' all-reduces are still in flight.
+        interleave = self.opt is not None and self._stream_ordered
+        todo = [b for b in self.buckets if not b.updated]
+        for b in todo:
+            self._complete(b)
+            if interleave:
+                self.opt.apply_range(b.start, b.end, inc_step=False)
+        if self.opt is not None and not interleave:
+            for b in todo:
+                self.opt.apply_range(b.start, b.end, inc_step=False)
         if self.opt is not None:
             self.opt.advance_step()
         self.reset()

@@ -37,10 +37,10 @@ def _batch(rank, i):
     return src, tgt
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, opt_mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
-                      TDG_DP_WAVE_TILES="37")
+                      TDG_DP_WAVE_TILES="37", TDG_DP_OVERLAP_OPT=opt_mode)
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
@@ -66,14 +66,15 @@ def _worker(rank, world, port, out):
     tdist.shutdown()
 
 
-def test_gpu_dp2_rehearsal_matches_single_process(tmp_path):
+@pytest.mark.parametrize("opt_mode", ["0", "tail"])  # ("tail" falls back to "0" over gloo)
+def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode):
     from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
     world = 2
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _port(), out), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _port(), out, opt_mode), nprocs=world, join=True,
                        start_method="spawn")
     r0 = torch.load(out + ".0", weights_only=True)
     r1 = torch.load(out + ".1", weights_only=True)
@@ -97,5 +98,6 @@ def test_gpu_dp2_rehearsal_matches_single_process(tmp_path):
     moved = (ref - init.cpu()).norm()
     assert moved > 0
     rel = (r0["flat"] - ref).norm() / moved
+    print(f"opt_mode={opt_mode}: rel {rel:.3e}")
     assert rel < 1e-3, f"DP update differs from the single-process update: rel {rel:.3e}"
     assert torch.allclose(r0["loss"], torch.stack(losses), rtol=1e-3, atol=1e-4)
