@@ -80,6 +80,8 @@ class Settings:
     idle_after_train: bool = False  # reference __main__.py:183-186 keeps the pod alive
     check_replicas_every: int = 0  # debug: assert bitwise-identical replicas every N steps
     metrics_file: Optional[str] = None  # JSONL metrics sink (rank 0)
+    profile_dir: Optional[str] = None  # torch.profiler (roctracer) Chrome trace of the first steps
+    profile_steps: int = 5  # active profiled steps (after 1 wait + 1 warm-up step)
     kill_at_step: int = -1  # fault injection (tests): global step at which to exit
     kill_rank: int = -1  # rank that exits (-1: the last rank)
     loss_mode: str = "replica_mean"  # reference per-replica token mean / workers

@@ -43,7 +43,7 @@ from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep
-from tensorflow_distributed_on_gke_amd.utils.profiling import MetricsWriter, StepTimer, summarize
+from tensorflow_distributed_on_gke_amd.utils.profiling import MetricsWriter, StepTimer, summarize, torch_profile
 
 RESUME_DIR = "resume"
 RESUME_PREFIX = "model_weights"
@@ -213,6 +213,10 @@ class Trainer:
         self.global_step = self.start_epoch * steps
         self.train_data.seek(self.global_step)
         captured = False
+        # optional Chrome trace of the first profile_steps + 2 steps (rank 0)
+        prof_cm = torch_profile(s.profile_dir if info.chief else None, active=s.profile_steps)
+        prof = prof_cm.__enter__()
+        prof_left = s.profile_steps + 2 if s.profile_dir and info.chief else 0
         for epoch in range(self.start_epoch, s.epochs):
             t0 = time.time()
             self.step_fn.accum.zero_()
@@ -227,6 +231,11 @@ class Trainer:
                 self.step_fn(src, tgt)
                 self.timer.stop()
                 self.global_step += 1
+                if prof_left:
+                    prof.step()
+                    prof_left -= 1
+                    if not prof_left:
+                        prof_cm.__exit__(None, None, None)
                 if self.ddp is not None and s.check_replicas_every > 0 and \
                         self.global_step % s.check_replicas_every == 0:
                     self.ddp.verify_replicas()
@@ -270,6 +279,8 @@ class Trainer:
                 self.log(f"Time taken for 1 epoch: {dt:.2f} secs ({st.tokens_per_s:,.0f} tokens/s)\n")
             if info.world > 1:
                 dist.barrier()
+        if prof_left:  # fewer steps than the profile window
+            prof_cm.__exit__(None, None, None)
         return self.history
 
 

@@ -31,3 +31,21 @@ def test_unknown_keys(tmp_path):
         load_settings(str(p))
     with pytest.raises(ValueError):
         load_settings(None, ["epochs"])
+
+
+def test_profiler_trace_written(tmp_path, monkeypatch):
+    """profile_dir: a torch.profiler Chrome trace of the first steps (CPU here,
+    roctracer HIP kernels on the GPU)."""
+    from tensorflow_distributed_on_gke_amd.config import Settings
+    from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
+    from tensorflow_distributed_on_gke_amd.train.loop import Trainer
+    import torch
+
+    monkeypatch.chdir(tmp_path)
+    s = Settings(preset="tiny", local_batch_size=4, src_len=8, tgt_len=8, src_vocab=40, tgt_vocab=40,
+                 epochs=1, steps_per_epoch=6, validation_steps=1, log_every=100,
+                 snapshot_every_epochs=0, resume=False, profile_dir=str(tmp_path / "trace"),
+                 profile_steps=2)
+    Trainer(s, DistInfo(0, 1, 0, torch.device("cpu")), log=lambda m: None).fit()
+    traces = list((tmp_path / "trace").glob("*.json"))
+    assert traces and traces[0].stat().st_size > 0
