@@ -22,7 +22,8 @@ def graph_time(fn, n=20):
     a.record(); g.replay(); b.record(); torch.cuda.synchronize()
     return a.elapsed_time(b) / n * 1e3
 
-B, H, L, hd = 64, 8, 128, 64
+B = int(os.environ.get("ATTN_B", "64"))
+H, L, hd = 8, 128, 64
 for causal in (False, True):
     q, k, v, do = (torch.randn(B, L, H, hd, device="cuda").bfloat16() for _ in range(4))
     kv = torch.full((B,), L, dtype=torch.int32, device="cuda")
@@ -30,4 +31,4 @@ for causal in (False, True):
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     tf = graph_time(lambda: kk.attn_fwd(q, k, v, kv, 0.125, causal))
     tb = graph_time(lambda: kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, causal))
-    print(f"causal={causal} split={os.environ.get('TDG_ATTN_BWD_SPLIT', '0')}: fwd {tf:.2f} us  bwd {tb:.2f} us", flush=True)
+    print(f"B={B} causal={causal} split={os.environ.get('TDG_ATTN_BWD_SPLIT', '0')}: fwd {tf:.2f} us  bwd {tb:.2f} us", flush=True)
