@@ -76,6 +76,8 @@ int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, 
              float grad_scale, float weight_decay, int sched, int zero_grad, int inc_step,
              hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
+int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
+                          hipStream_t st);
 }
 
 namespace {
@@ -823,6 +825,32 @@ void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
             "tdg adam");
 }
 
+// dsts[g] [C, R] = srcs[g] [R, C]^T (bf16, same shape, <= 64 matrices, one launch)
+void transpose_grouped(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
+  const size_t G = srcs.size();
+  TORCH_CHECK(G >= 1 && G <= 64 && dsts.size() == G, "transpose_grouped: 1..64 matrices");
+  const int64_t R = srcs[0].size(0), C = srcs[0].size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0, "transpose_grouped: rows and columns multiples of 8");
+  std::vector<const void*> s(G);
+  std::vector<void*> d(G);
+  for (size_t i = 0; i < G; ++i) {
+    check_bf16(srcs[i], "src");
+    check_bf16(dsts[i], "dst");
+    TORCH_CHECK(srcs[i].dim() == 2 && srcs[i].size(0) == R && srcs[i].size(1) == C &&
+                    srcs[i].is_contiguous(), "transpose_grouped: same-shape contiguous sources");
+    TORCH_CHECK(dsts[i].dim() == 2 && dsts[i].size(0) == C && dsts[i].size(1) == R &&
+                    dsts[i].is_contiguous(), "transpose_grouped: dst must be [C, R]");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(srcs[i].data_ptr()) % 16) == 0 &&
+                    (reinterpret_cast<uintptr_t>(dsts[i].data_ptr()) % 16) == 0,
+                "transpose_grouped: 16-byte aligned");
+    s[i] = srcs[i].data_ptr();
+    d[i] = dsts[i].data_ptr();
+  }
+  c10::DeviceGuard g(srcs[0].device());
+  check_err(tdg_transpose_grouped(s.data(), d.data(), (int)G, (int)R, (int)C, stream_of(srcs[0])),
+            "tdg transpose_grouped");
+}
+
 void to_bf16(const Tensor& p, const Tensor& o) {
   check_f32(p, "p");
   check_bf16(o, "o");
@@ -858,6 +886,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd_det", &embed_bwd_det);
   m.def("count_tokens", &count_tokens);
   m.def("prep_batch", &prep_batch);
+  m.def("transpose_grouped", &transpose_grouped);
   m.def("xent", &xent);
   m.def("xent_stats", &xent_stats);
   m.def("adam", &adam);

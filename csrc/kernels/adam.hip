@@ -83,9 +83,70 @@ __global__ void to_bf16_kernel(const float* __restrict__ p, bf16_t* __restrict__
     o[i] = f2bf(p[i]);
 }
 
+// Grouped bf16 transpose: dst[g] [C, R] = src[g] [R, C]^T, G same-shape
+// matrices in one launch (the K-contiguous weight copies the relu-backward
+// dgrads read; refreshed after every optimizer update). 64x64 tiles through
+// LDS (padded rows: conflict-free column reads), 16-byte global accesses.
+constexpr int TR_MAXG = 64;
+struct TransposeGroup {
+  const bf16_t* src[TR_MAXG];
+  bf16_t* dst[TR_MAXG];
+};
+
+__global__ __launch_bounds__(256) void transpose_grouped_kernel(TransposeGroup grp, int R, int C) {
+  __shared__ bf16_t tile[64][64 + 8];
+  const bf16_t* __restrict__ src = grp.src[blockIdx.y];
+  bf16_t* __restrict__ dst = grp.dst[blockIdx.y];
+  const int tiles_c = (C + 63) / 64;
+  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+  const int tid = threadIdx.x;
+  // load 64 rows x 64 cols: each thread 2 x 8 elements
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k;
+    const int r = id >> 3, c = (id & 7) * 8;
+    short8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + r < R && c0 + c + 8 <= C)
+      v = *reinterpret_cast<const short8_t*>(src + (size_t)(r0 + r) * C + c0 + c);
+    else
+      for (int e = 0; e < 8; ++e)
+        if (r0 + r < R && c0 + c + e < C) v[e] = (short)src[(size_t)(r0 + r) * C + c0 + c + e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[r][c + e] = (bf16_t)v[e];
+  }
+  __syncthreads();
+  // store 64 (former) columns x 64 (former) rows
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k;
+    const int c = id >> 3, r = (id & 7) * 8;
+    short8_t v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)tile[r + e][c];
+    if (c0 + c < C && r0 + r + 8 <= R)
+      *reinterpret_cast<short8_t*>(dst + (size_t)(c0 + c) * R + r0 + r) = v;
+    else
+      for (int e = 0; e < 8; ++e)
+        if (c0 + c < C && r0 + r + e < R) dst[(size_t)(c0 + c) * R + r0 + r + e] = (bf16_t)v[e];
+  }
+}
+
 }  // namespace tdg
 
 using namespace tdg;
+
+extern "C" int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
+                                     hipStream_t st) {
+  if (G < 1 || G > TR_MAXG || R < 1 || C < 1) return -1;
+  TransposeGroup g{};
+  for (int i = 0; i < G; ++i) {
+    g.src[i] = (const bf16_t*)src[i];
+    g.dst[i] = (bf16_t*)dst[i];
+  }
+  const int tiles = ((R + 63) / 64) * ((C + 63) / 64);
+  hipLaunchKernelGGL(transpose_grouped_kernel, dim3(tiles, G), dim3(256), 0, st, g, R, C);
+  return 0;
+}
 
 extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n,
                         long long* step, float beta1, float beta2, float eps, float lr_const,

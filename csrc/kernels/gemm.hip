@@ -826,11 +826,12 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
 }
 
 // Which (layout, epilogue) combinations have a 256x256 instantiation:
-// forward NT (plain / bias / bias+relu), dgrad NN (plain / relu-backward),
-// wgrad TN (f32 or bf16 out).
+// forward NT (plain / bias / bias+relu; relu-backward for dgrads against a
+// transposed weight copy), dgrad NN (plain / relu-backward), wgrad TN (f32 or
+// bf16 out).
 template <bool AK, bool BKc, int EPI, bool F32>
 constexpr bool has_256() {
-  if (AK && BKc) return EPI != EPI_DRELU;
+  if (AK && BKc) return !F32 || EPI == EPI_NONE;
   if (AK && !BKc) return !F32 && (EPI == EPI_NONE || EPI == EPI_DRELU);
   if (!AK && !BKc) return EPI == EPI_NONE;
   return false;

@@ -668,7 +668,10 @@ class FFNBlockFn(torch.autograd.Function):
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
             _wgrad(rt, ds2, h, d, w2)
-            dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
+            if w2.compute_t is not None:  # NT layout against W2^T (ParamStore.add_transposed)
+                dpre = K.linear_dgrad_t(ds2, w2.compute_t, relu_aux=h)
+            else:
+                dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
             _wgrad(rt, dpre, x2, ff, w1, b1)
             dx = _dgrad_into(dpre, w1, ff, dh)
             return (dx.view(B, L, d),) + (None,) * 8

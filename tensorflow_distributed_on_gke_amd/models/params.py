@@ -54,6 +54,7 @@ class Param:
     master: Optional[torch.Tensor] = None
     grad: Optional[torch.Tensor] = None
     compute: Optional[torch.Tensor] = None  # bf16 shadow (GPU) / master (CPU)
+    compute_t: Optional[torch.Tensor] = None  # transposed bf16 copy (ParamStore.add_transposed)
 
     def __repr__(self) -> str:  # pragma: no cover
         return f"Param({self.name}, {self.shape}, off={self.offset})"
@@ -107,6 +108,7 @@ class ParamStore:
         self._ready_hooks: List[Callable[[Param], None]] = []
         self._release_hooks: List[Callable[[], None]] = []
         self._sync_hooks: List[Callable[[], None]] = []
+        self.transposed: List[Param] = []  # weights with a transposed compute copy
         # autograd anchor: gives layers whose only inputs are token ids a
         # tensor that requires grad, so backward reaches them.
         self.anchor = torch.zeros((), requires_grad=True)
@@ -157,6 +159,34 @@ class ParamStore:
         from tensorflow_distributed_on_gke_amd.ops import _ext
 
         _ext.C().to_bf16(self.flat, self.flat_compute)
+        self.refresh_transposed()
+
+    # ------------------------------------------------------------------ transposed copies
+    def add_transposed(self, p: Param) -> None:
+        """Keep a transposed bf16 copy p.compute_t [in, out] of a 2-D weight
+        (GPU): kernels that read the weight K-contiguous the other way round
+        (the relu-backward dgrad of the FFN output projection) use it. Every
+        writer of the compute copy refreshes it (refresh_compute, the optimizer)."""
+        if self.flat_compute is None or p.compute_t is not None:
+            return
+        p.compute_t = torch.empty(p.shape[1], p.shape[0], dtype=self.compute_dtype,
+                                  device=self.device)
+        self.transposed.append(p)
+        self.refresh_transposed()
+
+    def refresh_transposed(self, start: int = 0, end: Optional[int] = None) -> None:
+        """Re-transpose the registered weights lying in flat[start:end]."""
+        if not self.transposed:
+            return
+        end = self.total if end is None else end
+        todo = [p for p in self.transposed if p.offset >= start and p.offset + p.numel <= end]
+        groups: Dict[tuple, List[Param]] = {}
+        for p in todo:
+            groups.setdefault(tuple(p.shape), []).append(p)
+        from tensorflow_distributed_on_gke_amd.ops import kernels as K
+
+        for ps in groups.values():
+            K.transpose_grouped([p.compute for p in ps], [p.compute_t for p in ps])
 
     # ------------------------------------------------------------------ grads
     def on_grad_ready(self, fn: Callable[[Param], None]) -> None:

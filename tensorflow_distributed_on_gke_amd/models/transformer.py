@@ -15,6 +15,7 @@ kernels.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -159,6 +160,9 @@ class DecoderLayer:
                                 self.ln3.beta, self.site3, rt)
 
 
+TRANSPOSED_FFN_DGRAD = os.environ.get("TDG_FFN_DGRAD_T", "1") != "0"
+
+
 def seq_lengths(tok: torch.Tensor) -> torch.Tensor:
     """Valid (non-PAD) length per row for right-padded batches -> int32 [B]
     (the reference's padding mask `tok == 0`, transformer_model.py:56-62)."""
@@ -201,6 +205,11 @@ class Transformer:
     def build(self, device="cpu", seed: int = 0, compute_dtype=torch.bfloat16) -> "Transformer":
         self.device = torch.device(device)
         self.store.finalize(self.device, compute_dtype, seed)
+        if self.device.type == "cuda" and TRANSPOSED_FFN_DGRAD:
+            # the FFN's relu-backward dgrad reads W2 K-contiguous the other way
+            # round: keep W2^T so it runs with the forward-layout (NT) kernels
+            for layer in self.enc_layers + self.dec_layers:
+                self.store.add_transposed(layer.ff2.w)
         self.pe_src = positional_encoding(self.cfg.max_src_len, self.cfg.d_model).to(self.device)
         self.pe_tgt = positional_encoding(self.cfg.max_tgt_len, self.cfg.d_model).to(self.device)
         return self

@@ -265,6 +265,26 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor, N: int, relu_aux: Optional[
                 aux=relu_aux, ldaux=(relu_aux.stride(0) if relu_aux is not None else 0), beta=beta)
 
 
+def transpose_grouped(srcs, dsts) -> None:
+    """dsts[g] = srcs[g].T for same-shape bf16 matrices, one launch per 64."""
+    for c0 in range(0, len(srcs), 64):
+        C().transpose_grouped(list(srcs[c0:c0 + 64]), list(dsts[c0:c0 + 64]))
+
+
+def linear_dgrad_t(dy2: torch.Tensor, w_t: torch.Tensor, relu_aux: Optional[torch.Tensor] = None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx[M,N] = dy[M,K] @ w[K,N] computed against the weight's transposed copy
+    w_t [N, K] (K-contiguous): the forward (NT) operand layout, whose kernels
+    are faster than the N-contiguous dgrad ones; optional ReLU-backward mask."""
+    M, K = dy2.shape
+    N = w_t.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dy2.device)
+    epi = EPI_DRELU if relu_aux is not None else EPI_NONE
+    return gemm(dy2, w_t, out, M, N, K, dy2.stride(0), w_t.stride(0), out.stride(0), True, True, epi,
+                aux=relu_aux, ldaux=(relu_aux.stride(0) if relu_aux is not None else 0))
+
+
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, N: int, dw: torch.Tensor,
                  beta: float = 0.0) -> torch.Tensor:
     """dw[N,K] (f32) (+)= dy[M,N]^T @ x[M,K]."""

@@ -64,6 +64,7 @@ class Adam:
                    self.beta1, self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model),
                    float(self.warmup), grad_scale, self.weight_decay,
                    0 if self.lr_const is not None else 1, self.zero_grad, inc_step)
+            s.refresh_transposed(start, end)  # transposed compute copies of updated weights
             return
         step = int(self.step.item())
         lr = self.lr_at(step)

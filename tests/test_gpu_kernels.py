@@ -479,3 +479,26 @@ def test_linear_fwd_library_bias_epilogue(relu):
         ref = torch.relu(ref)
     _close(out_lib, ref, 1e-2, "hipBLASLt bias epilogue")
     _close(out_own, ref, 1e-2, "in-tree bias epilogue")
+
+
+def test_transpose_grouped_and_dgrad_t():
+    """Grouped bf16 transpose (exact), and the relu-backward dgrad against the
+    transposed weight copy equals the N-contiguous dgrad kernel's result to
+    rounding (same math, different operand layout)."""
+    ws = [_bf(_rand(512, 2048, scale=0.05, seed=80 + i)).to(DEV) for i in range(3)]
+    wts = [torch.empty(2048, 512, dtype=torch.bfloat16, device=DEV) for _ in ws]
+    kk.transpose_grouped(ws, wts)
+    for w, wt in zip(ws, wts):
+        assert torch.equal(wt, w.t())
+    odd = _bf(_rand(136, 200, seed=90)).to(DEV)  # edge tiles
+    odd_t = torch.empty(200, 136, dtype=torch.bfloat16, device=DEV)
+    kk.transpose_grouped([odd], [odd_t])
+    assert torch.equal(odd_t, odd.t())
+    M = 1000
+    dy = _bf(_rand(M, 512, seed=91)).to(DEV)
+    h = _bf(_rand(M, 2048, seed=92)).to(DEV)
+    a = kk.linear_dgrad_t(dy, wts[0], relu_aux=h)
+    b = kk.linear_dgrad(dy, ws[0], 512, relu_aux=h)
+    ref = (dy.float() @ ws[0].float()) * (h.float() > 0)
+    _close(a, ref, 1e-2, "dgrad_t relu")
+    _close(b, ref, 1e-2, "dgrad relu")
