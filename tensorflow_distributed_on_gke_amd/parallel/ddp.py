@@ -93,8 +93,6 @@ class DataParallel:
         self._upd_stream = None
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
-        self._stream_ordered = (self.active and store.flat.is_cuda
-                                and dist.get_backend(group) == "nccl")
         if self.active:
             store.on_grad_ready(self._on_ready)
             store.on_grad_sync(self._on_sync)
@@ -217,18 +215,14 @@ class DataParallel:
         self._launch_span(self.store.total)
         if self._upd_stream is not None:
             torch.cuda.current_stream(self._upd_stream.device).wait_stream(self._upd_stream)
-        # RCCL: Work.wait() orders the current stream after the collective, so
-        # each bucket's Adam is queued right behind ITS wait and runs while the
+        # Work.wait() orders the current stream after the collective, so each
+        # bucket's Adam is queued right behind ITS wait and runs while the
         # later buckets' all-reduces are still in flight.
-        interleave = self.opt is not None and self._stream_ordered
-        todo = [b for b in self.buckets if not b.updated]
-        for b in todo:
-            self._complete(b)
-            if interleave:
-                self.opt.apply_range(b.start, b.end, inc_step=False)
-        if self.opt is not None and not interleave:
-            for b in todo:
-                self.opt.apply_range(b.start, b.end, inc_step=False)
+        for b in self.buckets:
+            if not b.updated:
+                self._complete(b)
+                if self.opt is not None:
+                    self.opt.apply_range(b.start, b.end, inc_step=False)
         if self.opt is not None:
             self.opt.advance_step()
         self.reset()

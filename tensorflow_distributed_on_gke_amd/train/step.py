@@ -65,13 +65,7 @@ class TrainStep:
         # (decoder side during the encoder's backward) -- on one MI355X with
         # --force-dp that concurrent Adam contended with the encoder backward
         # for more than it hid (6.45 vs 6.34 ms). "0": one Adam after finish.
-        # "tail" needs the collective's wait to order the device stream (RCCL);
-        # over gloo (CPU tests, the one-GPU rehearsal) a per-bucket update
-        # measured 1e-2 off the single-process update, so gloo keeps one
-        # optimizer launch after every wait.
         mode = os.environ.get("TDG_DP_OVERLAP_OPT", "tail")
-        if mode == "tail" and not (ddp is not None and ddp._stream_ordered):
-            mode = "0"
         if ddp is not None and ddp.active and fp8_state is None and mode != "0":
             ddp.attach_optimizer(opt, release=mode != "tail")
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
