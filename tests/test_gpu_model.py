@@ -27,7 +27,9 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("preset,kw", [("tiny", dict(src_vocab=300, tgt_vocab=250)),
                                        ("reference", dict(src_vocab=7765, tgt_vocab=7010)),
-                                       ("tiny", dict(d_model=512, heads=8, d_ff=2048, src_vocab=1000, tgt_vocab=1000))])
+                                       ("tiny", dict(d_model=512, heads=8, d_ff=2048, src_vocab=1000, tgt_vocab=1000)),
+                                       # d 1024: FFN dgrad against the transposed W2 copy
+                                       ("tiny", dict(d_model=1024, heads=16, d_ff=4096, src_vocab=500, tgt_vocab=500))])
 @pytest.mark.parametrize("dropout", [0.0, 0.1])
 def test_gpu_matches_cpu(preset, kw, dropout):
     cfg = model_config(preset, dropout=dropout, **kw)
