@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ gamma, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ ds_out,
     const bf16_t* __restrict__ dres_in, float* __restrict__ part_g, float* __restrict__ part_b,
     float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
-    const long long* ctr, uint64_t site) {
+    const long long* ctr, uint64_t site, int iters) {
   constexpr int VEC = D / 64;
   __shared__ float red[3][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -97,8 +97,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   float gm[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) gm[i] = gamma[lane * VEC + i];
-  const int r0 = blockIdx.x * (4 * RPW) + w * RPW;
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  // `iters` row groups per block, partial column sums accumulated across them
+  // (fewer partial rows for the fold: D = 1024 uses 2)
+#pragma unroll 1
+  for (int it = 0; it < iters; ++it) {
+  const int r0 = (blockIdx.x * iters + it) * (4 * RPW) + w * RPW;
+  if (r0 >= M) break;
   RowVec<VEC> g[RPW], h[RPW], e[RPW];
   float mean[RPW], rstd[RPW];
 #pragma unroll
@@ -149,6 +154,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     }
     dh.store_bf(dh_out + base);
   }
+  }  // row groups
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     red[0][w][lane * VEC + i] = ag[i];
@@ -192,14 +198,15 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
               int accumulate, int skip_reduce, hipStream_t st) {
   const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
   constexpr int RPW = D >= 1024 ? 2 : 4;
-  const int rpb = 4 * RPW;
+  constexpr int ITERS = D >= 1024 ? 2 : 1;  // keep in sync with kernels.py ln_bwd_nparts
+  const int rpb = 4 * RPW * ITERS;
   const int nb = cdiv(M, rpb);
   float* pg = ws;
   float* pb = ws + (size_t)nb * D;
   float* ps = dbias ? ws + 2 * (size_t)nb * D : nullptr;
   hipLaunchKernelGGL((ln_bwd_kernel<D, RPW>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
-                     (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site);
+                     (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site, ITERS);
   if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};

@@ -449,6 +449,13 @@ def gemm_ln(a2, w, bias, x2, gamma, beta, p, seed, ctr, site, eps=1e-6):
     return y, h, stats[0], stats[1]
 
 
+def ln_bwd_nparts(M: int, D: int) -> int:
+    """Partial-sum rows ln_bwd writes (norm.hip ln_bwd_d: 4 waves x RPW rows x
+    ITERS row groups per block)."""
+    rpw, iters = (2, 2) if D >= 1024 else (4, 1)
+    return math.ceil(M / (4 * rpw * iters))
+
+
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
            dres=None, accumulate=False, defer=None):
     """`defer` (a list): leave the dgamma / dbeta / dbias partial sums in a
@@ -466,7 +473,7 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
                accumulate, defer is not None)
     if defer is not None:
-        nb = math.ceil(M / (4 * (2 if D >= 1024 else 4)))  # rows per ln_bwd block (norm.hip)
+        nb = ln_bwd_nparts(M, D)
         outs = [dgamma, dbeta] + ([dbias] if dbias is not None else [])
         for i, o in enumerate(outs):
             defer.append((ws[i * nb * D:(i + 1) * nb * D], o, nb, D, 1.0 if accumulate else 0.0))
