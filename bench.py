@@ -54,7 +54,8 @@ def main() -> None:
     ap.add_argument("--defer-wgrad", type=int, default=-1,
                     help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: FFN forward GEMMs in e4m3 with delayed scaling (BASELINE config 5)")
+                    help="fp8: FFN + attention-input forward GEMMs in e4m3 with delayed scaling "
+                         "(BASELINE config 5)")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     ap.add_argument("--force-dp", type=int, default=0,
                     help="1: run the RCCL data-parallel path even with one rank (testing)")
@@ -136,7 +137,8 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16" if args.dtype == "bf16" else "fp8 (e4m3 FFN forward GEMMs, bf16 elsewhere)",
+            "dtype": "bf16" if args.dtype == "bf16" else
+                     "fp8 (e4m3 forward GEMMs of the FFNs and attention input projections, bf16 elsewhere)",
             "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
                 "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "

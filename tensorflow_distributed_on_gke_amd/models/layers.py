@@ -62,7 +62,7 @@ class RunCtx:
     store: Optional[ParamStore] = None
     # inference probe: {site: [B,H,Lq,Lk] f32 attention weights} when set
     attn_maps: Optional[dict] = None
-    # ops.fp8.Fp8State: FFN forward GEMMs in e4m3 (BASELINE config 5)
+    # ops.fp8.Fp8State: FFN and attention-input forward GEMMs in e4m3 (BASELINE config 5)
     fp8: Optional[object] = None
     # WgradQueue: weight gradients deferred to the end of backward (grouped)
     wgrad: Optional["WgradQueue"] = None
@@ -438,7 +438,9 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ctx.meta = (heads, causal, scale, site, rt)
         x2 = x.reshape(B * L, d)
         if x.is_cuda:
-            qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master, bias_lp=bqkv.compute)  # [M, 3d]
+            qkv = rt.fp8.linear(x2, wqkv, bqkv) if rt.fp8 is not None else None
+            if qkv is None:
+                qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master, bias_lp=bqkv.compute)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
             o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
             s = None  # projection fused with the LayerNorm below
@@ -506,7 +508,9 @@ class CrossKVFn(torch.autograd.Function):
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
         ctx.save_for_backward(e2)
         if enc.is_cuda:
-            kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master, bias_lp=bkv.compute)
+            kv = rt.fp8.linear(e2.contiguous(), wkv, bkv) if rt.fp8 is not None else None
+            if kv is None:
+                kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master, bias_lp=bkv.compute)
         else:
             kv = e2 @ wkv.master.t() + bkv.master
         return kv.view(B, S, -1)
@@ -559,7 +563,9 @@ class CrossAttnBlockFn(torch.autograd.Function):
         if kv5 is None:
             raise ValueError("kv_all must be contiguous")
         if x.is_cuda:
-            q = K.linear_fwd(x2, wq.compute, bq.master, bias_lp=bq.compute)
+            q = rt.fp8.linear(x2, wq, bq) if rt.fp8 is not None else None
+            if q is None:
+                q = K.linear_fwd(x2, wq.compute, bq.master, bias_lp=bq.compute)
             o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
                                 False)
             s = None  # projection fused with the LayerNorm below

@@ -151,15 +151,24 @@ class Fp8Weights:
 
 
 class Fp8State:
-    """Per-model fp8 bookkeeping: meta, weight copies and activation slots
-    (one set per FFN layer)."""
+    """Per-model fp8 bookkeeping: meta, weight copies and activation slots.
+
+    fp8 forward GEMMs: both FFN projections of every layer, and the attention
+    input projections -- self-attention Q|K|V, cross-attention Q and the
+    batched cross-attention K|V of the encoder output. Each of their inputs is
+    the output of a LayerNorm (which then emits the e4m3 copy, `ln_slots`),
+    except the first layer's Q|K|V input (the embedding), quantised by its
+    own kernel. The attention output projections stay bf16: their input, the
+    attention output, would need a separate quantisation pass."""
 
     def __init__(self, model, margin: int = 0):
         self.meta = Fp8Meta(model.device, margin=margin)
         self.weights = Fp8Weights(self.meta)
         self.ffn_slots: Dict[int, Tuple[int, int]] = {}
-        # LayerNorms whose output is an FFN input: they emit the e4m3 copy
+        # LayerNorms whose output is an fp8 GEMM input: they emit the e4m3 copy
         self.ln_slots: Dict[int, int] = {}
+        # attention input projections: weight -> activation slot
+        self.proj_slots: Dict[int, int] = {}
         self.stash: Dict[int, torch.Tensor] = {}
         for layer in list(model.enc_layers) + list(model.dec_layers):
             self.weights.add(layer.ff1.w)
@@ -169,7 +178,36 @@ class Fp8State:
             self.ffn_slots[id(layer.ff1.w)] = (xs, hs)
             feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
             self.ln_slots[id(feeder.gamma)] = xs
+
+        def proj(w, feeder_ln) -> None:
+            self.weights.add(w)
+            xs = self.meta.slot("p:" + w.name)
+            self.proj_slots[id(w)] = xs
+            if feeder_ln is not None:
+                self.ln_slots[id(feeder_ln.gamma)] = xs
+
+        enc, dec = list(model.enc_layers), list(model.dec_layers)
+        for i, layer in enumerate(enc):
+            proj(layer.qkv.w, enc[i - 1].ln2 if i else None)
+        for i, layer in enumerate(dec):
+            proj(layer.qkv1.w, dec[i - 1].ln3 if i else None)
+            proj(layer.q2.w, layer.ln1)
+        proj(model.cross_kv.w, enc[-1].ln2)
         self.weights.calibrate()
+
+    def linear(self, x2: torch.Tensor, w, b) -> Optional[torch.Tensor]:
+        """y = x2 @ w^T + b with e4m3 operands when `w` is an fp8 attention
+        projection (the input's e4m3 copy comes from its LayerNorm, else it is
+        quantised here); None otherwise."""
+        xs = self.proj_slots.get(id(w))
+        if xs is None:
+            return None
+        w8, ws = self.weights.get(w)
+        x8 = self.stash.pop(xs, None)
+        if x8 is None:
+            x8 = quantize(x2, self.meta, xs)
+        y, _ = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws)
+        return y
 
     def after_step(self) -> None:
         self.meta.update()
