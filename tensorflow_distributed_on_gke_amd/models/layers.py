@@ -648,7 +648,7 @@ class FFNBlockFn(torch.autograd.Function):
                 x8 = fp8.quantize(x2, st.meta, xs)
             x8 = x8.view(x2.shape)
             h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs)
-            f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2)
+            f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2, bias_lp=b2.compute)
         elif x.is_cuda:
             h = K.linear_fwd(x2, w1.compute, b1.master, relu=True, bias_lp=b1.compute)
             f = None  # second projection fused with the LayerNorm below
