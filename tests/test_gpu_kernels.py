@@ -224,6 +224,30 @@ def test_attention_fwd_bwd(hd, causal, Lq, Lk):
     _close(dq, qr.grad, 3e-2, "attn dq")
 
 
+@pytest.mark.parametrize("causal,Lq,Lk", [(False, 128, 128), (True, 128, 128), (False, 70, 100)])
+def test_attention_bwd_more_items_than_cus(causal, Lq, Lk):
+    """B*H = 267 (batch, head) items, more than the 256 CUs, ragged key lengths."""
+    B, H, hd = 89, 3, 64
+    torch.manual_seed(1)
+    q = _bf(torch.randn(B, Lq, H, hd))
+    k = _bf(torch.randn(B, Lk, H, hd))
+    v = _bf(torch.randn(B, Lk, H, hd))
+    kv_len = torch.randint(1, Lk + 1, (B,), dtype=torch.int32)
+    kv_len[0] = Lk
+    scale = 1 / math.sqrt(hd)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref, _ = _ref_attn(qr, kr, vr, kv_len, causal, scale)
+    out, lse = kk.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), kv_len.to(DEV), scale, causal)
+    dout = _bf(torch.randn(B, Lq, H, hd))
+    ref.backward(dout.float())
+    dq, dk, dv = (torch.empty_like(t, device=DEV) for t in (q, k, v))
+    kk.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), out, dout.to(DEV), lse, dq, dk, dv, kv_len.to(DEV),
+               scale, causal)
+    _close(dv, vr.grad, 3e-2, "attn dv")
+    _close(dk, kr.grad, 3e-2, "attn dk")
+    _close(dq, qr.grad, 3e-2, "attn dq")
+
+
 def test_attention_strided_fused_qkv():
     # q/k/v as strided views into a fused [B, L, 3, H, hd] projection output
     B, L, H, hd = 2, 96, 8, 64
