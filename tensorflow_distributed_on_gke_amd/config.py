@@ -84,7 +84,11 @@ class Settings:
     profile_steps: int = 5  # active profiled steps (after 1 wait + 1 warm-up step)
     kill_at_step: int = -1  # fault injection (tests): global step at which to exit
     kill_rank: int = -1  # rank that exits (-1: the last rank)
-    loss_mode: str = "replica_mean"  # reference per-replica token mean / workers
+    # "replica_mean": the reference's per-replica token mean / workers
+    # (transformer_model.py:11-17); "global_mean": sum of all replicas' token
+    # losses / all replicas' label count (equal to the single-process loss on
+    # the global batch, whatever the per-replica token counts)
+    loss_mode: str = "replica_mean"
 
     def global_batch(self, world: int) -> int:
         return self.local_batch_size * world

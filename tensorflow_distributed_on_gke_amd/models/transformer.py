@@ -271,18 +271,23 @@ class Transformer:
     def loss_and_backward(self, src, tgt, rt: RunCtx, workers: float,
                           accum: Optional[torch.Tensor] = None, backward: bool = True,
                           step_out: Optional[torch.Tensor] = None,
-                          bump_ctr: bool = False) -> torch.Tensor:
+                          bump_ctr: bool = False, ntok_sum=None) -> torch.Tensor:
         """Teacher-forced forward, masked CE / accuracy, and (if `backward`)
         the full backward into the flat gradient buffer. Returns a device
         tensor [local_loss, accuracy] (loss already / workers, as the
         reference's local_loss_function). No host synchronisation.
-        bump_ctr: advance the dropout RNG step counter rt.ctr first."""
+        bump_ctr: advance the dropout RNG step counter rt.ctr first.
+        ntok_sum: global-token-mean loss -- called with this replica's label
+        count, turns it in place into the count over all replicas (returns an
+        async work handle or None); pass workers = 1 with it."""
         cfg = self.cfg
         dev = src.device
         if dev.type == "cuda":  # split / lengths / token count / ctr: one launch
             tgt_in, labels, src_len, tgt_len, ntok = K.prep_batch(
                 src, tgt, rt.ctr if bump_ctr else None)
             lengths = (src_len, tgt_len)
+            # the label count all-reduce flies during the forward
+            ntok_work = ntok_sum(ntok) if ntok_sum is not None else None
         else:
             if bump_ctr:
                 rt.ctr.add_(1)
@@ -301,6 +306,8 @@ class Transformer:
             logits = self.project(dec.detach())
             row_loss = K.workspace("row_loss", M, dev)[:M]
             row_cor = K.workspace("row_correct", M, dev)[:M]
+            if ntok_work is not None:
+                ntok_work.wait()
             K.xent(logits, cfg.tgt_vocab, labels, ntok, workers, cfg.label_smoothing, row_loss,
                    row_cor, write_grad=backward)
             K.xent_stats(row_loss, row_cor, ntok, workers, step_out, accum)
@@ -314,7 +321,12 @@ class Transformer:
             lg = self.project(dec.detach())
             lab = labels.reshape(-1)
             mask = (lab != PAD_ID).to(torch.float32)
-            ntok = mask.sum().clamp_min(1.0)
+            ntok = mask.sum()
+            if ntok_sum is not None:
+                w = ntok_sum(ntok)
+                if w is not None:
+                    w.wait()
+            ntok = ntok.clamp_min(1.0)
             logp = torch.log_softmax(lg, dim=-1)
             eps = cfg.label_smoothing
             nll = -logp.gather(1, lab.view(-1, 1)).squeeze(1)

@@ -106,7 +106,10 @@ class Trainer:
             from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
             self.fp8 = Fp8State(self.model)
         self.step_fn = TrainStep(self.model, self.opt, self.ddp, workers=info.world, seed=s.seed + 17,
-                                 fp8_state=self.fp8)
+                                 fp8_state=self.fp8, loss_mode=s.loss_mode)
+        # summed accuracy over replicas: a mean of per-replica ratios, or (global
+        # token mean) already the global ratio
+        self._acc_div = 1 if self.step_fn.global_mean else info.world
         if self.tokenizers is not None:
             from tensorflow_distributed_on_gke_amd.data.text import TextPairs
             st, tt = self.tokenizers
@@ -250,14 +253,14 @@ class Trainer:
                     st = summarize(self.timer.drain())
                     if info.chief:
                         self.log(f"Epoch {epoch + 1} Batch {batch} Loss {float(a[0]) / n:.4f} "
-                                 f"Accuracy {float(a[1]) / (n * info.world):.4f}")
+                                 f"Accuracy {float(a[1]) / (n * self._acc_div):.4f}")
                         self.metrics.write(kind="train", epoch=epoch + 1, batch=batch, step=self.global_step,
-                                           loss=float(a[0]) / n, accuracy=float(a[1]) / (n * info.world),
+                                           loss=float(a[0]) / n, accuracy=float(a[1]) / (n * self._acc_div),
                                            **st)
             a = self._reduce(self.step_fn.accum)
             n = max(float(a[2]) / info.world, 1.0)
             train_loss = float(a[0]) / n
-            train_acc = float(a[1]) / (n * info.world)
+            train_acc = float(a[1]) / (n * self._acc_div)
             if info.device.type == "cuda":
                 torch.cuda.synchronize()
             train_time = time.time() - t0

@@ -16,6 +16,7 @@ import os
 from typing import Optional, Tuple
 
 import torch
+import torch.distributed as dist
 
 from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
@@ -37,11 +38,22 @@ ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 class TrainStep:
     def __init__(self, model: Transformer, opt: Adam, ddp: Optional[DataParallel], workers: float,
                  seed: int = 0, dropout: Optional[float] = None, fp8_state=None,
-                 defer_wgrad: Optional[bool] = None):
+                 defer_wgrad: Optional[bool] = None, loss_mode: str = "replica_mean"):
         self.model = model
         self.opt = opt
         self.ddp = ddp
         self.workers = float(workers)
+        # global token mean: every replica's loss is normalised by the label
+        # count of the whole global batch (one scalar all-reduce per step,
+        # overlapped with the forward) and the gradients are SUM-reduced
+        if loss_mode not in ("replica_mean", "global_mean"):
+            raise ValueError(f"loss_mode must be replica_mean or global_mean, got {loss_mode!r}")
+        self.global_mean = loss_mode == "global_mean" and ddp is not None and ddp.world > 1
+        self._ntok_sum = None
+        if self.global_mean:
+            self.workers = 1.0
+            grp = ddp.group
+            self._ntok_sum = lambda t: dist.all_reduce(t, group=grp, async_op=True)
         dev = model.device
         self.rt = RunCtx(training=True, dropout=model.cfg.dropout if dropout is None else dropout,
                          seed=seed, ctr=torch.zeros(1, dtype=torch.int64, device=dev),
@@ -76,7 +88,7 @@ class TrainStep:
 
     def eager(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         self.model.loss_and_backward(src, tgt, self.rt, self.workers, accum=self.accum,
-                                     step_out=self.last, bump_ctr=True)
+                                     step_out=self.last, bump_ctr=True, ntok_sum=self._ntok_sum)
         if self.ddp is not None:
             self.ddp.finish()
         else:

@@ -37,7 +37,7 @@ def _batch(rank, i):
     return src, tgt
 
 
-def _worker(rank, world, port, out, opt_mode):
+def _worker(rank, world, port, out, opt_mode, loss_mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
                       TDG_DP_WAVE_TILES="37", TDG_DP_OVERLAP_OPT=opt_mode)
@@ -54,7 +54,8 @@ def _worker(rank, world, port, out, opt_mode):
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     ddp = DataParallel(m.store, bucket_mb=1.0)
     ddp.broadcast_params(0)
-    step = TrainStep(m, opt, ddp, workers=world, seed=5)
+    step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
+    assert step.global_mean == (loss_mode == "global_mean")
     assert step.rt.wgrad is not None and step.rt.wgrad.wave_tiles == 37
     losses = []
     for i in range(STEPS):
@@ -68,8 +69,9 @@ def _worker(rank, world, port, out, opt_mode):
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("opt_mode", ["0", "tail"])
-def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, monkeypatch):
+@pytest.mark.parametrize("opt_mode,loss_mode", [("0", "replica_mean"), ("tail", "replica_mean"),
+                                                ("tail", "global_mean")])
+def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode, monkeypatch):
     from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
@@ -77,7 +79,7 @@ def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, monkeypatc
 
     world = 2
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _port(), out, opt_mode), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode), nprocs=world, join=True,
                        start_method="spawn")
     r0 = torch.load(out + ".0", weights_only=True)
     r1 = torch.load(out + ".1", weights_only=True)
@@ -93,11 +95,20 @@ def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, monkeypatc
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     losses = []
     for i in range(STEPS):
+        # global token mean: both parts normalised by the global label count
+        n_all = float(sum(int((_batch(r, i)[1][:, 1:] != 0).sum()) for r in range(world)))
+
+        def fill(t, n=n_all):
+            t.fill_(n)
+
         for r in range(world):
             rt = RunCtx(training=True, dropout=0.0, seed=5, store=m.store,
                         ctr=torch.zeros(1, dtype=torch.int64, device="cuda"), accumulate=r > 0)
             src, tgt = _batch(r, i)
-            o = m.loss_and_backward(src.cuda(), tgt.cuda(), rt, float(world))
+            if loss_mode == "global_mean":
+                o = m.loss_and_backward(src.cuda(), tgt.cuda(), rt, 1.0, ntok_sum=fill)
+            else:
+                o = m.loss_and_backward(src.cuda(), tgt.cuda(), rt, float(world))
             if r == 0:
                 losses.append(o.clone().cpu())
         opt.apply()

@@ -40,7 +40,7 @@ def _data(rank, world):
     return SyntheticPairs(4, 10, 11, 60, 50, seed=3, rank=rank, world=world, min_len=3)
 
 
-def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0):
+def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mode="replica_mean"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       TDG_DP_OVERLAP_OPT=str(overlap_opt))
@@ -62,7 +62,7 @@ def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0):
         early.append(sum(b.updated for b in ddp.buckets) - before)
 
     ddp._on_release = spy
-    step = TrainStep(m, opt, ddp, workers=world, seed=5)
+    step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
     data = _data(rank, world)
     losses = []
     for i in range(STEPS):
@@ -84,17 +84,27 @@ def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0):
     tdist.shutdown()
 
 
-def _single_process_reference(world):
+def _fill(n):
+    """ntok_sum stand-in: the global label count, known up front (no handle)."""
+    def f(t):
+        t.fill_(n)
+    return f
+
+
+def _single_process_reference(world, global_mean=False):
     m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=1)
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     datas = [_data(r, world) for r in range(world)]
     losses = []
     for i in range(STEPS):
-        tot = 0.0
+        n_all = float(sum(int((datas[r].batch(i)[1][:, 1:] != 0).sum()) for r in range(world)))
         for r in range(world):
             rt = RunCtx(training=True, dropout=0.0, seed=5, ctr=torch.zeros(1, dtype=torch.int64),
                         accumulate=r > 0)
-            out = m.loss_and_backward(*datas[r].batch(i), rt, float(world))
+            if global_mean:  # every part normalised by the whole global batch's label count
+                out = m.loss_and_backward(*datas[r].batch(i), rt, 1.0, ntok_sum=_fill(n_all))
+            else:
+                out = m.loss_and_backward(*datas[r].batch(i), rt, float(world))
             if r == 0:
                 losses.append(out.clone())
         opt.apply()
@@ -119,6 +129,26 @@ def test_dp2_matches_single_process(tmp_path, bucket_mb, overlap_opt):
     ref_flat, ref_loss = _single_process_reference(world)
     assert not torch.equal(r0["flat"], Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat)
     assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(r0["loss"], ref_loss, atol=1e-6)
+
+
+def test_dp2_global_token_mean_loss(tmp_path):
+    """loss_mode=global_mean: replicas with different label counts give the
+    update of one process on the global batch with a plain token-mean loss."""
+    world = 2
+    d0, d1 = _data(0, world), _data(1, world)
+    assert any(int((d0.batch(i)[1][:, 1:] != 0).sum()) != int((d1.batch(i)[1][:, 1:] != 0).sum())
+               for i in range(STEPS))
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, _free_port(), out, 64.0, None, 0, "global_mean"),
+                       nprocs=world, join=True, start_method="spawn")
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    assert torch.equal(r0["flat"], r1["flat"])
+    ref_flat, ref_loss = _single_process_reference(world, global_mean=True)
+    rep_flat, _ = _single_process_reference(world)
+    assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
+    assert not torch.allclose(ref_flat, rep_flat, atol=1e-6, rtol=1e-5)  # the modes differ
     assert torch.allclose(r0["loss"], ref_loss, atol=1e-6)
 
 
