@@ -90,9 +90,13 @@ def main() -> None:
         s, t = data.batch(i)
         batches.append((s.to(dev, non_blocking=True), t.to(dev, non_blocking=True)))
 
-    # HIP graph on one GPU only: the data-parallel path (also the --force-dp
-    # single-rank rehearsal of it) runs eager, its collectives outside capture
-    use_graph = args.graph if args.graph >= 0 else int(ddp is None and dev.type == "cuda")
+    # HIP graph by default on one GPU only. The data-parallel step (RCCL
+    # collectives inside the capture) replays bitwise like its eager run on a
+    # single-rank communicator (tests/test_gpu_graph.py) and takes 5.66 instead
+    # of 5.9-6.4 ms there, but is opt-in (--graph 1 or TDG_DP_GRAPH=1) until it
+    # has been validated on a multi-GPU node
+    dp_graph = os.environ.get("TDG_DP_GRAPH", "0") == "1"
+    use_graph = args.graph if args.graph >= 0 else int(dev.type == "cuda" and (ddp is None or dp_graph))
     if use_graph:
         step.capture(*batches[0])
     for i in range(args.warmup):

@@ -112,8 +112,19 @@ class TrainStep:
                 self.eager(*self._static)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.eager(*self._static)
+        if self.ddp is not None and self.ddp.active:
+            # collectives inside the graph (experimental, TDG_DP_GRAPH=1): no
+            # collective of the warm-up may still be pending in the process
+            # group's watchdog, and the watchdog's event queries from its own
+            # thread must not invalidate this thread's capture
+            torch.cuda.synchronize()
+            dist.barrier(group=self.ddp.group)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self.eager(*self._static)
+        else:
+            with torch.cuda.graph(g):
+                self.eager(*self._static)
         self.graph = g
 
     def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,105 @@
+"""HIP-graph replay of the whole training step equals the eager step.
+
+One GPU: TrainStep.capture() runs its warm-up steps eagerly, then captures
+one step; replays on new batches must leave exactly the weights that the
+same number of eager steps leave (dropout counter, Adam step and fp8 scales
+all live on the device). Data parallel (single-rank RCCL communicator,
+--force-dp): the step with its all-reduce spans and per-span Adam captured
+in one graph (thread-local capture mode) -- the experimental path the
+multi-GPU step could take (ROADMAP item 5); the 8-GPU RCCL replay itself is
+not testable on one GPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 3
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(dev):
+    g = torch.Generator().manual_seed(7)
+    out = []
+    for i in range(STEPS + 1):
+        src = torch.randint(4, 500, (16, 48), generator=g)
+        tgt = torch.randint(4, 400, (16, 41), generator=g)
+        src[:, 30 + i:] = 0
+        tgt[:, 25 + 2 * i:] = 0
+        out.append((src.to(dev), tgt.to(dev)))
+    return out
+
+
+def _run(dev, graph, ddp_factory=None):
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    from tensorflow_distributed_on_gke_amd.train.optim import Adam
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    kk.AUTOTUNE = False  # identical GEMM configs in both runs
+    cfg = model_config("tiny", d_model=256, heads=4, d_ff=1024, src_vocab=500, tgt_vocab=400, dropout=0.1)
+    m = Transformer(cfg).build(dev, seed=3)
+    opt = Adam(m.store, cfg.d_model, lr=0.003)
+    ddp = ddp_factory(m) if ddp_factory else None
+    step = TrainStep(m, opt, ddp, workers=1, seed=11)
+    bs = _batches(dev)
+    losses = []
+    if graph:
+        step.capture(*bs[0], warmup=2)  # two eager steps on batch 0
+    else:
+        for _ in range(2):
+            step(*bs[0])
+    for i in range(1, STEPS + 1):
+        losses.append(step(*bs[i]).clone())
+    torch.cuda.synchronize()
+    return m.store.flat.cpu(), torch.stack(losses).cpu(), step
+
+
+def test_graph_replay_matches_eager_one_gpu():
+    f_e, l_e, _ = _run("cuda", graph=False)
+    f_g, l_g, st = _run("cuda", graph=True)
+    assert st.graph is not None
+    assert torch.isfinite(f_g).all()
+    assert torch.equal(l_e, l_g), (l_e, l_g)
+    assert torch.equal(f_e, f_g)
+
+
+def _dp_worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
+    from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
+
+    info = tdist.init_distributed("cuda", force=True)
+
+    def mk(m):
+        d = DataParallel(m.store, bucket_mb=1.0, force=True)
+        d.broadcast_params(0)
+        return d
+
+    res = {}
+    for graph in (False, True):
+        f, l, st = _run(info.device, graph, mk)
+        assert st.ddp is not None and st.ddp.active and len(st.ddp.last_buckets) > 1
+        res["graph" if graph else "eager"] = (f, l)
+    torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1]},
+               out)
+    tdist.shutdown()
+
+
+def test_dp_step_graph_with_collectives_matches_eager(tmp_path):
+    out = str(tmp_path / "dp.pt")
+    mp.start_processes(_dp_worker, args=(_port(), out), nprocs=1, join=True, start_method="spawn")
+    r = torch.load(out, weights_only=True)
+    assert torch.equal(r["el"], r["gl"]), (r["el"], r["gl"])
+    assert torch.equal(r["ef"], r["gf"])
