@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel time over the LAST
-N training steps only (steps delimited by the Adam kernel, so autotuning and
-warm-up dispatches are excluded), as ms per step."""
+N training steps only (steps delimited by the batch-prep kernel that opens
+every step -- the Adam kernel when it is absent; the data-parallel path runs
+one Adam per bucket -- so autotuning and warm-up dispatches are excluded), as
+ms per step."""
 import csv
 import glob
 import os
@@ -13,7 +15,11 @@ def main(d, nsteps=5):
     traces = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     rows = list(csv.DictReader(open(traces[0])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ends = [i - 1 for i, r in enumerate(rows) if "prep_batch_kernel" in r["Kernel_Name"]]
+    if len(ends) > nsteps:
+        ends.append(len(rows) - 1)  # the last step runs to the end of the trace
+    else:
+        ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
     if len(ends) > nsteps:
         lo, hi = ends[-nsteps - 1] + 1, ends[-1] + 1
     else:
