@@ -43,6 +43,7 @@ from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+from tensorflow_distributed_on_gke_amd.utils.gcpolicy import ManualGC
 from tensorflow_distributed_on_gke_amd.utils.profiling import MetricsWriter, StepTimer, summarize, torch_profile
 
 RESUME_DIR = "resume"
@@ -220,6 +221,7 @@ class Trainer:
         prof_cm = torch_profile(s.profile_dir if info.chief else None, active=s.profile_steps)
         prof = prof_cm.__enter__()
         prof_left = s.profile_steps + 2 if s.profile_dir and info.chief else 0
+        mgc = ManualGC.from_env()  # no cyclic-GC pass inside a step
         for epoch in range(self.start_epoch, s.epochs):
             t0 = time.time()
             self.step_fn.accum.zero_()
@@ -233,6 +235,7 @@ class Trainer:
                 self.timer.start()
                 self.step_fn(src, tgt)
                 self.timer.stop()
+                mgc.step()
                 self.global_step += 1
                 if prof_left:
                     prof.step()
@@ -282,6 +285,7 @@ class Trainer:
                 self.log(f"Time taken for 1 epoch: {dt:.2f} secs ({st.tokens_per_s:,.0f} tokens/s)\n")
             if info.world > 1:
                 dist.barrier()
+        mgc.close()
         if prof_left:  # fewer steps than the profile window
             prof_cm.__exit__(None, None, None)
         return self.history
