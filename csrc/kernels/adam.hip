@@ -34,6 +34,49 @@ __device__ __forceinline__ float noam_lr(const AdamCfg& c, float step) {
   return rsqrtf(c.d_model) * fminf(rise, fall);
 }
 
+__device__ __forceinline__ void adam4(float4& pp, const float4& gg, float4& mm, float4& vv,
+                                      const AdamCfg& c, float lr, float lr_t, float ob1,
+                                      float ob2) {
+  float* P = &pp.x;
+  const float* G = &gg.x;
+  float* Mm = &mm.x;
+  float* Vv = &vv.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gk = G[k] * c.grad_scale;
+    Mm[k] += (gk - Mm[k]) * ob1;
+    Vv[k] += (gk * gk - Vv[k]) * ob2;
+    P[k] -= lr_t * Mm[k] / (sqrtf(Vv[k]) + c.eps) + lr * c.weight_decay * P[k];
+  }
+}
+
+__device__ __forceinline__ void st_nt4(float4* a, const float4& x) {
+  __builtin_nontemporal_store(x.x, &a->x);
+  __builtin_nontemporal_store(x.y, &a->y);
+  __builtin_nontemporal_store(x.z, &a->z);
+  __builtin_nontemporal_store(x.w, &a->w);
+}
+
+__device__ __forceinline__ void adam_store(float4* P4, float4* G4, float4* M4, float4* V4,
+                                           uint2* S2, long long i, const float4& pp,
+                                           const float4& mm, const float4& vv, int zero_grad) {
+  // the master weights are re-read by nothing until the next step: stream
+  // them (and the moments) past the caches; the bf16 shadow copy is read by
+  // the next forward's GEMMs, so it goes through L2 normally
+  st_nt4(P4 + i, pp);
+  st_nt4(M4 + i, mm);
+  st_nt4(V4 + i, vv);
+  if (zero_grad) G4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (S2) {
+    const uint32_t lo = (uint32_t)f2bf(pp.x) | ((uint32_t)f2bf(pp.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(pp.z) | ((uint32_t)f2bf(pp.w) << 16);
+    S2[i] = make_uint2(lo, hi);
+  }
+}
+
+// Streaming Adam: 16 B/param read (p, g, m, v) + 12 B written + 2 B shadow.
+// Two float4 groups per thread per iteration with all eight 16-byte loads
+// issued before any math (more bytes in flight per wave for HBM3E).
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ shadow, long long n,
@@ -45,32 +88,26 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   const float lr_t = lr * sqrtf(1.f - powf(c.beta2, t)) / (1.f - powf(c.beta1, t));
   const float ob1 = 1.f - c.beta1, ob2 = 1.f - c.beta2;
   const long long n4 = n >> 2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* P = &pp.x;
-    float* G = &gg.x;
-    float* Mm = &mm.x;
-    float* Vv = &vv.x;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = G[k] * c.grad_scale;
-      Mm[k] += (gk - Mm[k]) * ob1;
-      Vv[k] += (gk * gk - Vv[k]) * ob2;
-      P[k] -= lr_t * Mm[k] / (sqrtf(Vv[k]) + c.eps) + lr * c.weight_decay * P[k];
-    }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (c.zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (shadow) {
-      const uint32_t lo = (uint32_t)f2bf(P[0]) | ((uint32_t)f2bf(P[1]) << 16);
-      const uint32_t hi = (uint32_t)f2bf(P[2]) | ((uint32_t)f2bf(P[3]) << 16);
-      reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
-    }
+  float4* P4 = reinterpret_cast<float4*>(p);
+  float4* G4 = reinterpret_cast<float4*>(g);
+  float4* M4 = reinterpret_cast<float4*>(m);
+  float4* V4 = reinterpret_cast<float4*>(v);
+  uint2* S2 = shadow ? reinterpret_cast<uint2*>(shadow) : nullptr;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const long long j = i + stride;
+    float4 pa = P4[i], ga = G4[i], ma = M4[i], va = V4[i];
+    float4 pb = P4[j], gb = G4[j], mb = M4[j], vb = V4[j];
+    adam4(pa, ga, ma, va, c, lr, lr_t, ob1, ob2);
+    adam4(pb, gb, mb, vb, c, lr, lr_t, ob1, ob2);
+    adam_store(P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
+    adam_store(P4, G4, M4, V4, S2, j, pb, mb, vb, c.zero_grad);
+  }
+  if (i < n4) {
+    float4 pa = P4[i], ga = G4[i], ma = M4[i], va = V4[i];
+    adam4(pa, ga, ma, va, c, lr, lr_t, ob1, ob2);
+    adam_store(P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
   }
 }
 
