@@ -1,0 +1,37 @@
+"""bench.py contract under the driver's launcher, on CPU (gloo): two ranks via
+torch.distributed.run, one JSON line from rank 0 with the whole-job value."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_json_contract():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--preset", "tiny",
+           "--local-batch", "4", "--seq-len", "16"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 8
+    # whole-job tokens/s: global batch x (src + tgt) tokens per step / step time
+    expect = 8 * (16 + 16) / (d["ms_per_step"] / 1000.0)
+    assert abs(d["value"] - expect) / expect < 0.01
