@@ -50,7 +50,7 @@ def main() -> None:
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype (bf16 halves xGMI bytes)")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="1: capture step in a HIP graph (default: on for 1 GPU without data parallelism)")
+                    help="1: capture the step in HIP graphs (default on for GPUs; data parallel: segmented graph)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--defer-wgrad", type=int, default=-1,
                     help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
@@ -91,15 +91,13 @@ def main() -> None:
         s, t = data.batch(i)
         batches.append((s.to(dev, non_blocking=True), t.to(dev, non_blocking=True)))
 
-    # HIP graph by default on one GPU only. The data-parallel step (RCCL
-    # collectives inside the capture) replays bitwise like its eager run on a
-    # single-rank communicator (tests/test_gpu_graph.py) and takes 5.66 instead
-    # of 5.9-6.4 ms there, but is opt-in (--graph 1 or TDG_DP_GRAPH=1) until it
-    # has been validated on a multi-GPU node
-    dp_graph = os.environ.get("TDG_DP_GRAPH", "0") == "1"
-    use_graph = args.graph if args.graph >= 0 else int(dev.type == "cuda" and (ddp is None or dp_graph))
+    # HIP graph by default. One GPU: the whole step is one graph. Data
+    # parallel: a chain of graphs cut at the RCCL collectives, which stay
+    # eager calls between the segments (train/graphs.py; TDG_DP_GRAPH=full
+    # captures them inside one graph, TDG_DP_GRAPH=0 runs the step eagerly)
+    use_graph = args.graph if args.graph >= 0 else int(dev.type == "cuda")
     if use_graph:
-        step.capture(*batches[0])
+        use_graph = int(step.capture(*batches[0]))
     for i in range(args.warmup):
         step(*batches[i % len(batches)])
 
@@ -157,7 +155,8 @@ def main() -> None:
                 "local_batch": args.local_batch,
                 "seq_len": S,
                 "parallelism": f"dp{world}",
-                "hip_graph": bool(use_graph),
+                "hip_graph": (("segmented" if step.segments is not None else "full")
+                              if use_graph else False),
                 "grad_comm": args.grad_comm,
                 "defer_wgrad": step.rt.wgrad is not None,
                 "bucket_mb": args.bucket_mb,

@@ -50,7 +50,7 @@ int tdg_gemm_ln(const void* A, int lda, const void* W, int ldw, const float* bia
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
 int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, int B, int lab64, void* tgt_in,
                    void* labels, int* src_len, int* tgt_len, float* ntok, long long* ctr,
-                   int* row_lab, unsigned* ticket, hipStream_t st);
+                   int* row_lab, unsigned* ticket, int* bad_rows, hipStream_t st);
 int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* part, int M, int N,
                        int ld, int rows_per_block, float beta, hipStream_t st);
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
@@ -742,9 +742,10 @@ void prep_batch(const Tensor& src, const Tensor& tgt, const Tensor& tgt_in, cons
   for (const Tensor* t : {&src_len, &tgt_len})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() == B, "prep_batch: lengths");
   check_f32(ntok, "ntok");
-  // scratch: int32 [B + 1] -- per-row label counts + a zero-initialised ticket
-  TORCH_CHECK(scratch.is_cuda() && scratch.scalar_type() == at::kInt && scratch.numel() >= B + 1,
-              "prep_batch: scratch must be int32 [B + 1], last word zero");
+  // scratch: int32 [B + 2] -- per-row label counts, a zero-initialised
+  // ticket, and a sticky count of rows with a PAD before a non-PAD token
+  TORCH_CHECK(scratch.is_cuda() && scratch.scalar_type() == at::kInt && scratch.numel() >= B + 2,
+              "prep_batch: scratch must be int32 [B + 2], ticket word zero");
   long long* c = nullptr;
   if (ctr.has_value()) {
     TORCH_CHECK(ctr->is_cuda() && ctr->scalar_type() == at::kLong, "prep_batch: ctr");
@@ -755,7 +756,8 @@ void prep_batch(const Tensor& src, const Tensor& tgt, const Tensor& tgt_in, cons
                            tgt_in.data_ptr(), labels.data_ptr(), src_len.data_ptr<int>(),
                            tgt_len.data_ptr<int>(), ntok.data_ptr<float>(), c,
                            scratch.data_ptr<int>(),
-                           reinterpret_cast<unsigned*>(scratch.data_ptr<int>() + B), stream_of(src)),
+                           reinterpret_cast<unsigned*>(scratch.data_ptr<int>() + B),
+                           scratch.data_ptr<int>() + B + 1, stream_of(src)),
             "tdg prep_batch");
 }
 

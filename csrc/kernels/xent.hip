@@ -231,16 +231,26 @@ __global__ __launch_bounds__(64) void prep_batch_kernel(
     const LabT* __restrict__ src, int S, const LabT* __restrict__ tgt, int T1, int B,
     LabT* __restrict__ tgt_in, LabT* __restrict__ labels, int* __restrict__ src_len,
     int* __restrict__ tgt_len, float* __restrict__ ntok, long long* __restrict__ ctr,
-    int* __restrict__ row_lab, unsigned* __restrict__ ticket) {
+    int* __restrict__ row_lab, unsigned* __restrict__ ticket, int* __restrict__ bad_rows) {
   // one wave per row; the last wave to finish folds the label counts
   const int lane = threadIdx.x, b = blockIdx.x, T = T1 - 1;
-  int cs = 0, ct = 0, cl = 0;
-  for (int j = lane; j < S; j += 64) cs += src[(long long)b * S + j] != 0;
+  // cs/ct: non-PAD counts (the key lengths); es/et: one past the last non-PAD
+  // position. They differ only when a PAD sits inside a row: attention masks
+  // keys by length (trailing padding), while the reference masks every PAD
+  // position (transformer_model.py:56-62), so such rows are counted in
+  // bad_rows for the host to reject
+  int cs = 0, ct = 0, cl = 0, es = 0, et = 0;
+  for (int j = lane; j < S; j += 64) {
+    const bool nz = src[(long long)b * S + j] != 0;
+    cs += nz;
+    es = nz ? j + 1 : es;
+  }
   for (int j = lane; j < T1; j += 64) {
     const LabT v = tgt[(long long)b * T1 + j];
     if (j < T) {
       tgt_in[(long long)b * T + j] = v;
       ct += v != 0;
+      et = v != 0 ? j + 1 : et;
     }
     if (j > 0) {
       labels[(long long)b * T + j - 1] = v;
@@ -248,10 +258,12 @@ __global__ __launch_bounds__(64) void prep_batch_kernel(
     }
   }
   const float fs = wave_sum((float)cs), ft = wave_sum((float)ct), fl = wave_sum((float)cl);
+  const float ms = wave_max((float)es), mt = wave_max((float)et);
   __shared__ bool last;
   if (lane == 0) {
     src_len[b] = (int)fs;
     tgt_len[b] = (int)ft;
+    if (bad_rows && ((int)ms != (int)fs || (int)mt != (int)ft)) atomicAdd(bad_rows, 1);
     row_lab[b] = (int)fl;
     __threadfence();
     last = atomicAdd(ticket, 1u) == (unsigned)(B - 1);
@@ -322,16 +334,16 @@ extern "C" int tdg_count_tokens(const void* labels, int lab64, int M, float* out
 extern "C" int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, int B, int lab64,
                                void* tgt_in, void* labels, int* src_len, int* tgt_len,
                                float* ntok, long long* ctr, int* row_lab, unsigned* ticket,
-                               hipStream_t st) {
+                               int* bad_rows, hipStream_t st) {
   if (S < 1 || T1 < 2 || B < 1) return -1;
   if (lab64)
     hipLaunchKernelGGL(prep_batch_kernel<long long>, dim3(B), dim3(64), 0, st,
                        (const long long*)src, S, (const long long*)tgt, T1, B, (long long*)tgt_in,
-                       (long long*)labels, src_len, tgt_len, ntok, ctr, row_lab, ticket);
+                       (long long*)labels, src_len, tgt_len, ntok, ctr, row_lab, ticket, bad_rows);
   else
     hipLaunchKernelGGL(prep_batch_kernel<int>, dim3(B), dim3(64), 0, st, (const int*)src, S,
                        (const int*)tgt, T1, B, (int*)tgt_in, (int*)labels, src_len, tgt_len, ntok,
-                       ctr, row_lab, ticket);
+                       ctr, row_lab, ticket, bad_rows);
   return 0;
 }
 

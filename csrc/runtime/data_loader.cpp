@@ -85,7 +85,9 @@ void Prefetcher::worker() {
     synth_fill(cfg_, step, s.data(), t.data());
     {
       std::lock_guard<std::mutex> g(mu_);
-      ready_[step] = {std::move(s), std::move(t)};
+      // a skip-ahead (resume) may have passed this step while it was being
+      // filled: nobody will consume it, so do not keep it
+      if (step >= consumer_) ready_[step] = {std::move(s), std::move(t)};
     }
     cv_.notify_all();
   }

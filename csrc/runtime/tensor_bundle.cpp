@@ -138,16 +138,16 @@ static std::vector<PbField> pb_parse(const uint8_t* p, size_t n) {
       if (!get_varint(p, end, f.v)) throw std::runtime_error("protobuf: bad varint");
     } else if (f.wire == 2) {
       uint64_t l;
-      if (!get_varint(p, end, l) || p + l > end) throw std::runtime_error("protobuf: bad length");
+      if (!get_varint(p, end, l) || l > (uint64_t)(end - p)) throw std::runtime_error("protobuf: bad length");
       f.data = p;
       f.len = l;
       p += l;
     } else if (f.wire == 5) {
-      if (p + 4 > end) throw std::runtime_error("protobuf: short fixed32");
+      if (end - p < 4) throw std::runtime_error("protobuf: short fixed32");
       f.v = get_fixed32(p);
       p += 4;
     } else if (f.wire == 1) {
-      if (p + 8 > end) throw std::runtime_error("protobuf: short fixed64");
+      if (end - p < 8) throw std::runtime_error("protobuf: short fixed64");
       f.v = get_fixed64(p);
       p += 8;
     } else {
@@ -268,7 +268,9 @@ std::string write_block(std::string& file, const std::string& contents, Handle& 
 }
 
 std::string read_block(const std::string& file, Handle h, bool verify) {
-  if (h.offset + h.size + 5 > file.size()) throw std::runtime_error("sstable: block out of range");
+  // block + 5-byte trailer inside the file, written so no sum can wrap
+  if (file.size() < 5 || h.size > file.size() - 5 || h.offset > file.size() - 5 - h.size)
+    throw std::runtime_error("sstable: block out of range");
   const std::string contents = file.substr(h.offset, h.size);
   const uint8_t* tr = (const uint8_t*)file.data() + h.offset + h.size;
   if (tr[0] != 0) throw std::runtime_error("sstable: compressed blocks are not supported");
@@ -285,6 +287,8 @@ std::vector<std::pair<std::string, std::string>> parse_block(const std::string& 
   std::vector<std::pair<std::string, std::string>> out;
   if (b.size() < 4) throw std::runtime_error("sstable: short block");
   const uint32_t nr = get_fixed32((const uint8_t*)b.data() + b.size() - 4);
+  // the restart array (nr fixed32 entries) must fit in front of its count
+  if ((size_t)nr > (b.size() - 4) / 4) throw std::runtime_error("sstable: corrupt restart count");
   const size_t limit = b.size() - 4 - 4 * (size_t)nr;
   const uint8_t* p = (const uint8_t*)b.data();
   const uint8_t* end = p + limit;
@@ -292,7 +296,8 @@ std::vector<std::pair<std::string, std::string>> parse_block(const std::string& 
   while (p < end) {
     uint64_t shared, nonshared, vlen;
     if (!get_varint(p, end, shared) || !get_varint(p, end, nonshared) ||
-        !get_varint(p, end, vlen) || p + nonshared + vlen > end || shared > key.size())
+        !get_varint(p, end, vlen) || nonshared > (uint64_t)(end - p) ||
+        vlen > (uint64_t)(end - p) - nonshared || shared > key.size())
       throw std::runtime_error("sstable: corrupt entry");
     key.resize(shared);
     key.append((const char*)p, nonshared);
@@ -475,6 +480,14 @@ std::string BundleReader::read(const std::string& key, bool verify) const {
   const BundleEntry& e = entry(key);
   std::FILE* f = std::fopen((prefix_ + ".data-00000-of-00001").c_str(), "rb");
   if (!f) throw std::runtime_error("BundleReader: cannot open data file for " + prefix_);
+  // entry bounds against the data file before allocating (a corrupt or
+  // crafted index may carry any offset / size)
+  long fsize = -1;
+  if (std::fseek(f, 0, SEEK_END) == 0) fsize = std::ftell(f);
+  if (e.offset < 0 || e.size < 0 || fsize < 0 || e.size > fsize || e.offset > fsize - e.size) {
+    std::fclose(f);
+    throw std::runtime_error("BundleReader: entry out of range for " + key);
+  }
   std::string buf((size_t)e.size, '\0');
   if (std::fseek(f, (long)e.offset, SEEK_SET) != 0 ||
       std::fread(&buf[0], 1, (size_t)e.size, f) != (size_t)e.size) {
@@ -489,7 +502,7 @@ std::string BundleReader::read(const std::string& key, bool verify) const {
     const uint8_t* p = (const uint8_t*)buf.data();
     const uint8_t* end = p + buf.size();
     uint64_t len;
-    if (!get_varint(p, end, len) || p + 4 + len > end)
+    if (!get_varint(p, end, len) || end - p < 4 || len > (uint64_t)(end - p - 4))
       throw std::runtime_error("BundleReader: bad string tensor " + key);
     return std::string((const char*)p + 4, len);
   }

@@ -87,11 +87,100 @@ static void test_bundle(const std::string& dir) {
   CHECK(crc_unmask(crc_mask(0xdeadbeefu)) == 0xdeadbeefu);
 }
 
+// Malformed index files must fail with an exception, never read out of
+// bounds (this runs under ASan/UBSan): every 4-byte window overwritten with
+// 0xFFFFFFFF / 0x7FFFFFFF / 0x00000000 (huge restart counts, block handles,
+// varints), every truncation, and single-byte flips everywhere.
+static void test_malformed_sstable() {
+  std::vector<std::pair<std::string, std::string>> kv;
+  for (int i = 0; i < 40; ++i) {
+    char k[32];
+    std::snprintf(k, sizeof(k), "key/%03d/kernel", i);
+    kv.emplace_back(k, std::string((size_t)(i % 7) * 3 + 1, (char)('a' + i % 26)));
+  }
+  const std::string good = build_sstable(kv);
+  CHECK(parse_sstable(good, true).size() == kv.size());
+  int rejected = 0, parsed = 0;
+  auto attempt = [&](const std::string& f, bool verify) {
+    try {
+      parse_sstable(f, verify);
+      ++parsed;
+    } catch (const std::exception&) {
+      ++rejected;
+    }
+  };
+  for (uint32_t pat : {0xFFFFFFFFu, 0x7FFFFFFFu, 0u}) {
+    for (size_t off = 0; off + 4 <= good.size(); ++off) {
+      std::string f = good;
+      std::memcpy(&f[off], &pat, 4);
+      attempt(f, false);
+      attempt(f, true);
+    }
+  }
+  for (size_t n = 0; n < good.size(); ++n) attempt(good.substr(0, n), false);
+  for (size_t off = 0; off < good.size(); ++off) {
+    for (uint8_t x : {(uint8_t)0x80, (uint8_t)0x01, (uint8_t)0xFF}) {
+      std::string f = good;
+      f[off] = (char)((uint8_t)f[off] ^ x);
+      attempt(f, false);
+    }
+  }
+  CHECK(rejected > 0);
+  // the entry decoder on garbage
+  for (size_t off = 0; off + 4 <= good.size(); off += 3) {
+    try {
+      decode_entry(good.substr(off, 16));
+    } catch (const std::exception&) {
+    }
+  }
+  (void)parsed;
+}
+
+// A bundle whose index points past its data file is rejected before any
+// allocation of the claimed size.
+static void test_bundle_entry_bounds(const std::string& dir) {
+  const std::string prefix = dir + "/selftest_bounds";
+  std::vector<float> a(16, 1.f);
+  {
+    BundleWriter w(prefix);
+    w.add("x", 1, {16}, reinterpret_cast<const uint8_t*>(a.data()), a.size() * 4);
+    w.finish();
+  }
+  // rewrite the index with a huge offset / size for "x"
+  BundleReader ok(prefix, true);
+  BundleEntry e = ok.entry("x");
+  for (int which = 0; which < 3; ++which) {
+    BundleEntry bad = e;
+    if (which == 0) bad.offset = (int64_t)1 << 60;
+    if (which == 1) bad.size = (int64_t)1 << 60;
+    if (which == 2) bad.offset = 60;  // runs past the 64-byte file end
+    std::vector<std::pair<std::string, std::string>> kv = {{"", encode_header(1, 1)},
+                                                           {"x", encode_entry(bad)}};
+    const std::string idx = build_sstable(kv);
+    std::FILE* f = std::fopen((prefix + ".index").c_str(), "wb");
+    CHECK(f != nullptr);
+    std::fwrite(idx.data(), 1, idx.size(), f);
+    std::fclose(f);
+    BundleReader r(prefix, true);
+    bool threw = false;
+    try {
+      r.read("x", false);
+    } catch (const std::runtime_error&) {
+      threw = true;
+    }
+    CHECK(threw);
+  }
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : ".";
   const std::string what = argc > 2 ? argv[2] : "all";
   if (what == "all" || what == "prefetch") test_prefetcher();
-  if (what == "all" || what == "bundle") test_bundle(dir);
+  if (what == "all" || what == "bundle") {
+    test_bundle(dir);
+    test_malformed_sstable();
+    test_bundle_entry_bounds(dir);
+  }
   std::printf("runtime selftest ok (%s)\n", what.c_str());
   return 0;
 }

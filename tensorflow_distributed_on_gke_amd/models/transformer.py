@@ -163,10 +163,22 @@ class DecoderLayer:
 TRANSPOSED_FFN_DGRAD = os.environ.get("TDG_FFN_DGRAD_T", "1") != "0"
 
 
-def seq_lengths(tok: torch.Tensor) -> torch.Tensor:
+def seq_lengths(tok: torch.Tensor, check: bool = True) -> torch.Tensor:
     """Valid (non-PAD) length per row for right-padded batches -> int32 [B]
-    (the reference's padding mask `tok == 0`, transformer_model.py:56-62)."""
-    return (tok != PAD_ID).sum(dim=1, dtype=torch.int32)
+    (the reference's padding mask `tok == 0`, transformer_model.py:56-62).
+    Attention masks keys by this length, so a PAD before a non-PAD token
+    (which the reference would mask individually) is rejected: on the CPU
+    here (`check`), on the GPU by the batch-prep kernel's bad-row counter
+    (ops.kernels.check_trailing_padding)."""
+    nz = tok != PAD_ID
+    n = nz.sum(dim=1, dtype=torch.int32)
+    if check and tok.device.type == "cpu" and tok.numel():
+        pos = torch.arange(1, tok.shape[1] + 1, dtype=torch.int32).expand_as(tok)
+        last = torch.where(nz, pos, torch.zeros_like(pos)).amax(dim=1)
+        if not torch.equal(last, n):
+            raise ValueError("sequences must be right-padded: a PAD (id 0) token precedes a "
+                             "non-PAD token (attention masks keys by length)")
+    return n
 
 
 class Transformer:

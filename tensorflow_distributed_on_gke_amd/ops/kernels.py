@@ -538,10 +538,32 @@ def prep_batch(src, tgt, ctr=None):
     ntok = torch.empty(1, dtype=torch.float32, device=tgt.device)
     key = (tgt.device, B)
     scratch = _PREP_SCRATCH.get(key)
-    if scratch is None:  # [B] label counts + ticket (zero; the kernel re-arms it)
-        scratch = _PREP_SCRATCH[key] = torch.zeros(B + 1, dtype=torch.int32, device=tgt.device)
+    if scratch is None:  # [B] label counts, ticket (zero; the kernel re-arms it), bad-row count
+        scratch = _PREP_SCRATCH[key] = torch.zeros(B + 2, dtype=torch.int32, device=tgt.device)
     C().prep_batch(src, tgt, tgt_in, labels, lens[0], lens[1], ntok, ctr, scratch)
     return tgt_in, labels, lens[0], lens[1], ntok
+
+
+def interior_pad_rows(reset: bool = False) -> int:
+    """Rows seen by prep_batch (since the last reset) with a PAD token before
+    a non-PAD one. Attention masks keys by length, i.e. assumes trailing
+    padding; the reference masks each PAD position individually
+    (transformer_model.py:56-62), so callers reject batches where this is
+    non-zero. Reads a device counter (a host sync): call at log points."""
+    n = 0
+    for scratch in _PREP_SCRATCH.values():
+        n += int(scratch[-1].item())
+        if reset:
+            scratch[-1].zero_()
+    return n
+
+
+def check_trailing_padding() -> None:
+    """Raise if any batch prepared on the GPU had interior PAD tokens."""
+    n = interior_pad_rows(reset=True)
+    if n:
+        raise ValueError(f"{n} batch rows had a PAD (id 0) token before a non-PAD token; sequences "
+                         "must be right-padded (attention masks keys by length)")
 
 
 def xent(logits, V, labels, ntok, workers, smoothing, row_loss, row_correct, write_grad=True):

@@ -37,6 +37,21 @@ from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
 
 
+class Pending:
+    """Handle of an asynchronous collective issued through DataParallel.
+    `work` is the process group's Work once the collective has been issued
+    (at replay time when the step is a segmented graph, train/graphs.py)."""
+    __slots__ = ("owner", "work")
+
+    def __init__(self, owner: "DataParallel"):
+        self.owner = owner
+        self.work = None
+
+    def wait(self) -> None:
+        """The current stream waits for the collective (device-side)."""
+        self.owner._wait(self)
+
+
 @dataclass
 class Bucket:
     start: int
@@ -91,6 +106,9 @@ class DataParallel:
         self._comm_bufs = {}
         self.opt = None
         self._upd_stream = None
+        # a train/graphs.SegmentedGraph while the step is being captured: the
+        # collectives become host calls between graph segments
+        self.recorder = None
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
         if self.active:
@@ -160,9 +178,32 @@ class DataParallel:
                 buf = torch.empty(view.numel(), dtype=self.comm_dtype, device=view.device)
                 self._comm_bufs[(b.start, b.end)] = buf
             buf.copy_(view)
-            b.work = (dist.all_reduce(buf, group=self.group, async_op=True), buf, view)
+            b.work = (self.all_reduce_async(buf), buf, view)
         else:
-            b.work = (dist.all_reduce(view, group=self.group, async_op=True), None, None)
+            b.work = (self.all_reduce_async(view), None, None)
+
+    # ------------------------------------------------------------------ collectives
+    def all_reduce_async(self, t: torch.Tensor) -> Pending:
+        """SUM all-reduce of `t` in place, asynchronous. Under a segmented
+        capture it is recorded as a host call between graph segments (so it
+        is issued at replay, on the stream the graphs replay on)."""
+        h = Pending(self)
+        grp = self.group
+
+        def issue():
+            h.work = dist.all_reduce(t, group=grp, async_op=True)
+
+        if self.recorder is not None:
+            self.recorder.cut(issue)
+        else:
+            issue()
+        return h
+
+    def _wait(self, h: Pending) -> None:
+        if self.recorder is not None:
+            self.recorder.cut(lambda: h.work.wait())
+        else:
+            h.work.wait()
 
     def _on_ready(self, p: Param) -> None:
         self._ready[self._pos[p.index]] = True
@@ -177,10 +218,19 @@ class DataParallel:
 
     def _complete(self, b: Bucket) -> None:
         """Current stream waits for the bucket's all-reduce (device-side)."""
-        work, buf, view = b.work
-        work.wait()
-        if buf is not None:
-            view.copy_(buf)
+        self._complete_many([b])
+
+    def _complete_many(self, bs: List[Bucket]) -> None:
+        hs = [b.work[0] for b in bs]
+        if self.recorder is not None:  # one host call between two graph segments
+            self.recorder.cut(lambda: [h.work.wait() for h in hs])
+        else:
+            for h in hs:
+                h.wait()
+        for b in bs:
+            _, buf, view = b.work
+            if buf is not None:
+                view.copy_(buf)
 
     def _on_release(self) -> None:
         if self.opt is None:
@@ -215,13 +265,18 @@ class DataParallel:
         self._launch_span(self.store.total)
         if self._upd_stream is not None:
             torch.cuda.current_stream(self._upd_stream.device).wait_stream(self._upd_stream)
-        # Work.wait() orders the current stream after the collective, so each
-        # bucket's Adam is queued right behind ITS wait and runs while the
-        # later buckets' all-reduces are still in flight.
-        for b in self.buckets:
-            if not b.updated:
-                self._complete(b)
-                if self.opt is not None:
+        # Work.wait() orders the current stream after the collective. Two
+        # groups: the spans launched during backward (normally complete by
+        # now) and the span launched just above; the Adam of the first group
+        # runs while the last all-reduce is still in flight (the exposed
+        # tail). Grouping keeps a segmented graph at two wait points.
+        todo = [b for b in self.buckets if not b.updated]
+        for grp in (todo[:-1], todo[-1:]):
+            if not grp:
+                continue
+            self._complete_many(grp)
+            if self.opt is not None:
+                for b in grp:
                     self.opt.apply_range(b.start, b.end, inc_step=False)
         if self.opt is not None:
             self.opt.advance_step()

@@ -39,6 +39,7 @@ from tensorflow_distributed_on_gke_amd.config import Settings
 from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
 from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
@@ -203,6 +204,8 @@ class Trainer:
             # workers_count=1: the test loss is a plain per-replica mean
             self.model.loss_and_backward(src, tgt, rt, 1.0, accum=acc, backward=False, step_out=out)
         a = self._reduce(acc)
+        if self.info.device.type == "cuda":
+            K.check_trailing_padding()
         n = max(float(a[2]), 1.0)
         return {"loss": float(a[0]) / n, "acc": float(a[1]) / n}
 
@@ -230,7 +233,11 @@ class Trainer:
                 src, tgt = self._to_dev(self.train_data.next())
                 epoch_tokens += (src.shape[1] + tgt.shape[1] - 1) * src.shape[0] * info.world
                 if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured:
-                    self.step_fn.capture(src, tgt)
+                    # capture() restores the state its warm-up steps changed,
+                    # so this batch is still trained exactly once (below)
+                    if not self.step_fn.capture(src, tgt) and info.chief:
+                        self.log("note: the data-parallel step runs eagerly (TDG_DP_GRAPH=0 or an "
+                                 "option that needs an uncapturable stream)")
                     captured = True
                 self.timer.start()
                 self.step_fn(src, tgt)
@@ -251,6 +258,8 @@ class Trainer:
                     sys.stdout.flush()
                     os._exit(17)
                 if batch % s.log_every == 0:
+                    if info.device.type == "cuda":
+                        K.check_trailing_padding()  # rows with interior PADs (device counter)
                     a = self._reduce(self.step_fn.accum)
                     n = max(float(a[2]) / info.world, 1.0)
                     st = summarize(self.timer.drain())

@@ -22,7 +22,9 @@ from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
+from tensorflow_distributed_on_gke_amd.ops import streams
 from tensorflow_distributed_on_gke_amd.ops.streams import join
+from tensorflow_distributed_on_gke_amd.train.graphs import SegmentedGraph, prepare_capture
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 
@@ -33,6 +35,14 @@ CHUNKED_WGRAD = os.environ.get("TDG_DP_CHUNKED_WGRAD", "1") != "0"
 WAVE_TILES = int(os.environ.get("TDG_DP_WAVE_TILES", "0"))
 # skip the optimizer's gradient zeroing (all GPU gradient writers overwrite)
 ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
+# how a data-parallel step is captured (TrainStep.capture):
+#   "seg"  -- chain of HIP graphs cut at the collectives, which stay eager
+#             RCCL calls between the segments (train/graphs.py; default)
+#   "full" -- one graph with the collectives captured inside it
+#   "0"    -- no capture: the data-parallel step runs eagerly
+DP_GRAPH = os.environ.get("TDG_DP_GRAPH", "seg")
+if DP_GRAPH == "1":  # round-1 spelling of "full"
+    DP_GRAPH = "full"
 
 
 class TrainStep:
@@ -52,8 +62,7 @@ class TrainStep:
         self._ntok_sum = None
         if self.global_mean:
             self.workers = 1.0
-            grp = ddp.group
-            self._ntok_sum = lambda t: dist.all_reduce(t, group=grp, async_op=True)
+            self._ntok_sum = ddp.all_reduce_async
         dev = model.device
         self.rt = RunCtx(training=True, dropout=model.cfg.dropout if dropout is None else dropout,
                          seed=seed, ctr=torch.zeros(1, dtype=torch.int64, device=dev),
@@ -84,7 +93,51 @@ class TrainStep:
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)
         self.last = torch.zeros(2, dtype=torch.float32, device=dev)
         self.graph = None
+        self.segments: Optional[SegmentedGraph] = None
         self._static: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+
+    @property
+    def captured(self) -> bool:
+        return self.graph is not None or self.segments is not None
+
+    def capture_mode(self) -> str:
+        """"single" (one graph, no collectives), "seg", "full" or "0" (the
+        data-parallel step stays eager)."""
+        if self.ddp is None or not self.ddp.active:
+            return "single"
+        if DP_GRAPH not in ("seg", "full", "0"):
+            raise ValueError(f"TDG_DP_GRAPH must be seg, full or 0, got {DP_GRAPH!r}")
+        if DP_GRAPH == "seg" and (self.ddp._upd_stream is not None or streams.ENABLED):
+            # mid-backward Adam on its own stream / the weight-gradient side
+            # stream would leave unjoined work at a cut
+            return "0"
+        return DP_GRAPH
+
+    # ------------------------------------------------------------------ state
+    def _state(self):
+        """Every tensor a training step mutates that outlives the step."""
+        ts = [self.model.store.flat, self.opt.m, self.opt.v, self.opt.step, self.rt.ctr,
+              self.accum, self.last]
+        if self.fp8 is not None:
+            ts += [self.fp8.meta.scale, self.fp8.meta.inv_scale]
+        return ts
+
+    def snapshot(self):
+        st = [t.clone() for t in self._state()]
+        if self.fp8 is not None:
+            st.append(self.fp8.meta.amax.clone())
+        return st
+
+    def restore(self, st) -> None:
+        """Put back a snapshot(): weights (and their derived bf16 / transposed /
+        fp8 copies), Adam moments and step, dropout counter, metric
+        accumulators, fp8 scales."""
+        for t, v in zip(self._state(), st):
+            t.copy_(v)
+        self.model.store.refresh_compute()
+        if self.fp8 is not None:
+            self.fp8.weights.refresh()  # e4m3 copies with the restored scales
+            self.fp8.meta.amax.copy_(st[-1])
 
     def eager(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         self.model.loss_and_backward(src, tgt, self.rt, self.workers, accum=self.accum,
@@ -100,37 +153,79 @@ class TrainStep:
         return self.last
 
     # ------------------------------------------------------------------ HIP graph
-    def capture(self, src: torch.Tensor, tgt: torch.Tensor, warmup: int = 2) -> None:
-        """Capture the whole step (fwd+bwd+optimizer) into one HIP graph on
-        static input buffers. Warm-up iterations run on a side stream first so
-        lazily-allocated workspaces exist before capture."""
+    def capture(self, src: torch.Tensor, tgt: torch.Tensor, warmup: int = 2) -> bool:
+        """Capture the whole step (fwd+bwd+optimizer) on static input buffers:
+        one HIP graph on a single GPU; under data parallelism a segmented
+        graph whose collectives are eager calls between the segments (or, with
+        TDG_DP_GRAPH=full, one graph with the collectives inside).
+
+        Warm-up steps run first (lazily-allocated workspaces, GEMM tunings,
+        communication buffers); the training state is snapshotted before and
+        restored after them, so capture() itself trains nothing: after it the
+        model, optimizer and counters are exactly as they were. Returns False
+        (and leaves the step eager) when the data-parallel step is configured
+        not to be captured."""
+        mode = self.capture_mode()
+        if mode == "0":
+            return False
         self._static = (src.clone(), tgt.clone())
+        saved = self.snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.eager(*self._static)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        if self.ddp is not None and self.ddp.active:
-            # collectives inside the graph (experimental, TDG_DP_GRAPH=1): no
-            # collective of the warm-up may still be pending in the process
-            # group's watchdog, and the watchdog's event queries from its own
-            # thread must not invalidate this thread's capture
+        self.restore(saved)
+        del saved
+        if mode != "single":
+            # no collective of the warm-up may still be pending in the process
+            # group's watchdog when the capture starts
             torch.cuda.synchronize()
             dist.barrier(group=self.ddp.group)
             torch.cuda.synchronize()
+        if mode == "seg":
+            prepare_capture()
+            cap = torch.cuda.Stream()
+            cap.wait_stream(torch.cuda.current_stream())
+            rec = SegmentedGraph(cap)
+            self.ddp.recorder = rec
+            try:
+                with torch.cuda.stream(cap):
+                    rec.begin()
+                    self.eager(*self._static)
+                    rec.end()
+            except BaseException:
+                rec.abort()
+                raise
+            finally:
+                self.ddp.recorder = None
+            torch.cuda.current_stream().wait_stream(cap)
+            self.segments = rec
+            return True
+        g = torch.cuda.CUDAGraph()
+        if mode == "full":
+            # the watchdog's event queries from its own thread must not
+            # invalidate this thread's capture
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.eager(*self._static)
         else:
             with torch.cuda.graph(g):
                 self.eager(*self._static)
         self.graph = g
+        return True
 
     def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
-        if self.graph is None:
+        if not self.captured:
             return self.eager(src, tgt)
+        if src.shape != self._static[0].shape or tgt.shape != self._static[1].shape:
+            raise ValueError(f"captured step takes {tuple(self._static[0].shape)} / "
+                             f"{tuple(self._static[1].shape)} batches, got {tuple(src.shape)} / "
+                             f"{tuple(tgt.shape)}")
         self._static[0].copy_(src, non_blocking=True)
         self._static[1].copy_(tgt, non_blocking=True)
-        self.graph.replay()
+        if self.segments is not None:
+            self.segments.replay()
+        else:
+            self.graph.replay()
         return self.last

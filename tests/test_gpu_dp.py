@@ -5,7 +5,10 @@ production path: HIP kernels, deferred weight gradients launched in waves at
 layer ends (a small wave forces problems to be cut across launches), the
 frontier all-reduce spans, Adam. The update must match one process that runs
 both ranks' batches with the reference's loss scaling (per-replica token mean
-/ workers, SUM-reduced gradients), and the replicas must stay bitwise equal."""
+/ workers, SUM-reduced gradients), and the replicas must stay bitwise equal.
+The "seg" cases run the step as the segmented HIP graph the multi-GPU bench
+uses (train/graphs.py: graph segments with the collectives issued eagerly
+between them), captured on the first batch and replayed on every step."""
 import os
 import socket
 
@@ -37,10 +40,11 @@ def _batch(rank, i):
     return src, tgt
 
 
-def _worker(rank, world, port, out, opt_mode, loss_mode):
+def _worker(rank, world, port, out, opt_mode, loss_mode, graph):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
-                      TDG_DP_WAVE_TILES="37", TDG_DP_OVERLAP_OPT=opt_mode)
+                      TDG_DP_WAVE_TILES="37", TDG_DP_OVERLAP_OPT=opt_mode,
+                      TDG_DP_GRAPH=graph or "0")
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
@@ -57,21 +61,29 @@ def _worker(rank, world, port, out, opt_mode, loss_mode):
     step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
     assert step.global_mean == (loss_mode == "global_mean")
     assert step.rt.wgrad is not None and step.rt.wgrad.wave_tiles == 37
+    if graph:
+        src, tgt = _batch(rank, 0)
+        assert step.capture(src.to(info.device), tgt.to(info.device))  # trains nothing
+        assert step.segments is not None and step.segments.num_calls >= 2
+        assert opt.iterations == 0
     losses = []
     for i in range(STEPS):
         src, tgt = _batch(rank, i)
         losses.append(step(src.to(info.device), tgt.to(info.device)).clone().cpu())
         ddp.verify_replicas()
     torch.cuda.synchronize()
+    assert opt.iterations == STEPS
     torch.save({"flat": m.store.flat.cpu(), "loss": torch.stack(losses), "nb": len(ddp.last_buckets)},
                f"{out}.{rank}")
     tdist.barrier()
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("opt_mode,loss_mode", [("0", "replica_mean"), ("tail", "replica_mean"),
-                                                ("tail", "global_mean")])
-def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode, monkeypatch):
+@pytest.mark.parametrize("opt_mode,loss_mode,graph", [("0", "replica_mean", ""), ("tail", "replica_mean", ""),
+                                                      ("tail", "global_mean", ""),
+                                                      ("tail", "replica_mean", "seg"),
+                                                      ("0", "global_mean", "seg")])
+def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode, graph, monkeypatch):
     from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
@@ -79,7 +91,8 @@ def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode,
 
     world = 2
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode, graph), nprocs=world,
+                       join=True,
                        start_method="spawn")
     r0 = torch.load(out + ".0", weights_only=True)
     r1 = torch.load(out + ".1", weights_only=True)

@@ -1,13 +1,14 @@
 """HIP-graph replay of the whole training step equals the eager step.
 
-One GPU: TrainStep.capture() runs its warm-up steps eagerly, then captures
-one step; replays on new batches must leave exactly the weights that the
-same number of eager steps leave (dropout counter, Adam step and fp8 scales
-all live on the device). Data parallel (single-rank RCCL communicator,
---force-dp): the step with its all-reduce spans and per-span Adam captured
-in one graph (thread-local capture mode) -- the experimental path the
-multi-GPU step could take (ROADMAP item 5); the 8-GPU RCCL replay itself is
-not testable on one GPU."""
+One GPU: TrainStep.capture() runs warm-up steps eagerly, restores the state
+they changed, then captures one step; replays must leave exactly the weights
+that the same number of eager steps leave (dropout counter, Adam step and
+fp8 scales all live on the device), and capture() itself trains nothing
+(opt.iterations counts the replayed steps only). Data parallel (single-rank
+RCCL communicator, --force-dp): the segmented graph (collectives issued
+eagerly between graph segments, the default multi-GPU step) and the single
+graph with the collectives captured inside (TDG_DP_GRAPH=full); the 8-GPU
+RCCL replay itself is not testable on one GPU."""
 import os
 import socket
 
@@ -40,7 +41,7 @@ def _batches(dev):
     return out
 
 
-def _run(dev, graph, ddp_factory=None):
+def _run(dev, graph, ddp_factory=None, fp8=False):
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.train.optim import Adam
@@ -51,17 +52,20 @@ def _run(dev, graph, ddp_factory=None):
     m = Transformer(cfg).build(dev, seed=3)
     opt = Adam(m.store, cfg.d_model, lr=0.003)
     ddp = ddp_factory(m) if ddp_factory else None
-    step = TrainStep(m, opt, ddp, workers=1, seed=11)
+    fp8_state = None
+    if fp8:
+        from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
+        fp8_state = Fp8State(m)
+    step = TrainStep(m, opt, ddp, workers=1, seed=11, fp8_state=fp8_state)
     bs = _batches(dev)
     losses = []
     if graph:
-        step.capture(*bs[0], warmup=2)  # two eager steps on batch 0
-    else:
-        for _ in range(2):
-            step(*bs[0])
-    for i in range(1, STEPS + 1):
+        assert step.capture(*bs[0], warmup=2)  # warm-up steps are rolled back
+        assert opt.iterations == 0 and int(step.rt.ctr.item()) == 0
+    for i in range(STEPS + 1):
         losses.append(step(*bs[i]).clone())
     torch.cuda.synchronize()
+    assert opt.iterations == STEPS + 1
     return m.store.flat.cpu(), torch.stack(losses).cpu(), step
 
 
@@ -74,9 +78,17 @@ def test_graph_replay_matches_eager_one_gpu():
     assert torch.equal(f_e, f_g)
 
 
-def _dp_worker(rank, port, out):
+def test_graph_replay_matches_eager_fp8():
+    f_e, l_e, _ = _run("cuda", graph=False, fp8=True)
+    f_g, l_g, st = _run("cuda", graph=True, fp8=True)
+    assert st.graph is not None
+    assert torch.equal(l_e, l_g), (l_e, l_g)
+    assert torch.equal(f_e, f_g)
+
+
+def _dp_worker(rank, port, out, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
-                      LOCAL_RANK="0")
+                      LOCAL_RANK="0", TDG_DP_GRAPH=mode)
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 
@@ -91,15 +103,22 @@ def _dp_worker(rank, port, out):
     for graph in (False, True):
         f, l, st = _run(info.device, graph, mk)
         assert st.ddp is not None and st.ddp.active and len(st.ddp.last_buckets) > 1
+        if graph and mode == "seg":
+            assert st.segments is not None and st.graph is None
+            # one issue per span + two wait points (backward's spans, the last span)
+            assert st.segments.num_calls == len(st.ddp.last_buckets) + 2, st.segments.items
+        elif graph:
+            assert st.graph is not None and st.segments is None
         res["graph" if graph else "eager"] = (f, l)
     torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1]},
                out)
     tdist.shutdown()
 
 
-def test_dp_step_graph_with_collectives_matches_eager(tmp_path):
+@pytest.mark.parametrize("mode", ["seg", "full"])
+def test_dp_step_graph_matches_eager(tmp_path, mode):
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_dp_worker, args=(_port(), out), nprocs=1, join=True, start_method="spawn")
+    mp.start_processes(_dp_worker, args=(_port(), out, mode), nprocs=1, join=True, start_method="spawn")
     r = torch.load(out, weights_only=True)
     assert torch.equal(r["el"], r["gl"]), (r["el"], r["gl"])
     assert torch.equal(r["ef"], r["gf"])

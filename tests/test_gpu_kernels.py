@@ -448,6 +448,17 @@ def test_prep_batch(dtype):
     assert torch.equal(tl.cpu(), (tgt[:, :-1] != 0).sum(1).to(torch.int32))
     assert ntok.item() == float((tgt[:, 1:] != 0).sum())
     assert ctr.item() == 42
+    assert kk.interior_pad_rows(reset=True) == 0  # right-padded only
+    # a PAD inside a source row and one inside a target-input row are counted
+    src[3, 2] = 0
+    src[3, 5] = 7
+    tgt[9, 1] = 0
+    tgt[9, 4] = 7
+    kk.prep_batch(src.to(DEV), tgt.to(DEV), ctr)
+    assert kk.interior_pad_rows() == 2
+    with pytest.raises(ValueError, match="right-padded"):
+        kk.check_trailing_padding()
+    assert kk.interior_pad_rows() == 0  # reset by the check
 
 
 @pytest.mark.parametrize("M,K", [(300, 512), (8192, 512), (1000, 2048)])

@@ -86,3 +86,17 @@ def test_dropout_is_deterministic_and_scaled():
     assert not torch.allclose(a, c)
     e = m.logits(src, tgt[:, :-1], RunCtx(training=False))
     assert not torch.allclose(a, e)
+
+
+def test_interior_pad_rejected():
+    """Keys are masked by length (trailing padding); a PAD before a non-PAD
+    token, which the reference would mask position by position
+    (transformer_model.py:56-62), is an error rather than a silent mismatch."""
+    import pytest
+    from tensorflow_distributed_on_gke_amd.models.transformer import seq_lengths
+
+    ok = torch.tensor([[5, 6, 7, 0, 0], [5, 0, 0, 0, 0], [0, 0, 0, 0, 0]])
+    assert seq_lengths(ok).tolist() == [3, 1, 0]
+    bad = torch.tensor([[5, 0, 7, 0, 0]])
+    with pytest.raises(ValueError, match="right-padded"):
+        seq_lengths(bad)

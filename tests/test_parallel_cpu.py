@@ -257,3 +257,61 @@ def test_train_cli_fault_injection_and_resume(tmp_path):
     snaps = tmp_path / "snapshots" / "kubernetes-transformer-training"
     assert (snaps / "training-snapshots" / "initial_model" / "variables" / "variables.index").exists()
     assert (snaps / "training-snapshots_2" / "weights_snapshot_2" / "model_weights.index").exists()
+
+
+def test_segmented_capture_defers_collectives(monkeypatch):
+    """While a step is captured as a segmented graph (train/graphs.py) the
+    data-parallel code must not issue any collective: each all-reduce and the
+    two tail wait points become recorded host calls, which issue / wait in
+    order when replayed."""
+    import torch.distributed as tdist
+
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=0)
+    order = sorted(m.store.params, key=lambda p: p.offset)
+    dp = DataParallel(m.store, bucket_mb=0.05, min_mb=0.001)
+    dp.active = True
+    m.store.clear_grad_hooks()
+    m.store.on_grad_ready(dp._on_ready)
+    m.store.on_grad_sync(dp._on_sync)
+    issued = []
+
+    class _Work:
+        def __init__(self, t):
+            self.t, self.waited = t, False
+
+        def wait(self):
+            self.waited = True
+
+    def fake_all_reduce(t, group=None, async_op=False):
+        issued.append(_Work(t))
+        return issued[-1]
+
+    monkeypatch.setattr(tdist, "all_reduce", fake_all_reduce)
+
+    class _Rec:
+        def __init__(self):
+            self.calls = []
+
+        def cut(self, fn):
+            self.calls.append(fn)
+
+    rec = _Rec()
+    dp.recorder = rec
+    for p in order:
+        m.store.grad_ready(p)
+    dp.finish()
+    dp.recorder = None
+    spans = [(b.start, b.end) for b in dp.last_buckets]
+    assert len(spans) > 2 and issued == []
+    assert len(rec.calls) == len(spans) + 2  # one issue per span, two wait points
+    for fn in rec.calls:  # "replay"
+        fn()
+    assert [(w.t.data_ptr() - m.store.flat_grad.data_ptr()) // 4 for w in issued] == [s for s, _ in spans]
+    assert all(w.waited for w in issued)
+    # eager (no recorder): issued immediately, waited in finish
+    issued.clear()
+    for p in order:
+        m.store.grad_ready(p)
+    assert len(issued) == len(spans) - 1  # the last span is launched by finish()
+    dp.finish()
+    assert len(issued) == len(spans) and all(w.waited for w in issued)
