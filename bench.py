@@ -93,8 +93,8 @@ def main() -> None:
 
     # HIP graph by default. One GPU: the whole step is one graph. Data
     # parallel: a chain of graphs cut at the RCCL collectives, which stay
-    # eager calls between the segments (train/graphs.py; TDG_DP_GRAPH=full
-    # captures them inside one graph, TDG_DP_GRAPH=0 runs the step eagerly)
+    # eager calls between the segments (train/graphs.py; TDG_DP_GRAPH=0 runs
+    # the step eagerly)
     use_graph = args.graph if args.graph >= 0 else int(dev.type == "cuda")
     if use_graph:
         use_graph = int(step.capture(*batches[0]))
@@ -155,7 +155,7 @@ def main() -> None:
                 "local_batch": args.local_batch,
                 "seq_len": S,
                 "parallelism": f"dp{world}",
-                "hip_graph": (("segmented" if step.segments is not None else "full")
+                "hip_graph": (("segmented" if step.segments is not None else "single")
                               if use_graph else False),
                 "grad_comm": args.grad_comm,
                 "defer_wgrad": step.rt.wgrad is not None,

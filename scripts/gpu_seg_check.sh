@@ -1,7 +1,7 @@
 #!/bin/bash
 # Segmented data-parallel graph + round-2 fixes: targeted GPU tests, smoke,
 # then the bench single-GPU graph vs the data-parallel path (single RCCL rank)
-# as segmented graph / full graph / eager.
+# as segmented graph / eager.
 set -uo pipefail
 O=gpurun_out/seg
 mkdir -p $O
@@ -15,5 +15,3 @@ for v in "graph:" "dp_seg:--force-dp 1" "dp_eager:--force-dp 1 --graph 0" "dp_se
   timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 $a > $O/bench_$n.log 2>&1 || { tail -30 $O/bench_$n.log; exit 1; }
   echo "$n $(tail -1 $O/bench_$n.log)"
 done
-TDG_DP_GRAPH=full timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --force-dp 1 > $O/bench_dp_full.log 2>&1 || { tail -30 $O/bench_dp_full.log; exit 1; }
-echo "dp_full $(tail -1 $O/bench_dp_full.log)"

@@ -38,11 +38,10 @@ ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 # how a data-parallel step is captured (TrainStep.capture):
 #   "seg"  -- chain of HIP graphs cut at the collectives, which stay eager
 #             RCCL calls between the segments (train/graphs.py; default)
-#   "full" -- one graph with the collectives captured inside it
 #   "0"    -- no capture: the data-parallel step runs eagerly
+# (round 1 also had "full", the collectives captured inside one graph; it
+# failed capture under PyTorch 2.10's process-group watchdog and was removed)
 DP_GRAPH = os.environ.get("TDG_DP_GRAPH", "seg")
-if DP_GRAPH == "1":  # round-1 spelling of "full"
-    DP_GRAPH = "full"
 
 
 class TrainStep:
@@ -101,13 +100,13 @@ class TrainStep:
         return self.graph is not None or self.segments is not None
 
     def capture_mode(self) -> str:
-        """"single" (one graph, no collectives), "seg", "full" or "0" (the
+        """"single" (one graph, no collectives), "seg" or "0" (the
         data-parallel step stays eager)."""
         if self.ddp is None or not self.ddp.active:
             return "single"
-        if DP_GRAPH not in ("seg", "full", "0"):
-            raise ValueError(f"TDG_DP_GRAPH must be seg, full or 0, got {DP_GRAPH!r}")
-        if DP_GRAPH == "seg" and (self.ddp._upd_stream is not None or streams.ENABLED):
+        if DP_GRAPH not in ("seg", "0"):
+            raise ValueError(f"TDG_DP_GRAPH must be seg or 0, got {DP_GRAPH!r}")
+        if self.ddp._upd_stream is not None or streams.ENABLED:
             # mid-backward Adam on its own stream / the weight-gradient side
             # stream would leave unjoined work at a cut
             return "0"
@@ -156,8 +155,7 @@ class TrainStep:
     def capture(self, src: torch.Tensor, tgt: torch.Tensor, warmup: int = 2) -> bool:
         """Capture the whole step (fwd+bwd+optimizer) on static input buffers:
         one HIP graph on a single GPU; under data parallelism a segmented
-        graph whose collectives are eager calls between the segments (or, with
-        TDG_DP_GRAPH=full, one graph with the collectives inside).
+        graph whose collectives are eager calls between the segments.
 
         Warm-up steps run first (lazily-allocated workspaces, GEMM tunings,
         communication buffers); the training state is snapshotted before and
@@ -204,14 +202,8 @@ class TrainStep:
             self.segments = rec
             return True
         g = torch.cuda.CUDAGraph()
-        if mode == "full":
-            # the watchdog's event queries from its own thread must not
-            # invalidate this thread's capture
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                self.eager(*self._static)
-        else:
-            with torch.cuda.graph(g):
-                self.eager(*self._static)
+        with torch.cuda.graph(g):
+            self.eager(*self._static)
         self.graph = g
         return True
 

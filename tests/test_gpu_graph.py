@@ -6,9 +6,8 @@ that the same number of eager steps leave (dropout counter, Adam step and
 fp8 scales all live on the device), and capture() itself trains nothing
 (opt.iterations counts the replayed steps only). Data parallel (single-rank
 RCCL communicator, --force-dp): the segmented graph (collectives issued
-eagerly between graph segments, the default multi-GPU step) and the single
-graph with the collectives captured inside (TDG_DP_GRAPH=full); the 8-GPU
-RCCL replay itself is not testable on one GPU."""
+eagerly between graph segments, the default multi-GPU step); the 8-GPU RCCL
+replay itself is not testable on one GPU."""
 import os
 import socket
 
@@ -103,19 +102,17 @@ def _dp_worker(rank, port, out, mode):
     for graph in (False, True):
         f, l, st = _run(info.device, graph, mk)
         assert st.ddp is not None and st.ddp.active and len(st.ddp.last_buckets) > 1
-        if graph and mode == "seg":
+        if graph:
             assert st.segments is not None and st.graph is None
             # one issue per span + two wait points (backward's spans, the last span)
             assert st.segments.num_calls == len(st.ddp.last_buckets) + 2, st.segments.items
-        elif graph:
-            assert st.graph is not None and st.segments is None
         res["graph" if graph else "eager"] = (f, l)
     torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1]},
                out)
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("mode", ["seg", "full"])
+@pytest.mark.parametrize("mode", ["seg"])
 def test_dp_step_graph_matches_eager(tmp_path, mode):
     out = str(tmp_path / "dp.pt")
     mp.start_processes(_dp_worker, args=(_port(), out, mode), nprocs=1, join=True, start_method="spawn")
