@@ -4,6 +4,8 @@
 #pragma once
 #include "tdg_common.h"
 
+#include <type_traits>
+
 namespace tdg {
 
 constexpr int BK = 64;
@@ -112,6 +114,15 @@ struct Glds {
   }
 };
 
+// Epilogue stores write-through (sc1) by default: measured 8192x2048x512
+// 25.1 -> 22.8 us, 8192x512x512 10.3 -> 10.0 us (csrc/lab/gemm_lab.cpp): the
+// output lines are not left dirty in the XCD L2 for the kernel-end write-back,
+// and the consumer kernel runs on other XCDs anyway.
+#ifndef TDG_EPI_SC1
+#define TDG_EPI_SC1 1
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
 #ifndef TDG_GEMM_PRIO
 #define TDG_GEMM_PRIO 1
 #endif
@@ -156,6 +167,261 @@ template <bool KC>
 constexpr int frag_ops() {
   return KC ? 1 : 2;
 }
+
+// ---------------------------------------------------------------- epilogue
+// The GEMM kernels issue their MFMAs with the operands swapped
+// (mfma16(b_frag, a_frag)), so every 16x16 accumulator holds the TRANSPOSED
+// sub-tile: lane l has C[m = base_m + (l & 15)][n = base_n + 4 (l >> 4) + r],
+// r = 0..3 -- four consecutive output columns of one row: one 8-byte (bf16)
+// or 16-byte (f32) LDS write per sub-tile in the epilogue image (EpiLds
+// below; the untransposed layout needed one 2-byte write per element), or --
+// epi_store4, the simple fallback -- a direct store from registers.
+enum Epi : int {
+  EPI_NONE = 0,       // alpha*acc (+beta*C)
+  EPI_BIAS = 1,       // alpha*acc + bias[n]
+  EPI_BIAS_RELU = 2,  // relu(alpha*acc + bias[n])
+  EPI_DRELU = 3,      // alpha*acc * (aux[m,n] > 0)      (ReLU backward fused in dgrad)
+};
+
+// 4 bias values of columns n..n+3 (clamped to N-1 past the edge).
+template <int EPI>
+__device__ __forceinline__ f32x4 load_bias4(const float* __restrict__ bias, int n, int N) {
+  f32x4 b = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+    if (n + 4 <= N && (reinterpret_cast<uintptr_t>(bias + n) & 15) == 0) {
+      b = *reinterpret_cast<const f32x4*>(bias + n);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b[r] = bias[min(n + r, N - 1)];
+    }
+  }
+  return b;
+}
+
+// Whether the 4-wide vector path is legal for this launch (alignment of C,
+// its row stride and the ReLU-mask operand).
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ bool epi_vec_ok(const void* C, int ldc, const bf16_t* aux, int ldaux) {
+  constexpr int ES = OUT_F32 ? 4 : 2;
+  bool ok = (ldc % 4) == 0 && (reinterpret_cast<uintptr_t>(C) % (4 * ES)) == 0;
+  if constexpr (EPI == EPI_DRELU) ok = ok && (ldaux % 4) == 0 && (reinterpret_cast<uintptr_t>(aux) & 7) == 0;
+  return ok;
+}
+
+// Store C[m][n..n+3] = epilogue(alpha * a) (+ beta * C_old).
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void epi_store4(void* __restrict__ Cv, int ldc, int M, int N, int m, int n,
+                                           const f32x4& a, float alpha, float beta, const f32x4& bn,
+                                           const bf16_t* __restrict__ aux, int ldaux, bool vec) {
+  if (m >= M || n >= N) return;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = alpha * a[r];
+    if constexpr (EPI == EPI_BIAS) v[r] += bn[r];
+    if constexpr (EPI == EPI_BIAS_RELU) v[r] = fmaxf(v[r] + bn[r], 0.f);
+  }
+  const size_t off = (size_t)m * ldc + n;
+  if (vec && n + 4 <= N) {
+    if constexpr (EPI == EPI_DRELU) {
+      const short4_t x = *reinterpret_cast<const short4_t*>(aux + (size_t)m * ldaux + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(bf2f((bf16_t)x[r]) > 0.f)) v[r] = 0.f;
+    }
+    if constexpr (OUT_F32) {
+      f32x4* cp = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + off);
+      f32x4 o = {v[0], v[1], v[2], v[3]};
+      if (beta != 0.f) o += beta * *cp;
+      *cp = o;
+    } else {
+      short4_t* cp = reinterpret_cast<short4_t*>(reinterpret_cast<bf16_t*>(Cv) + off);
+      if (beta != 0.f) {
+        const short4_t old = *cp;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += beta * bf2f((bf16_t)old[r]);
+      }
+      short4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+      *cp = o;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= N) break;
+      float x = v[r];
+      if constexpr (EPI == EPI_DRELU) {
+        if (!(bf2f(aux[(size_t)m * ldaux + n + r]) > 0.f)) x = 0.f;
+      }
+      if constexpr (OUT_F32) {
+        float* cp = reinterpret_cast<float*>(Cv) + off + r;
+        if (beta != 0.f) x += beta * *cp;
+        *cp = x;
+      } else {
+        bf16_t* cp = reinterpret_cast<bf16_t*>(Cv) + off + r;
+        if (beta != 0.f) x += beta * bf2f(*cp);
+        *cp = f2bf(x);
+      }
+    }
+  }
+}
+
+// Epilogue through a per-wave LDS image (what the kernels use). The direct
+// store above writes 16 rows x 8-16 bytes per wave instruction; measured on
+// MI355X (csrc/lab/gemm_lab.cpp stamps) that store stream is issue-bound at
+// ~20-35 GB/s per CU -- 3.7 us for a 256x256 bf16 tile. Here each lane's 4
+// consecutive columns go to a padded row-major image as ONE 8-byte (bf16) or
+// 16-byte (f32) LDS write, are read back as 16-byte row chunks, and leave as
+// fully coalesced 16-byte stores (8 lanes per 128-byte row for bf16).
+// RPASS rows of the wave tile per pass (the image is reused across passes);
+// pre_aux / pre_c: optional epilogue operands prefetched in the chunk layout
+// (one int4 per lane per chunk iteration), single-pass only.
+template <int EPI, bool OUT_F32, int TM, int TN, int RPASS>
+struct EpiLds {
+  static constexpr int ES = OUT_F32 ? 4 : 2;
+  static constexpr int SP = TN * 16 * ES + 16;  // padded image row (bytes)
+  static constexpr int CPR = TN * 16 * ES / 16;  // 16-byte chunks per row
+  static constexpr int EPC = 16 / ES;            // elements per chunk
+  static constexpr int ITER = RPASS * CPR / 64;  // chunk iterations per lane per pass
+  static constexpr int BYTES = RPASS * SP;       // image bytes per wave
+  static_assert(RPASS % 16 == 0 && (TM * 16) % RPASS == 0, "passes of whole 16-row sub-tiles");
+  static_assert((RPASS * CPR) % 64 == 0, "whole chunk iterations");
+
+  // m_of / n_of: row / column of chunk iteration t (pass 0) -- for prefetch.
+  __device__ static __forceinline__ int row_of(int lane, int t) { return (lane + 64 * t) / CPR; }
+  __device__ static __forceinline__ int col_of(int lane, int t) { return ((lane + 64 * t) % CPR) * EPC; }
+
+  __device__ static __forceinline__ void run(char* wimg, const f32x4 (&acc)[TM][TN], int lane,
+                                             void* __restrict__ Cv, int ldc, int M, int N, int mw0,
+                                             int nw0, float alpha, float beta,
+                                             const float* __restrict__ bias,
+                                             const bf16_t* __restrict__ aux, int ldaux, bool vec) {
+    int4 none[ITER];
+    run_pre<false>(wimg, acc, lane, Cv, ldc, M, N, mw0, nw0, alpha, beta, bias, aux, ldaux, vec,
+                   none, false, none, false);
+  }
+  // With operands prefetched in the chunk layout (arrays indexed by constants
+  // only after unrolling: no private-memory copies).
+  template <bool PRE>
+  __device__ static __forceinline__ void run_pre(char* wimg, const f32x4 (&acc)[TM][TN], int lane,
+                                                 void* __restrict__ Cv, int ldc, int M, int N,
+                                                 int mw0, int nw0, float alpha, float beta,
+                                                 const float* __restrict__ bias,
+                                                 const bf16_t* __restrict__ aux, int ldaux, bool vec,
+                                                 const int4 (&pre_aux)[ITER], bool use_aux,
+                                                 const int4 (&pre_c)[ITER], bool use_c) {
+    const int g = lane >> 4, r16 = lane & 15;
+    // 16-byte chunk path: C rows 16-byte aligned, the ReLU mask likewise
+    bool vok = vec && ((ldc * ES) % 16) == 0 && (reinterpret_cast<uintptr_t>(Cv) & 15) == 0;
+    if constexpr (EPI == EPI_DRELU)
+      vok = vok && (ldaux % EPC) == 0 && (reinterpret_cast<uintptr_t>(aux) % (2 * EPC)) == 0;
+#if TDG_EPI_SC1
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        Cv, 0, (int)min((size_t)0x7fffffff, ((size_t)(M - 1) * ldc + N) * ES), 0x00020000);
+#endif
+    f32x4 bn[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bn[j] = load_bias4<EPI>(bias, nw0 + 16 * j + 4 * g, N);
+#pragma unroll
+    for (int p = 0; p < TM * 16 / RPASS; ++p) {
+      // 1) accumulators (alpha, bias, relu applied) -> image
+#pragma unroll
+      for (int ii = 0; ii < RPASS / 16; ++ii) {
+        const int i = p * (RPASS / 16) + ii;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = alpha * acc[i][j][r];
+            if constexpr (EPI == EPI_BIAS) v[r] += bn[j][r];
+            if constexpr (EPI == EPI_BIAS_RELU) v[r] = fmaxf(v[r] + bn[j][r], 0.f);
+          }
+          char* dst = wimg + (16 * ii + r16) * SP + (16 * j + 4 * g) * ES;
+          if constexpr (OUT_F32) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            short4_t w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = (short)f2bf(v[r]);
+            *reinterpret_cast<short4_t*>(dst) = w;
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local image complete
+      // 2) image -> 16-byte row chunks -> global
+#pragma unroll
+      for (int t = 0; t < ITER; ++t) {
+        const int id = lane + 64 * t;
+        const int row = id / CPR, ch = id % CPR;
+        const int m = mw0 + p * RPASS + row;
+        const int n = nw0 + ch * EPC;
+        // vector types only (a reinterpret_cast of a local array would put
+        // it in private memory)
+        using VecT = typename std::conditional<OUT_F32, f32x4, short8_t>::type;
+        VecT vals = *reinterpret_cast<const VecT*>(wimg + row * SP + ch * 16);
+        if (m >= M || n >= N) continue;
+        char* cp = reinterpret_cast<char*>(Cv) + ((size_t)m * ldc + n) * ES;
+        if (vok && n + EPC <= N) {
+          if constexpr (EPI == EPI_DRELU) {
+            if constexpr (EPC == 8) {
+              const short8_t x = (PRE && use_aux)
+                                     ? __builtin_bit_cast(short8_t, pre_aux[t])
+                                     : *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (!(bf2f((bf16_t)x[e]) > 0.f)) vals[e] = 0;
+            } else {
+              const short4_t x = *reinterpret_cast<const short4_t*>(aux + (size_t)m * ldaux + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (!(bf2f((bf16_t)x[e]) > 0.f)) vals[e] = 0;
+            }
+          }
+          if (beta != 0.f) {
+            const VecT old = (PRE && use_c) ? __builtin_bit_cast(VecT, pre_c[t])
+                                            : *reinterpret_cast<const VecT*>(cp);
+            if constexpr (OUT_F32) {
+              vals += beta * old;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                vals[e] = (short)f2bf(bf2f((bf16_t)vals[e]) + beta * bf2f((bf16_t)old[e]));
+            }
+          }
+#if TDG_EPI_SC1
+          // write-through (sc1): nothing left dirty in the XCD's L2 for the
+          // end-of-kernel write-back
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, vals), crs,
+                                                 (int)(cp - reinterpret_cast<char*>(Cv)), 0, 16);
+#else
+          *reinterpret_cast<VecT*>(cp) = vals;
+#endif
+        } else {
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            if (n + e >= N) break;
+            float v = OUT_F32 ? (float)vals[e] : bf2f((bf16_t)vals[e]);
+            if constexpr (EPI == EPI_DRELU) {
+              if (!(bf2f(aux[(size_t)m * ldaux + n + e]) > 0.f)) v = 0.f;
+            }
+            if constexpr (OUT_F32) {
+              float* c = reinterpret_cast<float*>(cp) + e;
+              if (beta != 0.f) v += beta * *c;
+              *c = v;
+            } else {
+              bf16_t* c = reinterpret_cast<bf16_t*>(cp) + e;
+              if (beta != 0.f) v += beta * bf2f(*c);
+              *c = f2bf(v);
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before the next pass
+    }
+  }
+};
 
 // Fragments read with lds_read_tr_async are not tracked by the compiler:
 // make every later use wait for them (see tdg_common.h).

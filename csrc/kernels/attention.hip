@@ -44,22 +44,46 @@ struct ATile {
     const int seg = (byte >> 5) ^ ((row / RPB) & (SEGS - 1));
     return row * RB + (seg << 5) + (byte & 31);
   }
-  // Stage 64 rows (row0..row0+63, rows >= nrows zero) of a [L, ...] tensor.
+  // Stage 64 rows (row0..row0+63, rows >= nrows zero) of a [L, ...] tensor,
+  // in two halves so that callers can issue the global loads of several
+  // tiles before the first LDS write (one memory latency, not one per tile).
+  template <int NT = 256>
+  struct Chunks {
+    static constexpr int CPR = HD / 8;
+    static constexpr int TOTAL = 64 * CPR;
+    static constexpr int NI = (TOTAL + NT - 1) / NT;
+    short8_t v[NI];
+  };
+  template <int NT = 256>
+  __device__ static __forceinline__ void fetch(Chunks<NT>& c, const bf16_t* __restrict__ base,
+                                               long long sl, int row0, int nrows, int tid) {
+    using C = Chunks<NT>;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) {
+      const int id = tid + i * NT;
+      const int row = id / C::CPR, cc = id % C::CPR;
+      c.v[i] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if ((C::TOTAL % NT == 0 || id < C::TOTAL) && row0 + row < nrows)
+        c.v[i] = *reinterpret_cast<const short8_t*>(base + (long long)(row0 + row) * sl + cc * 8);
+    }
+  }
+  template <int NT = 256>
+  __device__ static __forceinline__ void put(char* lds, const Chunks<NT>& c, int tid) {
+    using C = Chunks<NT>;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) {
+      const int id = tid + i * NT;
+      if (C::TOTAL % NT != 0 && id >= C::TOTAL) break;
+      const int row = id / C::CPR, cc = id % C::CPR;
+      *reinterpret_cast<short8_t*>(lds + off(row, cc * 16)) = c.v[i];
+    }
+  }
   template <int NT = 256>
   __device__ static __forceinline__ void load(char* lds, const bf16_t* __restrict__ base,
                                               long long sl, int row0, int nrows, int tid) {
-    constexpr int CPR = HD / 8;
-    constexpr int TOTAL = 64 * CPR;
-#pragma unroll
-    for (int i = 0; i < (TOTAL + NT - 1) / NT; ++i) {
-      const int id = tid + i * NT;
-      if (TOTAL % NT != 0 && id >= TOTAL) break;
-      const int row = id / CPR, c = id % CPR;
-      short8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (row0 + row < nrows)
-        v = *reinterpret_cast<const short8_t*>(base + (long long)(row0 + row) * sl + c * 8);
-      *reinterpret_cast<short8_t*>(lds + off(row, c * 16)) = v;
-    }
+    Chunks<NT> c;
+    fetch<NT>(c, base, sl, row0, nrows, tid);
+    put<NT>(lds, c, tid);
   }
   // Row fragment: lane holds X[rbase + (lane&15)][32s + 8(lane>>4) + j]
   __device__ static __forceinline__ short8_t frag_row(const char* lds, int rbase, int s, int lane) {
@@ -134,10 +158,19 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
 
   for (int k0 = 0; k0 < klim; k0 += KT) {
+    {
+      // every K / V load of the tile in flight before the first LDS write
+      typename T::template Chunks<NWV * 64> ck[KT / 64], cv[KT / 64];
 #pragma unroll
-    for (int h64 = 0; h64 < KT / 64; ++h64) {
-      T::template load<NWV * 64>(ldsK + h64 * T::BYTES, kb, a.k_sl, k0 + 64 * h64, a.Lk, tid);
-      T::template load<NWV * 64>(ldsV + h64 * T::BYTES, vb, a.v_sl, k0 + 64 * h64, a.Lk, tid);
+      for (int h64 = 0; h64 < KT / 64; ++h64) {
+        T::template fetch<NWV * 64>(ck[h64], kb, a.k_sl, k0 + 64 * h64, a.Lk, tid);
+        T::template fetch<NWV * 64>(cv[h64], vb, a.v_sl, k0 + 64 * h64, a.Lk, tid);
+      }
+#pragma unroll
+      for (int h64 = 0; h64 < KT / 64; ++h64) {
+        T::template put<NWV * 64>(ldsK + h64 * T::BYTES, ck[h64], tid);
+        T::template put<NWV * 64>(ldsV + h64 * T::BYTES, cv[h64], tid);
+      }
     }
     __syncthreads();
     f32x4 s[NT16];

@@ -29,12 +29,23 @@
 
 namespace tdg {
 
-enum Epi : int {
-  EPI_NONE = 0,       // alpha*acc (+beta*C)
-  EPI_BIAS = 1,       // alpha*acc + bias[n]
-  EPI_BIAS_RELU = 2,  // relu(alpha*acc + bias[n])
-  EPI_DRELU = 3,      // alpha*acc * (aux[m,n] > 0)      (ReLU backward fused in dgrad)
-};
+// Diagnostic build only (csrc/lab/gemm_lab.cpp, -DTDG_STAMPS): wave 0 of every
+// workgroup records s_memrealtime (100 MHz) at phase boundaries, one slot per
+// lane (vector stores), so a single launch yields per-workgroup timelines.
+#ifdef TDG_STAMPS
+__device__ unsigned long long* tdg_stamps;
+#define TDG_STAMP(i)                                                                      \
+  do {                                                                                    \
+    if (threadIdx.x < 64)                                                                 \
+      tdg_stamps[((size_t)blockIdx.x * 8 + (i)) * 64 + threadIdx.x] =                     \
+          __builtin_amdgcn_s_memrealtime();                                               \
+  } while (0)
+#else
+#define TDG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 
 // Grouped launch: up to MAXG same-shape problems in one grid (blockIdx.y =
 // problem). Used for the weight gradients, deferred to the end of backward and
@@ -89,6 +100,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     tn = t / tiles_m;
   }
   const int m0 = tm * BM, n0 = tn * BN;
+  TDG_STAMP(0);
 
   // split-K range
   const int kb = blockIdx.z * k_per_split;
@@ -107,24 +119,27 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   // loaded after the MFMAs their latency sat fully exposed at the end of
   // every tile. Issued first, they are older than every DMA, so the
   // pipeline's vmcnt waits stay exact (they only also cover these loads).
+  // Layout = the epilogue's 16-byte row chunks (EpiLds, tdg_gemm.h).
   using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
   constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int ES = sizeof(OutT);
-  constexpr int EPC = 16 / ES;                  // elements per 16-byte chunk
-  constexpr int CPR = WTN / EPC;                // chunks per sub-tile row
-  constexpr int NPRE = (WTM * CPR) / 64;        // 16-byte chunks per lane
+  constexpr int RPASS = OUT_F32 ? (WTM < 32 ? WTM : 32) : WTM;
+  using Epi = EpiLds<EPI, OUT_F32, TM, TN, RPASS>;
+  using EpiF = EpiLds<EPI_NONE, true, TM, TN, (WTM < 32 ? WTM : 32)>;  // split-K slabs
+  static_assert(NW * Epi::BYTES <= STAGES * (BM + BN) * BK * 2 &&
+                    NW * EpiF::BYTES <= STAGES * (BM + BN) * BK * 2,
+                "epilogue images must fit in the pipeline LDS");
   const bool split = gridDim.z > 1;
-  const bool pre_aux = EPI == EPI_DRELU && !split && (ldaux % 8) == 0 &&
+  const bool vec = epi_vec_ok<EPI, OUT_F32>(Cv, ldc, aux, ldaux);
+  constexpr bool SINGLE = RPASS == WTM;
+  const bool pre_aux = SINGLE && EPI == EPI_DRELU && !split && vec && (ldaux % 8) == 0 &&
                        (reinterpret_cast<uintptr_t>(aux) & 15) == 0;
-  const bool pre_c = beta != 0.f && !split && ((ldc * ES) % 16) == 0 &&
-                     (reinterpret_cast<uintptr_t>(Cv) & 15) == 0;
-  int4 aux_r[NPRE], c_r[NPRE];
+  const bool pre_c = SINGLE && beta != 0.f && !split && vec && ((ldc * (int)sizeof(OutT)) % 16) == 0;
+  int4 aux_r[Epi::ITER], c_r[Epi::ITER];
 #pragma unroll
-  for (int t = 0; t < NPRE; ++t) {
-    const int id = lane + 64 * t;
-    const int m = m0 + wm * WTM + id / CPR;
-    const int n = n0 + wn * WTN + (id % CPR) * EPC;
-    const bool in = m < M && n + EPC <= N;
+  for (int t = 0; t < Epi::ITER; ++t) {
+    const int m = m0 + wm * WTM + Epi::row_of(lane, t);
+    const int n = n0 + wn * WTN + Epi::col_of(lane, t);
+    const bool in = m < M && n + Epi::EPC <= N;
     if (pre_aux && in) aux_r[t] = *reinterpret_cast<const int4*>(aux + (size_t)m * ldaux + n);
     if (pre_c && in)
       c_r[t] = *reinterpret_cast<const int4*>(reinterpret_cast<const OutT*>(Cv) + (size_t)m * ldc + n);
@@ -159,6 +174,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     else
       wait_vmcnt<0>();
     lds_barrier();
+    TDG_STAMP(1);
     if (ktail && nk == 1) {
       GA::zero_ktail(smem, kb, ke, tid, NT);
       GB::zero_ktail(smem + A_BYTES, kb, ke, tid, NT);
@@ -186,7 +202,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb0[j], fa0[i], acc[i][j]);
     prio_lo();
     if (kt + 1 < nk) {
       // tile kt+1 landed (this wave's DMA), then everyone's; everyone is done
@@ -221,98 +237,29 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
     prio_lo();
   }
 
-  // ---------------- epilogue (LDS-staged, 16-byte coalesced stores)
-  // 1) every lane writes its accumulators (alpha, bias, relu applied; C/D
-  //    layout col = lane&15, row = 4*(lane>>4) + r) into a row-major LDS image
-  //    of the wave's sub-tile; 2) the wave reads the image back as 16-byte row
-  //    chunks, applies the elementwise epilogue that needs a second operand
-  //    (ReLU-mask aux, beta*C) with vector loads, and stores 16 bytes per lane.
-  // Split-K partial products take the same path into the f32 slab of split z.
-  constexpr int SROW = WTN * ES + 16;          // padded LDS row (bytes)
-  OutT* C = reinterpret_cast<OutT*>(Cv) + (split ? (size_t)blockIdx.z * split_stride : 0);
-  const float a_ = split ? 1.f : alpha;
-  const float b_ = split ? 0.f : beta;
+  TDG_STAMP(2);
+  // ---------------- epilogue: per-wave LDS image over the pipeline stages
+  // (EpiLds, tdg_gemm.h). Split-K partial products go unscaled into the f32
+  // slab of split z.
   lds_barrier();  // all waves done with the pipeline stages
-  char* wimg = smem + wid * (WTM * SROW);
-  const int g = lane >> 4, cl = lane & 15;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + 16 * j + cl;
-    float bn = 0.f;
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
-      if (!split) bn = bias[n < N ? n : N - 1];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = a_ * acc[i][j][r];
-        if constexpr (EPI == EPI_BIAS) v += bn;
-        if constexpr (EPI == EPI_BIAS_RELU) {
-          if (!split) v = fmaxf(v + bn, 0.f);
-        }
-        OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW +
-                                            (16 * j + cl) * ES);
-        if constexpr (OUT_F32) *dst = v;
-        else *dst = f2bf(v);
-      }
-    }
+  const int mw0 = m0 + wm * WTM, nw0 = n0 + wn * WTN;
+  if (split) {
+    float* Cs = reinterpret_cast<float*>(Cv) + (size_t)blockIdx.z * split_stride;
+    EpiF::run(smem + wid * EpiF::BYTES, acc, lane, Cs, ldc, M, N, mw0, nw0, 1.f, 0.f, nullptr,
+              nullptr, 0, epi_vec_ok<EPI_NONE, true>(Cs, ldc, nullptr, 0));
+  } else {
+    Epi::template run_pre<true>(smem + wid * Epi::BYTES, acc, lane, Cv, ldc, M, N, mw0, nw0, alpha,
+                                beta, bias, aux, ldaux, vec, aux_r, pre_aux, c_r, pre_c);
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local image complete
-  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
-                      (EPI != EPI_DRELU ||
-                       ((ldaux % 8) == 0 && (reinterpret_cast<uintptr_t>(aux) & 15) == 0));
-#pragma unroll
-  for (int t = 0; t < (WTM * CPR) / 64; ++t) {
-    const int id = lane + 64 * t;
-    const int row = id / CPR, ch = id % CPR;
-    const int m = m0 + wm * WTM + row;
-    const int n = n0 + wn * WTN + ch * EPC;
-    if (m >= M || n >= N) continue;
-    OutT vals[EPC];
-    *reinterpret_cast<int4*>(vals) =
-        *reinterpret_cast<const int4*>(wimg + row * SROW + ch * 16);
-    OutT* cp = C + (size_t)m * ldc + n;
-    if (vec_ok && n + EPC <= N) {
-      if constexpr (EPI == EPI_DRELU) {
-        short8_t x;
-        if (pre_aux) x = *reinterpret_cast<const short8_t*>(&aux_r[t]);
-        else x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
-#pragma unroll
-        for (int e = 0; e < EPC; ++e)
-          if (!(bf2f((bf16_t)x[e * (8 / EPC)]) > 0.f)) vals[e] = OutT(0);
-      }
-      if (b_ != 0.f) {
-        OutT old[EPC];
-        if (pre_c) *reinterpret_cast<int4*>(old) = c_r[t];
-        else *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
-#pragma unroll
-        for (int e = 0; e < EPC; ++e) {
-          if constexpr (OUT_F32) vals[e] += b_ * old[e];
-          else vals[e] = f2bf(bf2f(vals[e]) + b_ * bf2f(old[e]));
-        }
-      }
-      *reinterpret_cast<int4*>(cp) = *reinterpret_cast<const int4*>(vals);
-    } else {
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        if (n + e >= N) break;
-        OutT v = vals[e];
-        if constexpr (EPI == EPI_DRELU) {
-          if (!(bf2f(aux[(size_t)m * ldaux + n + e]) > 0.f)) v = OutT(0);
-        }
-        if (b_ != 0.f) {
-          if constexpr (OUT_F32) v += b_ * cp[e];
-          else v = f2bf(bf2f(v) + b_ * bf2f(cp[e]));
-        }
-        cp[e] = v;
-      }
-    }
-  }
+#ifdef TDG_STAMPS
+  TDG_STAMP(3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  TDG_STAMP(4);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -404,6 +351,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
   float bsum0 = 0.f, bsum1 = 0.f;
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = K / BK;  // host guarantees K % 64 == 0
+  TDG_STAMP(0);
 
   GA ga;
   GB gb;
@@ -478,6 +426,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
         if (more) wait_vmcnt<4>();
         else wait_vmcnt<0>();
         lds_barrier();
+        if (kt == 0 && ph == 0) TDG_STAMP(1);
       }
       if (ph == 0) {
 #pragma unroll
@@ -525,7 +474,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[i0 + i][j0 + j] = mfma16(fa[i0 + i][s2], fb[j0 + j][s2], acc[i0 + i][j0 + j]);
+            acc[i0 + i][j0 + j] = mfma16(fb[j0 + j][s2], fa[i0 + i][s2], acc[i0 + i][j0 + j]);
       __builtin_amdgcn_s_setprio(0);
       if (do_bsum && (ph == 0 || ph == 2)) {
         const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3f803f80);
@@ -561,86 +510,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     }
   }
 
-  // ---------------- epilogue: two 64-row halves through a per-wave LDS image
-  using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
-  constexpr int ES = sizeof(OutT);
-  constexpr int WTN = 64;
-  constexpr int SROW = WTN * ES + 16;
-  constexpr int EPC = 16 / ES;
-  constexpr int CPR = WTN / EPC;
+  TDG_STAMP(2);
+  // ---------------- epilogue: per-wave LDS image (EpiLds, tdg_gemm.h) over
+  // the pipeline stages; the wave tile is rows wm*128.., columns wn*64..
   wait_vmcnt<0>();
   lds_barrier();
-  char* wimg = smem + wid * (64 * SROW);
-  const int g = lane >> 4, cl16 = lane & 15;
-  OutT* C = reinterpret_cast<OutT*>(Cv);
-  const bool vec_ok = ((ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
-                      (EPI != EPI_DRELU ||
-                       ((ldaux % 8) == 0 && (reinterpret_cast<uintptr_t>(aux) & 15) == 0));
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + 16 * j + cl16;
-      float bn = 0.f;
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = alpha * acc[4 * hf + i][j][r];
-          if constexpr (EPI == EPI_BIAS) v += bn;
-          if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v + bn, 0.f);
-          OutT* dst = reinterpret_cast<OutT*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl16) * ES);
-          if constexpr (OUT_F32) *dst = v;
-          else *dst = f2bf(v);
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int tt = 0; tt < (64 * CPR) / 64; ++tt) {
-      const int id = lane + 64 * tt;
-      const int row = id / CPR, ch = id % CPR;
-      const int m = m0 + wm * 128 + hf * 64 + row;
-      const int n = n0 + wn * 64 + ch * EPC;
-      if (m >= M || n >= N) continue;
-      OutT vals[EPC];
-      *reinterpret_cast<int4*>(vals) = *reinterpret_cast<const int4*>(wimg + row * SROW + ch * 16);
-      OutT* cp = C + (size_t)m * ldc + n;
-      if (vec_ok && n + EPC <= N) {
-        if constexpr (EPI == EPI_DRELU) {
-          const short8_t x = *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
-#pragma unroll
-          for (int e = 0; e < EPC; ++e)
-            if (!(bf2f((bf16_t)x[e * (8 / EPC)]) > 0.f)) vals[e] = OutT(0);
-        }
-        if (beta != 0.f) {
-          OutT old[EPC];
-          *reinterpret_cast<int4*>(old) = *reinterpret_cast<const int4*>(cp);
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            if constexpr (OUT_F32) vals[e] += beta * old[e];
-            else vals[e] = f2bf(bf2f(vals[e]) + beta * bf2f(old[e]));
-          }
-        }
-        *reinterpret_cast<int4*>(cp) = *reinterpret_cast<const int4*>(vals);
-      } else {
-#pragma unroll
-        for (int e = 0; e < EPC; ++e) {
-          if (n + e >= N) break;
-          OutT v = vals[e];
-          if constexpr (EPI == EPI_DRELU) {
-            if (!(bf2f(aux[(size_t)m * ldaux + n + e]) > 0.f)) v = OutT(0);
-          }
-          if (beta != 0.f) {
-            if constexpr (OUT_F32) v += beta * cp[e];
-            else v = f2bf(bf2f(v) + beta * bf2f(cp[e]));
-          }
-          cp[e] = v;
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before rewrite
+  {
+    constexpr int RPASS = OUT_F32 ? 32 : 64;
+    using Epi = EpiLds<EPI, OUT_F32, 8, 4, RPASS>;
+    static_assert(8 * Epi::BYTES <= 2 * 4 * 128 * BK * 2, "epilogue images fit in the stages");
+    Epi::run(smem + wid * Epi::BYTES, acc, lane, Cv, ldc, M, N, m0 + wm * 128, n0 + wn * 64, alpha,
+             beta, bias, aux, ldaux, epi_vec_ok<EPI, OUT_F32>(Cv, ldc, aux, ldaux));
   }
+#ifdef TDG_STAMPS
+  TDG_STAMP(3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  TDG_STAMP(4);
+#endif
 }
 
 // Split-K reduction: C = sum_z slab[z] (+beta*C) with the epilogue.
@@ -796,9 +682,7 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
   static const GemmGroup kNoGroup{};
   const GemmGroup& gr = grp ? *grp : kNoGroup;
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int img = WM * (BM / WM) * ((BN / WN) * (F32 ? 4 : 2) + 16) * WN;
-  const int img32 = WM * (BM / WM) * ((BN / WN) * 4 + 16) * WN;  // split-K slab staging
-  const int lds = std::max(ST * (BM + BN) * BK * 2, std::max(img, splits > 1 ? img32 : 0));
+  const int lds = ST * (BM + BN) * BK * 2;  // pipeline stages only (register epilogue)
   static bool attr_set = false;  // >64 KiB dynamic LDS needs the opt-in
   if (!attr_set) {
     hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>,
@@ -844,9 +728,7 @@ int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t*
     return -4;
   } else {
     if (K % BK != 0 || tiles <= 0) return -3;
-    constexpr int stages = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
-    constexpr int img = 8 * 64 * (64 * (F32 ? 4 : 2) + 16);
-    constexpr int lds = stages > img ? stages : img;
+    constexpr int lds = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32>,
