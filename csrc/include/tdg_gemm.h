@@ -121,8 +121,6 @@ struct Glds {
 #ifndef TDG_EPI_SC1
 #define TDG_EPI_SC1 1
 #endif
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
 #ifndef TDG_GEMM_PRIO
 #define TDG_GEMM_PRIO 1
 #endif
@@ -317,8 +315,7 @@ struct EpiLds {
     if constexpr (EPI == EPI_DRELU)
       vok = vok && (ldaux % EPC) == 0 && (reinterpret_cast<uintptr_t>(aux) % (2 * EPC)) == 0;
 #if TDG_EPI_SC1
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        Cv, 0, (int)min((size_t)0x7fffffff, ((size_t)(M - 1) * ldc + N) * ES), 0x00020000);
+    const WtBuf wt(Cv, ((size_t)(M - 1) * ldc + N) * ES);
 #endif
     f32x4 bn[TN];
 #pragma unroll
@@ -393,8 +390,7 @@ struct EpiLds {
 #if TDG_EPI_SC1
           // write-through (sc1): nothing left dirty in the XCD's L2 for the
           // end-of-kernel write-back
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, vals), crs,
-                                                 (int)(cp - reinterpret_cast<char*>(Cv)), 0, 16);
+          wt.st16(cp, vals);
 #else
           *reinterpret_cast<VecT*>(cp) = vals;
 #endif

@@ -28,6 +28,25 @@ struct RowVec {
       }
     }
   }
+  // write-through variant (tdg_common.h WtBuf)
+  __device__ __forceinline__ void store_bf(bf16_t* p, const WtBuf& wt) const {
+    if constexpr (VEC == 2) {
+      wt.st4(p, (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16));
+    } else if constexpr (VEC == 4) {
+      short4_t w;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = (short)f2bf(v[i]);
+      wt.st8(p, w);
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC / 8; ++c) {
+        short8_t w;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = (short)f2bf(v[8 * c + i]);
+        wt.st16(p + 8 * c, w);
+      }
+    }
+  }
   __device__ __forceinline__ void store_bf(bf16_t* p) const {
     if constexpr (VEC == 2) {
       *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -85,7 +104,7 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
                                            bf16_t* __restrict__ hsave, float* __restrict__ mean_out,
                                            float* __restrict__ rstd_out, float p, uint32_t thresh,
                                            uint64_t seed, const long long* ctr, uint64_t site,
-                                           float eps, RowVec<D / 64>& o) {
+                                           float eps, RowVec<D / 64>& o, size_t wt_bytes = 0) {
   constexpr int VEC = D / 64;
   if (has_t) {
     if (p > 0.f) {
@@ -97,8 +116,10 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h.v[i] += t.v[i];
   }
+  // wt_bytes > 0: y / hsave (that many bytes each) stored write-through
   if (hsave) {
-    h.store_bf(hsave + base);
+    if (wt_bytes) h.store_bf(hsave + base, WtBuf(hsave, wt_bytes));
+    else h.store_bf(hsave + base);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h.v[i] = bf2f(f2bf(h.v[i]));
   }
@@ -119,7 +140,8 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
     const int col = lane * VEC + i;
     o.v[i] = (h.v[i] - mean) * rstd * gamma[col] + beta[col];
   }
-  o.store_bf(y + base);
+  if (wt_bytes) o.store_bf(y + base, WtBuf(y, wt_bytes));
+  else o.store_bf(y + base);
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;

@@ -50,27 +50,28 @@ __device__ __forceinline__ void adam4(float4& pp, const float4& gg, float4& mm, 
   }
 }
 
-__device__ __forceinline__ void st_nt4(float4* a, const float4& x) {
-  __builtin_nontemporal_store(x.x, &a->x);
-  __builtin_nontemporal_store(x.y, &a->y);
-  __builtin_nontemporal_store(x.z, &a->z);
-  __builtin_nontemporal_store(x.w, &a->w);
-}
 
-__device__ __forceinline__ void adam_store(float4* P4, float4* G4, float4* M4, float4* V4,
-                                           uint2* S2, long long i, const float4& pp,
+// Write-through (sc1) stores of everything Adam writes: the master weights
+// and moments are re-read by nothing until the next step and the bf16 shadow
+// by the next forward's GEMMs on other XCDs, so none of it should sit dirty
+// in an XCD's L2 for the end-of-kernel write-back (tdg_common.h WtBuf).
+struct AdamOut {
+  WtBuf p, m, v, s;
+  __device__ __forceinline__ AdamOut(float* P, float* M, float* V, bf16_t* S, long long n)
+      : p(P, (size_t)n * 4), m(M, (size_t)n * 4), v(V, (size_t)n * 4), s(S ? (const void*)S : (const void*)P, (size_t)n * 2) {}
+};
+
+__device__ __forceinline__ void adam_store(const AdamOut& o, float4* P4, float4* G4, float4* M4,
+                                           float4* V4, uint2* S2, long long i, const float4& pp,
                                            const float4& mm, const float4& vv, int zero_grad) {
-  // the master weights are re-read by nothing until the next step: stream
-  // them (and the moments) past the caches; the bf16 shadow copy is read by
-  // the next forward's GEMMs, so it goes through L2 normally
-  st_nt4(P4 + i, pp);
-  st_nt4(M4 + i, mm);
-  st_nt4(V4 + i, vv);
+  o.p.st16(P4 + i, pp);
+  o.m.st16(M4 + i, mm);
+  o.v.st16(V4 + i, vv);
   if (zero_grad) G4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (S2) {
     const uint32_t lo = (uint32_t)f2bf(pp.x) | ((uint32_t)f2bf(pp.y) << 16);
     const uint32_t hi = (uint32_t)f2bf(pp.z) | ((uint32_t)f2bf(pp.w) << 16);
-    S2[i] = make_uint2(lo, hi);
+    o.s.st8(S2 + i, make_uint2(lo, hi));
   }
 }
 
@@ -93,6 +94,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   float4* M4 = reinterpret_cast<float4*>(m);
   float4* V4 = reinterpret_cast<float4*>(v);
   uint2* S2 = shadow ? reinterpret_cast<uint2*>(shadow) : nullptr;
+  const AdamOut o(p, m, v, shadow, n);
   const long long stride = (long long)gridDim.x * blockDim.x;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i + stride < n4; i += 2 * stride) {
@@ -101,13 +103,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     float4 pb = P4[j], gb = G4[j], mb = M4[j], vb = V4[j];
     adam4(pa, ga, ma, va, c, lr, lr_t, ob1, ob2);
     adam4(pb, gb, mb, vb, c, lr, lr_t, ob1, ob2);
-    adam_store(P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
-    adam_store(P4, G4, M4, V4, S2, j, pb, mb, vb, c.zero_grad);
+    adam_store(o, P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
+    adam_store(o, P4, G4, M4, V4, S2, j, pb, mb, vb, c.zero_grad);
   }
   if (i < n4) {
     float4 pa = P4[i], ga = G4[i], ma = M4[i], va = V4[i];
     adam4(pa, ga, ma, va, c, lr, lr_t, ob1, ob2);
-    adam_store(P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
+    adam_store(o, P4, G4, M4, V4, S2, i, pa, ma, va, c.zero_grad);
   }
 }
 
@@ -192,10 +194,16 @@ extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, lo
   if (n % 4 != 0) return -1;
   AdamCfg c{beta1, beta2, eps, lr_const, d_model, warmup, grad_scale, weight_decay, sched,
             zero_grad};
-  const long long n4 = n / 4;
-  const int blocks = (int)std::min<long long>(8192, (n4 + 255) / 256);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p, g, m, v,
-                     (bf16_t*)shadow, n, step, c);
+  // launches over chunks of <= 2^28 parameters: the write-through stores
+  // address each buffer through a descriptor with 31-bit byte offsets
+  constexpr long long CHUNK = 1LL << 28;
+  for (long long o = 0; o < n; o += CHUNK) {
+    const long long cn = std::min(CHUNK, n - o);
+    const long long n4 = cn / 4;
+    const int blocks = (int)std::min<long long>(8192, (n4 + 255) / 256);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p + o, g + o,
+                       m + o, v + o, shadow ? (bf16_t*)shadow + o : nullptr, cn, step, c);
+  }
   // per-bucket updates (data parallel) share one step: only the last advances it
   if (inc_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   return 0;

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   h.load_bf(x + base);
   if (s) t.load_bf(s + base);
   ln_row_fwd<D>(h, t, s != nullptr, base, row, lane, gamma, beta, y, hsave, mean_out, rstd_out, p,
-                thresh, seed, ctr, site, eps, o);
+                thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t));
   if (y8) {  // fused e4m3 copy of y for an fp8 GEMM (delayed per-tensor scale)
     const float s8 = s8p[0];
     float am = 0.f;
@@ -98,6 +98,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
   for (int i = 0; i < VEC; ++i) gm[i] = gamma[lane * VEC + i];
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const WtBuf wdh(dh_out, (size_t)M * D * sizeof(bf16_t));  // write-through outputs
+  const WtBuf wds(ds_out ? ds_out : dh_out, (size_t)M * D * sizeof(bf16_t));
   // `iters` row groups per block, partial column sums accumulated across them
   // (fewer partial rows for the fold: D = 1024 uses 2)
 #pragma unroll 1
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       for (int i = 0; i < VEC; ++i) ds.v[i] = ((km >> i) & 1u) ? dh.v[i] * sc : 0.f;
     }
     if (ds_out) {
-      ds.store_bf(ds_out + base);
+      ds.store_bf(ds_out + base, wds);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
     }
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < VEC; ++i) dh.v[i] += e[k].v[i];
     }
-    dh.store_bf(dh_out + base);
+    dh.store_bf(dh_out + base, wdh);
   }
   }  // row groups
 #pragma unroll
