@@ -112,8 +112,13 @@ __device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset
 
 // ---------------------------------------------------------------- MFMA
 __device__ __forceinline__ f32x4 mfma16(const short8_t& a, const short8_t& b, const f32x4& c) {
+#ifdef TDG_ABLATE_MFMA  // lab-only ablation: operands consumed, no matrix work
+  asm volatile("" ::"v"(a), "v"(b));
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+#endif
 }
 
 // ds_read_b64_tr_b16: per 16-lane group, reads 4 rows x 16 columns (16-bit) and

@@ -58,11 +58,18 @@ struct Case {
 };
 
 int main(int argc, char** argv) {
-  std::vector<Case> cases = {
-      {2048, 2048, 128, 12}, {2048, 2048, 512, 12}, {8192, 2048, 128, 12}, {8192, 2048, 512, 12},
-      {8192, 1536, 512, 12}, {8192, 512, 128, 7},   {8192, 512, 512, 7},   {8192, 512, 2048, 7},
-      {8192, 512, 512, 4},   {8192, 512, 2048, 4},
-  };
+  std::vector<Case> cases;
+  for (int cfg : {12}) {
+    cases.push_back({2048, 2048, 512, cfg});
+    cases.push_back({8192, 2048, 512, cfg});
+    cases.push_back({8192, 1536, 512, cfg});
+    cases.push_back({8192, 2048, 2048, cfg});
+    cases.push_back({4096, 4096, 4096, cfg});
+  }
+  for (int cfg : {4, 7, 13}) {
+    cases.push_back({8192, 512, 512, cfg});
+    cases.push_back({8192, 512, 2048, cfg});
+  }
   if (argc > 1) {  // M N K cfg
     cases = {{std::atoi(argv[1]), std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4])}};
   }
@@ -145,7 +152,8 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(stamps, 0, nst * sizeof(unsigned long long), st));
     launch();
     CK(hipStreamSynchronize(st));
-    int tm = c.cfg == 12 ? 256 : (c.cfg == 7 ? 64 : 128), tn = c.cfg == 12 ? 256 : 128;
+    const bool t256 = c.cfg == 12;
+    int tm = t256 ? 256 : (c.cfg == 7 ? 64 : 128), tn = t256 ? 256 : 128;
     const int nwg = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
     std::vector<unsigned long long> hs((size_t)nwg * 8 * 64);
     CK(hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost));

@@ -107,8 +107,9 @@ def test_gemm_wgrad_f32(M, N, K, splits):
 @pytest.mark.parametrize("M,N,K", [(512, 256, 1024), (300, 520, 128), (7010, 512, 256)])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_gemm256_nn_tn(M, N, K, beta):
-    """256x256 tiles (cfg 12) with MN-contiguous operands: dgrad NN (bf16, beta)
-    and wgrad TN (f32, beta)."""
+    """256x256 tiles (cfg 12) with MN-contiguous operands: dgrad NN (bf16,
+    beta) and wgrad TN (f32, beta); NT with the bias + ReLU epilogue."""
+    cfg = 12
     from tensorflow_distributed_on_gke_amd.ops._ext import C
     ld = (M + 7) // 8 * 8
     # NN: out[M,N] = dy[M,K] @ w[K,N]
@@ -116,15 +117,23 @@ def test_gemm256_nn_tn(M, N, K, beta):
     w = _bf(_rand(K, N, scale=0.5, seed=22)).to(DEV)
     out = _bf(_rand(M, N, seed=23)).to(DEV)
     ref = dy.float() @ w.float() + beta * out.float()
-    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=beta, cfg=(12, 1))
+    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=beta, cfg=(cfg, 1))
     _close(out, ref, 1e-2, "gemm256 NN")
     # TN: dw[M,N] = a[K,M]^T @ x[K,N]  (a stored [K][ld])
     a = _bf(_rand(K, ld, seed=24)).to(DEV)
     x = _bf(_rand(K, N, seed=25)).to(DEV)
     dw = _rand(M, N, seed=26).to(DEV)
     ref = a[:, :M].float().t() @ x.float() + beta * dw
-    C().gemm(a, x, dw, None, None, M, N, K, ld, N, N, 0, False, False, 0, 1.0, beta, 12, 1, None)
+    C().gemm(a, x, dw, None, None, M, N, K, ld, N, N, 0, False, False, 0, 1.0, beta, cfg, 1, None)
     _close(dw, ref, 2e-3, "gemm256 TN")
+    # NT with the bias + ReLU epilogue (forward)
+    xa = _bf(_rand(M, K, seed=27)).to(DEV)
+    wt = _bf(_rand(N, K, scale=0.5, seed=28)).to(DEV)
+    bias = _rand(N, seed=29).to(DEV)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ref = torch.relu(xa.float() @ wt.float().t() + bias)
+    kk.gemm(xa, wt, y, M, N, K, K, K, N, True, True, kk.EPI_BIAS_RELU, bias=bias, cfg=(cfg, 1))
+    _close(y, ref, 1e-2, "gemm256 NT bias relu")
 
 
 def test_wgrad_ragged():
