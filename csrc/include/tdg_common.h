@@ -8,6 +8,23 @@
 
 namespace tdg {
 
+// Diagnostic build only (csrc/lab/*.cpp, -DTDG_STAMPS): wave 0 of every
+// workgroup records s_memrealtime (100 MHz) at phase boundaries, one slot per
+// lane (vector stores), so a single launch yields per-workgroup timelines.
+#ifdef TDG_STAMPS
+__device__ unsigned long long* tdg_stamps;
+#define TDG_STAMP(i)                                                                      \
+  do {                                                                                    \
+    if (threadIdx.x < 64)                                                                 \
+      tdg_stamps[(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 512 + (i) * 64 + threadIdx.x] =                     \
+          __builtin_amdgcn_s_memrealtime();                                               \
+  } while (0)
+#else
+#define TDG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 typedef uint16_t bf16_t;  // raw bf16 bits in memory
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

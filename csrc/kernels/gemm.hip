@@ -29,22 +29,6 @@
 
 namespace tdg {
 
-// Diagnostic build only (csrc/lab/gemm_lab.cpp, -DTDG_STAMPS): wave 0 of every
-// workgroup records s_memrealtime (100 MHz) at phase boundaries, one slot per
-// lane (vector stores), so a single launch yields per-workgroup timelines.
-#ifdef TDG_STAMPS
-__device__ unsigned long long* tdg_stamps;
-#define TDG_STAMP(i)                                                                      \
-  do {                                                                                    \
-    if (threadIdx.x < 64)                                                                 \
-      tdg_stamps[((size_t)blockIdx.x * 8 + (i)) * 64 + threadIdx.x] =                     \
-          __builtin_amdgcn_s_memrealtime();                                               \
-  } while (0)
-#else
-#define TDG_STAMP(i) \
-  do {               \
-  } while (0)
-#endif
 
 
 // Grouped launch: up to MAXG same-shape problems in one grid (blockIdx.y =

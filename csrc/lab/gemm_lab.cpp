@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   unsigned long long* stamps;
-  const size_t nst = 4096 * 8 * 64;
+  const size_t nst = 4096 * 512;
   CK(hipMalloc(&stamps, nst * sizeof(unsigned long long)));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(tdg::tdg_stamps), &stamps, sizeof(stamps)));
   std::mt19937 rng(1);
@@ -155,13 +155,13 @@ int main(int argc, char** argv) {
     const bool t256 = c.cfg == 12;
     int tm = t256 ? 256 : (c.cfg == 7 ? 64 : 128), tn = t256 ? 256 : 128;
     const int nwg = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
-    std::vector<unsigned long long> hs((size_t)nwg * 8 * 64);
+    std::vector<unsigned long long> hs((size_t)nwg * 512);
     CK(hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost));
     std::vector<double> ph[4];
     unsigned long long t0min = ~0ull, t0max = 0, t4max = 0;
     for (int b = 0; b < nwg; ++b) {
       unsigned long long t[5];
-      for (int i = 0; i < 5; ++i) t[i] = hs[((size_t)b * 8 + i) * 64];
+      for (int i = 0; i < 5; ++i) t[i] = hs[(size_t)b * 512 + i * 64];
       if (!t[0] || !t[4]) continue;
       for (int i = 0; i < 4; ++i) ph[i].push_back((double)(t[i + 1] - t[i]) * 0.01);  // us
       t0min = std::min(t0min, t[0]);
