@@ -138,6 +138,15 @@ class WgradQueue:
         # part of a wave cost a whole wave each: 4 chunks measured 1004 us vs
         # 745 us for one launch on Transformer-base)
         self.wave_tiles = wave_tiles
+        # layer_end() calls per backward (set by the owner: encoder + decoder
+        # layers). With wave chunking the LAST layer end flushes everything
+        # queued, partial wave included: otherwise the remainder waits for the
+        # end of backward and its gradients join the embedding gradients in
+        # the final, fully exposed all-reduce span (71 MB at Transformer-base;
+        # with the full flush the final span holds little more than the
+        # source embedding)
+        self.layers_per_step = 0
+        self._layer_ends = 0
         self._cursor = 0  # tiles of items[0] already launched
         # deferred LayerNorm dgamma/dbeta/bias partial folds (one launch per flush)
         self.reductions = []
@@ -162,9 +171,11 @@ class WgradQueue:
 
     def layer_end(self) -> None:
         """A decoder or encoder layer's backward is complete."""
+        self._layer_ends += 1
+        last = self.layers_per_step > 0 and self._layer_ends >= self.layers_per_step
         if not self._chunking() or not self.items:
             return
-        if not all(self._ragged_ok(it) for it in self.items):
+        if last or not all(self._ragged_ok(it) for it in self.items):
             self.flush()
             return
         queued = sum(self._tiles(it) for it in self.items) - self._cursor
@@ -175,6 +186,10 @@ class WgradQueue:
 
     def add(self, dy2, x2, N, w: Param, b: Optional[Param], beta: float, rt: "RunCtx"):
         self.items.append((dy2, x2, N, w, b, beta, rt))
+
+    def step_done(self) -> None:
+        """End of a backward: the layer-end count restarts."""
+        self._layer_ends = 0
 
     def flush(self) -> None:
         if self.items:

@@ -371,6 +371,7 @@ class Transformer:
         dec.backward(ddec.view(B, T, cfg.d_model).to(dec.dtype))
         if rt.wgrad is not None:
             rt.wgrad.flush()
+            rt.wgrad.step_done()
         if dev.type == "cuda":
             join(dev)  # weight gradients are final when this returns
         return step_out

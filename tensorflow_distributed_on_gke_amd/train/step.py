@@ -76,6 +76,8 @@ class TrainStep:
             dp = ddp is not None and ddp.active
             self.rt.wgrad = WgradQueue(flush_at_boundary=dp,
                                        wave_tiles=(WAVE_TILES or K.NUM_CU) if dp and CHUNKED_WGRAD else 0)
+            # every encoder and decoder layer's backward ends with a layer_end()
+            self.rt.wgrad.layers_per_step = 2 * model.cfg.layers
         self.fp8 = fp8_state
         if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
             opt.zero_grad = False  # every GPU gradient writer overwrites
