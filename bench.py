@@ -145,7 +145,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16" if args.dtype == "bf16" else
+            "dtype": ("fp32 (CPU reference ops)" if dev.type != "cuda" else "bf16") if args.dtype == "bf16" else
                      "fp8 (e4m3 forward GEMMs of the FFNs and attention input projections, bf16 elsewhere)",
             "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
