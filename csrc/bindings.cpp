@@ -76,6 +76,7 @@ int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, 
              float grad_scale, float weight_decay, int sched, int zero_grad, int inc_step,
              hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
+int tdg_cu_hog(const void* buf, float* out, int nblocks, int iters, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
 }
@@ -853,6 +854,16 @@ void transpose_grouped(const std::vector<Tensor>& srcs, const std::vector<Tensor
             "tdg transpose_grouped");
 }
 
+// diagnostic: nblocks workgroups streaming 1 MiB each of buf, iters times
+void cu_hog(const Tensor& buf, const Tensor& out, int64_t nblocks, int64_t iters) {
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous() && buf.nbytes() >= (size_t)nblocks << 20,
+              "cu_hog: buf needs nblocks MiB");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= nblocks, "cu_hog: out");
+  check_err(tdg_cu_hog(buf.data_ptr(), out.data_ptr<float>(), (int)nblocks, (int)iters,
+                       stream_of(buf)),
+            "tdg cu_hog");
+}
+
 void to_bf16(const Tensor& p, const Tensor& o) {
   check_f32(p, "p");
   check_bf16(o, "o");
@@ -894,5 +905,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("reduce_partials_multi", &reduce_partials_multi);
   m.def("to_bf16", &to_bf16);
+  m.def("cu_hog", &cu_hog);
   m.attr("ARCH") = "gfx950";
 }
