@@ -161,6 +161,8 @@ class DecoderLayer:
 
 
 TRANSPOSED_FFN_DGRAD = os.environ.get("TDG_FFN_DGRAD_T", "1") != "0"
+# smallest d_model that keeps W2^T for the FFN relu-backward dgrad
+TRANSPOSED_FFN_MIN_D = int(os.environ.get("TDG_FFN_DGRAD_T_MIN_D", "1024"))
 
 
 def seq_lengths(tok: torch.Tensor, check: bool = True) -> torch.Tensor:
@@ -217,7 +219,7 @@ class Transformer:
     def build(self, device="cpu", seed: int = 0, compute_dtype=torch.bfloat16) -> "Transformer":
         self.device = torch.device(device)
         self.store.finalize(self.device, compute_dtype, seed)
-        if self.device.type == "cuda" and TRANSPOSED_FFN_DGRAD and self.cfg.d_model >= 1024:
+        if self.device.type == "cuda" and TRANSPOSED_FFN_DGRAD and self.cfg.d_model >= TRANSPOSED_FFN_MIN_D:
             # the FFN's relu-backward dgrad reads W2 K-contiguous the other way
             # round: keep W2^T so it runs with the forward-layout (NT) 256x256
             # kernel. Measured per call: d 1024 / ff 4096: 111.5 -> 102.6 us
