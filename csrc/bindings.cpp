@@ -56,6 +56,8 @@ int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* pa
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
                      int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc, int out_f32,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
+void tdg_set_gemm256_pp(int on);
+int tdg_get_gemm256_pp();
 int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                     const int* shapes, int K, int a_kc, int b_kc, int out_f32, float alpha,
                     float beta, float* const* bias_out, hipStream_t st);
@@ -883,6 +885,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),
         py::arg("bias_out") = std::vector<c10::optional<Tensor>>{});
   m.def("colsum_grouped", &colsum_grouped);
+  m.def("set_gemm256_pp", [](bool on) { tdg_set_gemm256_pp(on ? 1 : 0); });
+  m.def("get_gemm256_pp", []() { return tdg_get_gemm256_pp() != 0; });
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_scale_update", &fp8_scale_update);

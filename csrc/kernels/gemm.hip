@@ -25,6 +25,7 @@
 #include "tdg_gemm.h"
 #include "tdg_reduce.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace tdg {
@@ -285,7 +286,36 @@ struct R256Args {
   int ncls;
 };
 
-template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+// PP (ping-pong variant): the two waves sharing a SIMD (wave rows wm = 0 / 1)
+// run one barrier apart, so while one issues a phase's MFMAs the other does
+// its fragment reads, waits and LDS-DMA issue -- the lock-step loop above
+// leaves the MFMA pipe idle during every wait. Each phase is
+//   [vmcnt wait, ds_reads, DMA of one half-tile]  barrier  [MFMAs]  barrier
+// with wave row 1 lagging by one barrier. Half-tiles are issued 6 phases
+// before they are read (3 in flight in steady state, vmcnt(6)):
+//   phase 0 of tile t issues B1(t+1), 1: A1(t+1), 2: A0(t+2), 3: B0(t+2);
+// a half read in phase p is retired (vmcnt) by every wave in phase p-1, and a
+// buffer half is restaged >= 2 phases after its last read (the lagging row's
+// reads complete one barrier later than the leading row's).
+// vmcnt wait leaving `n` (0..4) younger half-tiles (2 LDS-DMA each) in flight
+__device__ __forceinline__ void wait_halves(int n) {
+  switch (n) {
+    case 4: wait_vmcnt<8>(); break;
+    case 3: wait_vmcnt<6>(); break;
+    case 2: wait_vmcnt<4>(); break;
+    case 1: wait_vmcnt<2>(); break;
+    default: wait_vmcnt<0>(); break;
+  }
+}
+// lds_barrier fenced against the scheduler: the register-only MFMAs of a
+// ping-pong section must not move across the barriers that delimit it
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, bool PP>
 __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
                                                       const float* __restrict__ bias,
                                                       const bf16_t* __restrict__ aux, int K,
@@ -394,13 +424,109 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int h = 0; h < 4; ++h) issue_half(0, h);
-
   // this wave's rows/columns inside the half-tile images: a-subtile i (0..3)
   // of half hA at wm*64 + 16i; b-subtile j (0..1) of half hB at wn*32 + 16j
   const int arow = wm * 64, brow = wn * 32;
   short8_t fa[8][2], fb[4][2];
+  auto bias_sum = [&](int ph) {
+    const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3f803f80);
+    float bs = ph == 0 ? bsum0 : bsum1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i != wn) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t f = ph == 0 ? fa[i][s2] : fa[4 + i][s2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bs = __builtin_amdgcn_fdot2_f32_bf16(
+              __builtin_bit_cast(bf16x2_t, (short2_t){f[2 * e], f[2 * e + 1]}), one, bs, false);
+      }
+    }
+    if (ph == 0) bsum0 = bs;
+    else bsum1 = bs;
+  };
+  if constexpr (PP) {
+    // prologue: A0(0) B0(0) B1(0) A1(0) [A0(1) B0(1)]; retire A0(0), B0(0)
+    issue_half(0, 0);
+    issue_half(0, 1);
+    issue_half(0, 2);
+    issue_half(0, 3);
+    if (nk > 1) {
+      issue_half(1, 0);
+      issue_half(1, 1);
+    }
+    wait_halves(nk > 1 ? 4 : 2);
+    pp_barrier();
+    TDG_STAMP(1);
+    if (wm == 1) pp_barrier();  // the lag
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* st = smem + (kt & 1) * SB;
+      const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        // ---- memory section: retire the half the NEXT phase reads
+        if (ph == 0) wait_halves(n1 ? 3 : 1);       // B1(kt)
+        else if (ph == 1) wait_halves(n1 ? 3 : 0);  // A1(kt)
+        else if (ph == 3 && n1) wait_halves(n2 ? 3 : 2);  // A0(kt+1), B0(kt+1)
+        if (ph == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<A_KC, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<B_KC, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
+          if (n1) issue_half(kt + 1, 2);
+        } else if (ph == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<B_KC, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
+          if (n1) issue_half(kt + 1, 3);
+        } else if (ph == 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
+          if (n2) issue_half(kt + 2, 0);
+        } else {
+          if (n2) issue_half(kt + 2, 1);
+        }
+        pp_barrier();  // lgkmcnt(0): this phase's fragments are in registers
+        // ---- MFMA section
+        if (ph == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tie_all(fa[i]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) tie_all(fb[j]);
+        } else if (ph == 1) {
+#pragma unroll
+          for (int j = 2; j < 4; ++j) tie_all(fb[j]);
+        } else if (ph == 2) {
+#pragma unroll
+          for (int i = 4; i < 8; ++i) tie_all(fa[i]);
+        }
+        const int i0 = (ph < 2) ? 0 : 4;
+        const int j0 = (ph == 0 || ph == 3) ? 0 : 2;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i0 + i][j0 + j] = mfma16(fb[j0 + j][s2], fa[i0 + i][s2], acc[i0 + i][j0 + j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (do_bsum && (ph == 0 || ph == 2)) bias_sum(ph);
+        pp_barrier();
+      }
+    }
+    if (wm == 0) pp_barrier();  // re-align the rows before the epilogue
+  } else {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue_half(0, h);
   for (int kt = 0; kt < nk; ++kt) {
     const char* st = smem + (kt & 1) * SB;
     const bool more = kt + 1 < nk;
@@ -460,27 +586,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
           for (int j = 0; j < 2; ++j)
             acc[i0 + i][j0 + j] = mfma16(fb[j0 + j][s2], fa[i0 + i][s2], acc[i0 + i][j0 + j]);
       __builtin_amdgcn_s_setprio(0);
-      if (do_bsum && (ph == 0 || ph == 2)) {
-        const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3f803f80);
-        float bs = ph == 0 ? bsum0 : bsum1;
-        // constant fragment indices only (a wave-uniform branch per candidate):
-        // a runtime index would move fa[] to scratch
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (i != wn) continue;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const short8_t f = ph == 0 ? fa[i][s2] : fa[4 + i][s2];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              bs = __builtin_amdgcn_fdot2_f32_bf16(
-                  __builtin_bit_cast(bf16x2_t, (short2_t){f[2 * e], f[2 * e + 1]}), one, bs, false);
-          }
-        }
-        if (ph == 0) bsum0 = bs;
-        else bsum1 = bs;
-      }
+      // bias-gradient row sums: constant fragment indices only (a
+      // wave-uniform branch per candidate): a runtime index would move fa[]
+      // to scratch
+      if (do_bsum && (ph == 0 || ph == 2)) bias_sum(ph);
     }
+  }
   }
   if (do_bsum) {  // lanes l, l+16, l+32, l+48 hold disjoint K subsets of row l&15
     bsum0 += __shfl_xor(bsum0, 16, 64);
@@ -693,6 +804,17 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
   }
 }
 
+// 256x256 main loop: ping-pong (TDG_GEMM256_PP=1) or lock-step (0). Read once
+// per process; tdg_set_gemm256_pp overrides it (tests, A/B in one process).
+static int g_gemm256_pp = -1;
+inline bool tdg_gemm256_pp() {
+  if (g_gemm256_pp < 0) {
+    const char* e = getenv("TDG_GEMM256_PP");
+    g_gemm256_pp = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_gemm256_pp == 1;
+}
+
 // Which (layout, epilogue) combinations have a 256x256 instantiation:
 // forward NT (plain / bias / bias+relu; relu-backward for dgrads against a
 // transposed weight copy), dgrad NN (plain / relu-backward), wgrad TN (f32 or
@@ -715,12 +837,18 @@ int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t*
     constexpr int lds = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32>,
+      hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds, st, args,
-                       bias, aux, K, ldaux, alpha, beta);
+    if (tdg_gemm256_pp())
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, true>), dim3(tiles), dim3(512), lds, st,
+                         args, bias, aux, K, ldaux, alpha, beta);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, false>), dim3(tiles), dim3(512), lds, st,
+                         args, bias, aux, K, ldaux, alpha, beta);
     return 0;
   }
 }
@@ -905,6 +1033,9 @@ extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void*
   return -4;
 #undef TDG_RG
 }
+
+extern "C" void tdg_set_gemm256_pp(int on) { g_gemm256_pp = on ? 1 : 0; }
+extern "C" int tdg_get_gemm256_pp() { return tdg_gemm256_pp() ? 1 : 0; }
 
 extern "C" void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld,
                            int rows_per_block, float beta, hipStream_t st) {
