@@ -178,3 +178,27 @@ def test_gpu_trainer_on_text_data(tmp_path, monkeypatch):
     losses = [h.train_loss for h in hist]
     assert all(l == l for l in losses) and losses[-1] < 0.85 * losses[0], losses
     assert torch.isfinite(tr.model.store.flat).all()
+
+
+def test_gpu_trainer_hip_graph_matches_eager(tmp_path, monkeypatch):
+    """The training loop with hip_graph=1 (capture on the first batch, its
+    warm-up steps rolled back) leaves the same weights, bitwise, as the eager
+    loop over the same batches, and opt.iterations == global_step -- so the
+    Noam schedule and the resume bundle count real steps only."""
+    from tensorflow_distributed_on_gke_amd.config import Settings
+    from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
+    from tensorflow_distributed_on_gke_amd.train.loop import Trainer
+
+    monkeypatch.chdir(tmp_path)
+    out = {}
+    for graph in (False, True):
+        s = Settings(preset="tiny", local_batch_size=16, src_len=24, tgt_len=24, epochs=2,
+                     steps_per_epoch=5, validation_steps=1, log_every=100, snapshot_every_epochs=0,
+                     resume=False, hip_graph=graph, seed=3)
+        tr = Trainer(s, DistInfo(0, 1, 0, torch.device("cuda", 0)), log=lambda m: None)
+        tr.fit()
+        torch.cuda.synchronize()
+        assert tr.opt.iterations == tr.global_step == 10, (graph, tr.opt.iterations, tr.global_step)
+        out[graph] = tr.model.store.flat.detach().clone()
+    assert torch.equal(out[False], out[True]), \
+        f"graph vs eager weights differ: max {(out[False] - out[True]).abs().max().item():.3e}"
