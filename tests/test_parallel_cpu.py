@@ -1,4 +1,4 @@
-"""Multi-process data parallelism on CPU (gloo, world_size 2).
+"""Multi-process data parallelism on CPU (gloo, world_size 2 and 4).
 
 The bucketed, backward-overlapped all-reduce must give exactly the update a
 single process computes from both ranks' batches with the reference's loss
@@ -130,6 +130,25 @@ def test_dp2_matches_single_process(tmp_path, bucket_mb, overlap_opt):
     assert not torch.equal(r0["flat"], Transformer(model_config("tiny", **CFG)).build("cpu", seed=1).store.flat)
     assert torch.allclose(r0["flat"], ref_flat, atol=1e-6, rtol=1e-5)
     assert torch.allclose(r0["loss"], ref_loss, atol=1e-6)
+
+
+def test_dp4_matches_single_process(tmp_path):
+    """Four ranks (the rehearsal closest to a node's 8 we can run on CPU):
+    small spans launched from inside backward, per-span Adam mid-backward;
+    every replica bitwise equal and equal to the single-process update on all
+    four ranks' batches."""
+    world = 4
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, _free_port(), out, 0.05, None, 1),
+                       nprocs=world, join=True, start_method="spawn")
+    rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    assert rs[0]["nb"] > 3
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["flat"], r["flat"])
+    assert all(r["diverged"] for r in rs)
+    ref_flat, ref_loss = _single_process_reference(world)
+    assert torch.allclose(rs[0]["flat"], ref_flat, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(rs[0]["loss"], ref_loss, atol=1e-6)
 
 
 def test_dp2_global_token_mean_loss(tmp_path):
