@@ -158,23 +158,28 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   for (int i = 0; i < T::DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
+  // K / V tiles staged global -> registers -> LDS; the NEXT tile's loads are
+  // issued right after the current one is in LDS, so they are in flight
+  // during this tile's MFMAs (every load of a tile in flight before the
+  // first LDS write, one memory latency per tile at most)
+  typename T::template Chunks<NWV * 64> ck[KT / 64], cv[KT / 64];
+  auto fetch_kv = [&](int kk0) {
+#pragma unroll
+    for (int h64 = 0; h64 < KT / 64; ++h64) {
+      T::template fetch<NWV * 64>(ck[h64], kb, a.k_sl, kk0 + 64 * h64, a.Lk, tid);
+      T::template fetch<NWV * 64>(cv[h64], vb, a.v_sl, kk0 + 64 * h64, a.Lk, tid);
+    }
+  };
+  if (klim > 0) fetch_kv(0);
   for (int k0 = 0; k0 < klim; k0 += KT) {
-    {
-      // every K / V load of the tile in flight before the first LDS write
-      typename T::template Chunks<NWV * 64> ck[KT / 64], cv[KT / 64];
 #pragma unroll
-      for (int h64 = 0; h64 < KT / 64; ++h64) {
-        T::template fetch<NWV * 64>(ck[h64], kb, a.k_sl, k0 + 64 * h64, a.Lk, tid);
-        T::template fetch<NWV * 64>(cv[h64], vb, a.v_sl, k0 + 64 * h64, a.Lk, tid);
-      }
-#pragma unroll
-      for (int h64 = 0; h64 < KT / 64; ++h64) {
-        T::template put<NWV * 64>(ldsK + h64 * T::BYTES, ck[h64], tid);
-        T::template put<NWV * 64>(ldsV + h64 * T::BYTES, cv[h64], tid);
-      }
+    for (int h64 = 0; h64 < KT / 64; ++h64) {
+      T::template put<NWV * 64>(ldsK + h64 * T::BYTES, ck[h64], tid);
+      T::template put<NWV * 64>(ldsV + h64 * T::BYTES, cv[h64], tid);
     }
     __syncthreads();
     if (k0 == 0) TDG_STAMP(1);
+    if (k0 + KT < klim) fetch_kv(k0 + KT);
     f32x4 s[NT16];
 #pragma unroll
     for (int t = 0; t < NT16; ++t) {
@@ -307,15 +312,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     const float* lse = a.lse + ((long long)b * a.H + h) * a.Lq;
     const float* del = a.delta + ((long long)b * a.H + h) * a.Lq;
     const int qstart = a.causal ? (k0 / QB) * QB : 0;
-    for (int q0 = qstart; q0 < a.Lq; q0 += QB) {
-      T::load(ldsQ, qb, a.q_sl, q0, a.Lq, tid);
-      T::load(ldsO, ob, a.do_sl, q0, a.Lq, tid);
+    // Q / dO / lse / delta of query block q0+QB are loaded into registers
+    // while block q0 is computed (register prefetch, single LDS buffer)
+    typename T::template Chunks<256> cq, co;
+    float lv = INFINITY, dlv = 0.f;
+    auto fetch_q = [&](int qq0) {
+      T::template fetch<256>(cq, qb, a.q_sl, qq0, a.Lq, tid);
+      T::template fetch<256>(co, ob, a.do_sl, qq0, a.Lq, tid);
       if (tid < QB) {
-        const int q = q0 + tid;
-        ldsL[tid] = q < a.Lq ? lse[q] : INFINITY;
-        ldsD[tid] = q < a.Lq ? del[q] : 0.f;
+        const int q = qq0 + tid;
+        lv = q < a.Lq ? lse[q] : INFINITY;
+        dlv = q < a.Lq ? del[q] : 0.f;
+      }
+    };
+    if (qstart < a.Lq) fetch_q(qstart);
+    for (int q0 = qstart; q0 < a.Lq; q0 += QB) {
+      T::template put<256>(ldsQ, cq, tid);
+      T::template put<256>(ldsO, co, tid);
+      if (tid < QB) {
+        ldsL[tid] = lv;
+        ldsD[tid] = dlv;
       }
       __syncthreads();
+      if (q0 + QB < a.Lq) fetch_q(q0 + QB);
       // S[q][key] and dP[q][key]: rows q = q0 + 16t + 4g + r, col key (lane)
       f32x4 p[4], ds[4];
 #pragma unroll
@@ -401,10 +420,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int i = 0; i < T::DT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // K / V of key block k0+KB in registers while block k0 is computed
+  typename T::template Chunks<256> ck, cv;
+  if (klim > 0) {
+    T::template fetch<256>(ck, kb, a.k_sl, 0, a.Lk, tid);
+    T::template fetch<256>(cv, vb, a.v_sl, 0, a.Lk, tid);
+  }
   for (int k0 = 0; k0 < klim; k0 += KB) {
-    T::load(ldsK, kb, a.k_sl, k0, a.Lk, tid);
-    T::load(ldsV, vb, a.v_sl, k0, a.Lk, tid);
+    T::template put<256>(ldsK, ck, tid);
+    T::template put<256>(ldsV, cv, tid);
     __syncthreads();
+    if (k0 + KB < klim) {
+      T::template fetch<256>(ck, kb, a.k_sl, k0 + KB, a.Lk, tid);
+      T::template fetch<256>(cv, vb, a.v_sl, k0 + KB, a.Lk, tid);
+    }
     f32x4 ds[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

@@ -206,7 +206,7 @@ def _ref_attn(q, k, v, kv_len, causal, scale):
 
 @pytest.mark.parametrize("hd", [16, 32, 64, 128])
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("Lq,Lk", [(128, 128), (70, 200), (1, 33), (37, 100)])
+@pytest.mark.parametrize("Lq,Lk", [(128, 128), (70, 200), (1, 33), (37, 100), (512, 512), (260, 390)])
 def test_attention_fwd_bwd(hd, causal, Lq, Lk):
     if causal and Lq != Lk:
         pytest.skip("causal self-attention only")
