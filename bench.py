@@ -96,7 +96,13 @@ def main() -> None:
     # eager calls between the segments (train/graphs.py; TDG_DP_GRAPH=0 runs
     # the step eagerly)
     use_graph = args.graph if args.graph >= 0 else int(dev.type == "cuda")
-    if use_graph:
+    dp_select = None
+    if use_graph and ddp is not None and ddp.active:
+        # segmented graph or eager step, whichever measures faster on this node
+        # (every rank takes the same decision; TDG_DP_AUTOSELECT=0: graph)
+        dp_select = step.choose_dp_mode(*batches[0])
+        use_graph = int(step.captured)
+    elif use_graph:
         use_graph = int(step.capture(*batches[0]))
     for i in range(args.warmup):
         step(*batches[i % len(batches)])
@@ -157,6 +163,7 @@ def main() -> None:
                 "parallelism": f"dp{world}",
                 "hip_graph": (("segmented" if step.segments is not None else "single")
                               if use_graph else False),
+                **({"dp_mode_select": dp_select} if dp_select else {}),
                 "grad_comm": args.grad_comm,
                 "defer_wgrad": step.rt.wgrad is not None,
                 "bucket_mb": args.bucket_mb,

@@ -235,9 +235,12 @@ class Trainer:
                 if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured:
                     # capture() restores the state its warm-up steps changed,
                     # so this batch is still trained exactly once (below)
-                    if not self.step_fn.capture(src, tgt) and info.chief:
-                        self.log("note: the data-parallel step runs eagerly (TDG_DP_GRAPH=0 or an "
-                                 "option that needs an uncapturable stream)")
+                    if self.ddp is not None and self.ddp.active:
+                        sel = self.step_fn.choose_dp_mode(src, tgt)
+                        if info.chief:
+                            self.log(f"data-parallel step mode: {sel}")
+                    elif not self.step_fn.capture(src, tgt) and info.chief:
+                        self.log("note: the step runs eagerly")
                     captured = True
                 self.timer.start()
                 self.step_fn(src, tgt)

@@ -13,7 +13,8 @@ replicas only when the host reads it (log points).
 from __future__ import annotations
 
 import os
-from typing import Optional, Tuple
+import time
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -42,6 +43,9 @@ ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 # (round 1 also had "full", the collectives captured inside one graph; it
 # failed capture under PyTorch 2.10's process-group watchdog and was removed)
 DP_GRAPH = os.environ.get("TDG_DP_GRAPH", "seg")
+# data parallel: time the segmented graph against the eager step once and keep
+# the faster (TrainStep.choose_dp_mode); 0 keeps the segmented graph
+DP_AUTOSELECT = os.environ.get("TDG_DP_AUTOSELECT", "1") != "0"
 
 
 class TrainStep:
@@ -208,6 +212,57 @@ class TrainStep:
             self.eager(*self._static)
         self.graph = g
         return True
+
+    def choose_dp_mode(self, src: torch.Tensor, tgt: torch.Tensor, steps: int = 8,
+                       rounds: int = 2, margin: float = 0.03) -> Dict[str, object]:
+        """Data parallel: capture the segmented graph, then time it against the
+        eager step on this batch (interleaved rounds, best per mode, MAX over
+        ranks so every rank takes the same decision) and keep the faster. The
+        segmented graph wins when the host is the bottleneck (eight ranks
+        sharing a node's CPUs: the eager step's enqueue costs about its GPU
+        time); the eager step wins when the host keeps ahead (on one MI355X
+        with a fast host the graph cuts cost ~0.3 ms/step, docs/PERF.md). The
+        training state is restored afterwards, so this trains nothing. Returns
+        {"mode": "seg" | "0", "seg_ms": .., "eager_ms": ..}."""
+        if not self.capture(src, tgt):
+            return {"mode": self.capture_mode()}
+        if not (self.ddp is not None and self.ddp.active and self.segments is not None) \
+                or not DP_AUTOSELECT:
+            return {"mode": "seg" if self.segments is not None else self.capture_mode()}
+        saved = self.snapshot()
+        dev = self.model.device
+        seg = self.segments
+
+        def timed(run) -> float:
+            for _ in range(2):
+                run()
+            torch.cuda.synchronize()
+            dist.barrier(group=self.ddp.group)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                run()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / steps
+
+        best = {"seg": float("inf"), "0": float("inf")}
+        for _ in range(rounds):
+            self.segments = seg
+            best["seg"] = min(best["seg"], timed(lambda: self(src, tgt)))
+            self.segments = None
+            best["0"] = min(best["0"], timed(lambda: self.eager(src, tgt)))
+        t = torch.tensor([best["seg"], best["0"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ddp.group)
+        seg_s, eager_s = float(t[0]), float(t[1])
+        self.restore(saved)
+        if eager_s < seg_s * (1.0 - margin):
+            self.segments = None
+            self._static = None
+            mode = "0"
+        else:
+            self.segments = seg
+            mode = "seg"
+        torch.cuda.synchronize()
+        return {"mode": mode, "seg_ms": round(seg_s * 1e3, 3), "eager_ms": round(eager_s * 1e3, 3)}
 
     def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         if not self.captured:

@@ -40,7 +40,7 @@ def _batches(dev):
     return out
 
 
-def _run(dev, graph, ddp_factory=None, fp8=False):
+def _run(dev, graph, ddp_factory=None, fp8=False, select_margin=None):
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.train.optim import Adam
@@ -58,7 +58,14 @@ def _run(dev, graph, ddp_factory=None, fp8=False):
     step = TrainStep(m, opt, ddp, workers=1, seed=11, fp8_state=fp8_state)
     bs = _batches(dev)
     losses = []
-    if graph:
+    if graph and select_margin is not None:
+        # measured choice between the segmented graph and the eager step; the
+        # margin forces either outcome. Neither the capture nor the timed
+        # steps may train anything.
+        sel = step.choose_dp_mode(*bs[0], steps=2, rounds=1, margin=select_margin)
+        step.selected = sel
+        assert opt.iterations == 0 and int(step.rt.ctr.item()) == 0
+    elif graph:
         assert step.capture(*bs[0], warmup=2)  # warm-up steps are rolled back
         assert opt.iterations == 0 and int(step.rt.ctr.item()) == 0
     for i in range(STEPS + 1):
@@ -107,8 +114,16 @@ def _dp_worker(rank, port, out, mode):
             # one issue per span + two wait points (backward's spans, the last span)
             assert st.segments.num_calls == len(st.ddp.last_buckets) + 2, st.segments.items
         res["graph" if graph else "eager"] = (f, l)
-    torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1]},
-               out)
+    # measured mode selection, each outcome forced by the margin
+    for name, margin, want in (("sel_eager", -10.0, "0"), ("sel_seg", 0.99, "seg")):
+        f, l, st = _run(info.device, True, mk, select_margin=margin)
+        assert st.selected["mode"] == want, st.selected
+        assert (st.segments is not None) == (want == "seg")
+        assert st.selected["seg_ms"] > 0 and st.selected["eager_ms"] > 0
+        res[name] = (f, l)
+    torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1],
+                "sef": res["sel_eager"][0], "ssf": res["sel_seg"][0], "sel": res["sel_eager"][1],
+                "ssl": res["sel_seg"][1]}, out)
     tdist.shutdown()
 
 
@@ -119,3 +134,7 @@ def test_dp_step_graph_matches_eager(tmp_path, mode):
     r = torch.load(out, weights_only=True)
     assert torch.equal(r["el"], r["gl"]), (r["el"], r["gl"])
     assert torch.equal(r["ef"], r["gf"])
+    # after a measured mode choice (either outcome) training is unchanged
+    for k in ("sef", "ssf"):
+        assert torch.equal(r["ef"], r[k]), k
+    assert torch.equal(r["el"], r["sel"]) and torch.equal(r["el"], r["ssl"])
