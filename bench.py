@@ -173,6 +173,8 @@ def main() -> None:
     if args.save_tuned and info.rank == 0:
         from tensorflow_distributed_on_gke_amd.ops import kernels as _kk
         _kk.save_tuned(args.save_tuned)
+    if ddp is not None:
+        ddp.close()
     tdist.shutdown()
 
 

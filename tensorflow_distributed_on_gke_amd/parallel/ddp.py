@@ -17,18 +17,24 @@ the last reduced offset and the frontier:
     the deferred weight-gradient GEMMs) once it is >= `min_mb`,
 so collective boundaries follow the real completion order of the step instead
 of a fixed bucket grid (a fixed grid straddling two flushes delays its
-collective to the later one). ProcessGroupNCCL (RCCL on ROCm) runs each
-collective on its own HIP stream, ordered after the producing kernels by an
-event, so communication overlaps the rest of backward; the optimizer's stream
-waits on the work handles (no host sync). Large spans (tens of MB) are what a
+collective to the later one). On the GPU each span's all-reduce is issued by a
+host thread (CommThread) on a communication stream once the compute stream has
+reached the span's issue point, so communication overlaps the rest of backward
+without the communication stream ever waiting on the compute stream on the
+GPU (that handoff costs the compute stream ~55 us per span on MI355X); the
+compute stream waits on the finished all-reduce device-side, and the host only
+waits until the collective has been enqueued. Large spans (tens of MB) are what a
 ring all-reduce over point-to-point xGMI needs to spread over RCCL's channels
 and the 7 links per GPU.
 """
 from __future__ import annotations
 
 import math
+import os
+import queue
+import threading
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -37,15 +43,64 @@ from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
 
 
+# Issue GPU collectives from a host thread (CommThread) instead of making the
+# communication stream wait on the compute stream (TDG_DP_COMM_THREAD=0: the
+# process group's own stream handoff)
+COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1") != "0"
+
+
+class CommThread:
+    """Issues the data-parallel collectives from one host thread, each once the
+    compute-stream event recorded at its issue point has completed, on a
+    communication stream that never waits on the compute stream on the GPU.
+
+    Why: on MI355X a stream waiting on an event still pending on another
+    stream costs the producing (compute) stream ~55 us per handoff -- 0.3 ms
+    per step for the five all-reduce spans of Transformer-base -- while the
+    reverse wait (compute waits for the finished all-reduce) and a plain event
+    record are cheap (scripts/seg_comm_probe.py, docs/ROADMAP.md). One thread
+    issues everything, so every rank issues its collectives in the same
+    order, as ProcessGroupNCCL requires."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.stream = torch.cuda.Stream(device)
+        self._q: "queue.Queue[Optional[Callable[[], None]]]" = queue.Queue()
+        self._t = threading.Thread(target=self._run, name="tdg-comm", daemon=True)
+        self._t.start()
+
+    def _run(self) -> None:
+        torch.cuda.set_device(self.device)
+        while True:
+            job = self._q.get()
+            if job is None:
+                return
+            job()
+
+    def submit(self, job: Callable[[], None]) -> None:
+        self._q.put(job)
+
+    def close(self) -> None:
+        if self._t.is_alive():
+            self._q.put(None)
+            self._t.join(timeout=60)
+
+
 class Pending:
     """Handle of an asynchronous collective issued through DataParallel.
     `work` is the process group's Work once the collective has been issued
-    (at replay time when the step is a segmented graph, train/graphs.py)."""
-    __slots__ = ("owner", "work")
+    (at replay time when the step is a segmented graph, train/graphs.py).
+    Thread-issued collectives also carry `issued` (set by the comm thread once
+    the collective is enqueued), `done` (event on the comm stream after it)
+    and `error`."""
+    __slots__ = ("owner", "work", "issued", "done", "error")
 
     def __init__(self, owner: "DataParallel"):
         self.owner = owner
         self.work = None
+        self.issued: Optional[threading.Event] = None
+        self.done = None
+        self.error: Optional[BaseException] = None
 
     def wait(self) -> None:
         """The current stream waits for the collective (device-side)."""
@@ -109,6 +164,11 @@ class DataParallel:
         # a train/graphs.SegmentedGraph while the step is being captured: the
         # collectives become host calls between graph segments
         self.recorder = None
+        # GPU collectives issued from a host thread (CommThread)
+        self._thread: Optional[CommThread] = None
+        if self.active and COMM_THREAD and store.flat.is_cuda and \
+                dist.get_backend(group) == "nccl":
+            self._thread = CommThread(store.flat.device)
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
         if self.active:
@@ -189,9 +249,32 @@ class DataParallel:
         is issued at replay, on the stream the graphs replay on)."""
         h = Pending(self)
         grp = self.group
+        th = self._thread
 
         def issue():
-            h.work = dist.all_reduce(t, group=grp, async_op=True)
+            if th is None:
+                h.work = dist.all_reduce(t, group=grp, async_op=True)
+                return
+            ready = torch.cuda.Event()
+            ready.record()  # the current (compute) stream: t is final here
+            h.issued = threading.Event()
+            h.error = None
+
+            def job():
+                try:
+                    ready.synchronize()
+                    with torch.cuda.stream(th.stream):
+                        w = dist.all_reduce(t, group=grp, async_op=True)
+                        w.wait()  # comm stream after the collective
+                        done = torch.cuda.Event()
+                        done.record(th.stream)
+                    h.work, h.done = w, done
+                except BaseException as e:  # surfaced by the waiter
+                    h.error = e
+                finally:
+                    h.issued.set()
+
+            th.submit(job)
 
         if self.recorder is not None:
             self.recorder.cut(issue)
@@ -199,11 +282,23 @@ class DataParallel:
             issue()
         return h
 
+    @staticmethod
+    def _wait_now(h: Pending) -> None:
+        """Current stream waits for the collective (device-side; the host only
+        waits until a thread-issued collective has been enqueued)."""
+        if h.issued is None:
+            h.work.wait()
+            return
+        h.issued.wait()
+        if h.error is not None:
+            raise RuntimeError("data-parallel collective failed on the comm thread") from h.error
+        torch.cuda.current_stream().wait_event(h.done)
+
     def _wait(self, h: Pending) -> None:
         if self.recorder is not None:
-            self.recorder.cut(lambda: h.work.wait())
+            self.recorder.cut(lambda: self._wait_now(h))
         else:
-            h.work.wait()
+            self._wait_now(h)
 
     def _on_ready(self, p: Param) -> None:
         self._ready[self._pos[p.index]] = True
@@ -223,7 +318,7 @@ class DataParallel:
     def _complete_many(self, bs: List[Bucket]) -> None:
         hs = [b.work[0] for b in bs]
         if self.recorder is not None:  # one host call between two graph segments
-            self.recorder.cut(lambda: [h.work.wait() for h in hs])
+            self.recorder.cut(lambda: [self._wait_now(h) for h in hs])
         else:
             for h in hs:
                 h.wait()
@@ -297,6 +392,12 @@ class DataParallel:
         if bad:
             raise RuntimeError(f"replica divergence: ranks {bad} differ from rank 0 "
                                f"({[tuple(v.tolist()) for v in allv]})")
+
+    def close(self) -> None:
+        """Stop the comm thread (all its collectives have been waited for)."""
+        if self._thread is not None:
+            self._thread.close()
+            self._thread = None
 
     def allreduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
