@@ -47,6 +47,9 @@ from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
 # communication stream wait on the compute stream (TDG_DP_COMM_THREAD=0: the
 # process group's own stream handoff)
 COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1") != "0"
+# seconds the host waits for the comm thread to enqueue a collective (a GPU
+# that never reaches the issue point would otherwise hang the step silently)
+COMM_ISSUE_TIMEOUT_S = float(os.environ.get("TDG_DP_ISSUE_TIMEOUT_S", "1800"))
 
 
 class CommThread:
@@ -289,7 +292,9 @@ class DataParallel:
         if h.issued is None:
             h.work.wait()
             return
-        h.issued.wait()
+        if not h.issued.wait(timeout=COMM_ISSUE_TIMEOUT_S):
+            raise RuntimeError(f"data-parallel collective not issued within {COMM_ISSUE_TIMEOUT_S:.0f} s "
+                               "(the compute stream never reached its issue point)")
         if h.error is not None:
             raise RuntimeError("data-parallel collective failed on the comm thread") from h.error
         torch.cuda.current_stream().wait_event(h.done)
