@@ -45,8 +45,9 @@ from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
 
 # Issue GPU collectives from a host thread (CommThread) instead of making the
 # communication stream wait on the compute stream (TDG_DP_COMM_THREAD=0: the
-# process group's own stream handoff)
-COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1") != "0"
+# process group's own stream handoff; "force": also over gloo with GPU tensors
+# -- the two-rank rehearsal on one GPU, tests/test_gpu_dp.py)
+COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1")
 # seconds the host waits for the comm thread to enqueue a collective (a GPU
 # that never reaches the issue point would otherwise hang the step silently)
 COMM_ISSUE_TIMEOUT_S = float(os.environ.get("TDG_DP_ISSUE_TIMEOUT_S", "1800"))
@@ -169,8 +170,8 @@ class DataParallel:
         self.recorder = None
         # GPU collectives issued from a host thread (CommThread)
         self._thread: Optional[CommThread] = None
-        if self.active and COMM_THREAD and store.flat.is_cuda and \
-                dist.get_backend(group) == "nccl":
+        if self.active and COMM_THREAD != "0" and store.flat.is_cuda and \
+                (dist.get_backend(group) == "nccl" or COMM_THREAD == "force"):
             self._thread = CommThread(store.flat.device)
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)

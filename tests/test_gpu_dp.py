@@ -40,11 +40,11 @@ def _batch(rank, i):
     return src, tgt
 
 
-def _worker(rank, world, port, out, opt_mode, loss_mode, graph):
+def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
                       TDG_DP_WAVE_TILES="37", TDG_DP_OVERLAP_OPT=opt_mode,
-                      TDG_DP_GRAPH=graph or "0")
+                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD=comm_thread)
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
@@ -57,6 +57,7 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph):
     m = Transformer(model_config("tiny", **CFG)).build(info.device, seed=1 + rank)
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     ddp = DataParallel(m.store, bucket_mb=1.0)
+    assert (ddp._thread is not None) == (comm_thread == "force")
     ddp.broadcast_params(0)
     step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
     assert step.global_mean == (loss_mode == "global_mean")
@@ -75,15 +76,20 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph):
     assert opt.iterations == STEPS
     torch.save({"flat": m.store.flat.cpu(), "loss": torch.stack(losses), "nb": len(ddp.last_buckets)},
                f"{out}.{rank}")
+    ddp.close()
     tdist.barrier()
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("opt_mode,loss_mode,graph", [("0", "replica_mean", ""), ("tail", "replica_mean", ""),
-                                                      ("tail", "global_mean", ""),
-                                                      ("tail", "replica_mean", "seg"),
-                                                      ("0", "global_mean", "seg")])
-def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode, graph, monkeypatch):
+@pytest.mark.parametrize("opt_mode,loss_mode,graph,comm_thread", [
+    ("0", "replica_mean", "", "1"), ("tail", "replica_mean", "", "1"),
+    ("tail", "global_mean", "", "1"), ("tail", "replica_mean", "seg", "1"),
+    ("0", "global_mean", "seg", "1"),
+    # the host comm thread (the RCCL default) driven over gloo: two ranks
+    ("tail", "replica_mean", "", "force"), ("tail", "replica_mean", "seg", "force"),
+    ("tail", "global_mean", "seg", "force")])
+def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode, graph, comm_thread,
+                                                  monkeypatch):
     from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
@@ -91,7 +97,7 @@ def test_gpu_dp2_rehearsal_matches_single_process(tmp_path, opt_mode, loss_mode,
 
     world = 2
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode, graph), nprocs=world,
+    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode, graph, comm_thread), nprocs=world,
                        join=True,
                        start_method="spawn")
     r0 = torch.load(out + ".0", weights_only=True)
