@@ -57,6 +57,8 @@ def cmd_train(args) -> int:
         print(f"Number of devices: {info.world}", flush=True)
     trainer = Trainer(settings, info, log=lambda m: print(m, flush=True))
     trainer.fit()
+    if trainer.ddp is not None:
+        trainer.ddp.close()
     tdist.shutdown()
     if settings.idle_after_train and not in_child:
         idle_forever()
