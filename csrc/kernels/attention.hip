@@ -254,28 +254,6 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
 #endif
 }
 
-// ============================================================================ delta = rowsum(dO*O)
-template <int HD>
-__global__ void attn_delta_kernel(AttnArgs a) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)a.B * a.H * a.Lq;
-  if (idx >= total) return;
-  const int q = (int)(idx % a.Lq);
-  const int h = (int)((idx / a.Lq) % a.H);
-  const int b = (int)(idx / ((long long)a.Lq * a.H));
-  const bf16_t* op = a.o + b * a.o_sb + (long long)q * a.o_sl + h * a.o_sh;
-  const bf16_t* dp = a.dout + b * a.do_sb + (long long)q * a.do_sl + h * a.do_sh;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < HD / 8; ++c) {
-    const short8_t x = *reinterpret_cast<const short8_t*>(op + 8 * c);
-    const short8_t y = *reinterpret_cast<const short8_t*>(dp + 8 * c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += bf2f((bf16_t)x[e]) * bf2f((bf16_t)y[e]);
-  }
-  a.delta[idx] = s;  // idx == (b*H + h)*Lq + q
-}
-
 // ============================================================================ dK, dV
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
@@ -413,7 +391,23 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   }
   const long long bh = ((long long)b * a.H + h) * a.Lq + qr;
   const float L = a.lse[bh];
-  const float D = a.delta[bh];
+  // delta = rowsum(dO * O) of this lane's query row, from the dO fragments
+  // already in registers and the matching O fragments (the 4 lane groups g
+  // hold disjoint head-dim slices); written for the dK/dV kernel, which runs
+  // after this one -- no separate delta pass over O and dO
+  float D = 0.f;
+  {
+    const bf16_t* opr = a.o + b * a.o_sb + (long long)qr * a.o_sl + h * a.o_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) {
+      const short8_t ov = gfrag<HD>(opr, qvalid, s, lane);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) D += bf2f((bf16_t)of[s][e]) * bf2f((bf16_t)ov[e]);
+    }
+    D += __shfl_xor(D, 16, 64);
+    D += __shfl_xor(D, 32, 64);
+    if (qvalid && g == 0) a.delta[bh] = D;
+  }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
   f32x4 dq[T::DT];
@@ -761,13 +755,11 @@ int bwd_hd(const AttnArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(attn_bwd_fused_kernel<HD>, dim3(a.B * a.H), dim3(512), lds, st, a);
     return 0;
   }
-  const long long rows = (long long)a.B * a.H * a.Lq;
-  hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
-                     a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
-                     2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
+  // dQ first: it also writes delta = rowsum(dO * O), which dK/dV reads
   hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, dim3(cdiv(a.Lq, QB), a.H, a.B), dim3(256),
                      2 * ATile<HD>::BYTES, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
+                     2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
   return 0;
 }
 template <int HD>
