@@ -367,12 +367,16 @@ class DataParallel:
         if self._upd_stream is not None:
             torch.cuda.current_stream(self._upd_stream.device).wait_stream(self._upd_stream)
         # Work.wait() orders the current stream after the collective. Two
-        # groups: the spans launched during backward (normally complete by
-        # now) and the span launched just above; the Adam of the first group
-        # runs while the last all-reduce is still in flight (the exposed
-        # tail). Grouping keeps a segmented graph at two wait points.
+        # groups, so a segmented graph keeps two wait points: the spans
+        # launched well before the end of backward (normally complete by now)
+        # and the last two -- the one launched at the last layer end, just
+        # before backward finishes, and the one launched just above. The Adam
+        # of the first group runs while those two all-reduces are in flight
+        # (and while the host thread issues them: the first wait does not
+        # block the host on a span issued moments ago).
         todo = [b for b in self.buckets if not b.updated]
-        for grp in (todo[:-1], todo[-1:]):
+        cut = -2 if len(todo) >= 3 else -1
+        for grp in (todo[:cut], todo[cut:]):
             if not grp:
                 continue
             self._complete_many(grp)
