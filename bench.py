@@ -32,7 +32,6 @@ from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel  # noqa:
 from tensorflow_distributed_on_gke_amd.train.optim import Adam  # noqa: E402
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep  # noqa: E402
 from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs  # noqa: E402
-from tensorflow_distributed_on_gke_amd.utils.gcpolicy import ManualGC  # noqa: E402
 
 METRIC = "tokens/sec (whole node), Transformer-base en-pt at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
@@ -107,9 +106,6 @@ def main() -> None:
     for i in range(args.warmup):
         step(*batches[i % len(batches)])
 
-    # manual GC (utils/gcpolicy.py): no cyclic-GC pass inside an eager step;
-    # its periodic collection stays inside the timed loop, as in training
-    mgc = ManualGC.from_env()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     tdist.barrier()
@@ -118,18 +114,18 @@ def main() -> None:
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(*batches[i % len(batches)])
-        mgc.step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     tdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    mgc.close()
 
-    if ddp is not None and info.rank == 0:
+    if ddp is not None:
+        # every rank reports its own decision and spans (they must agree)
         spans = [round((b.end - b.start) * 4 / 2 ** 20, 1) for b in ddp.last_buckets]
-        print(f"all-reduce spans per step (MB, launch order): {spans}", file=sys.stderr)
+        print(f"[rank {info.rank}/{world}] dp_mode_select={dp_select} comm_thread={ddp._thread is not None} "
+              f"all-reduce spans per step (MB, launch order): {spans}", file=sys.stderr, flush=True)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -43,10 +43,6 @@ int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, i
 int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable, long long* acc,
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
-int tdg_gemm_ln(const void* A, int lda, const void* W, int ldw, const float* bias, const void* X,
-                int ldx, const float* gamma, const float* beta, void* Y, void* H, float* mean,
-                float* rstd, int M, int K, int D, float p, uint64_t seed, const long long* ctr,
-                uint64_t site, float eps, hipStream_t st);
 int tdg_count_tokens(const void* labels, int lab64, int M, float* out, hipStream_t st);
 int tdg_prep_batch(const void* src, int S, const void* tgt, int T1, int B, int lab64, void* tgt_in,
                    void* labels, int* src_len, int* tgt_len, float* ntok, long long* ctr,
@@ -56,8 +52,6 @@ int tdg_colsum_grouped(const void* const* X, float* const* out, int G, float* pa
 int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C, int G, int M,
                      int N, int K, int lda, int ldb, int ldc, int a_kc, int b_kc, int out_f32,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
-void tdg_set_gemm256_pp(int on);
-int tdg_get_gemm256_pp();
 int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                     const int* shapes, int K, int a_kc, int b_kc, int out_f32, float alpha,
                     float beta, float* const* bias_out, hipStream_t st);
@@ -78,7 +72,6 @@ int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, 
              float grad_scale, float weight_decay, int sched, int zero_grad, int inc_step,
              hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
-int tdg_cu_hog(const void* buf, float* out, int nblocks, int iters, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
 }
@@ -373,37 +366,6 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
 // Fused output projection + bias + dropout + residual + LayerNorm:
 // y = LN(x + dropout(a @ w^T + bias)). Returns 0, or a negative code when the
 // shape is not covered (nothing launched; the caller runs GEMM + ln_fwd).
-int64_t gemm_ln(const Tensor& a, const Tensor& w, const Tensor& bias, const Tensor& x,
-                const Tensor& gamma, const Tensor& beta, const Tensor& y, const Tensor& hsave,
-                const Tensor& mean, const Tensor& rstd, double p, int64_t seed,
-                const optional<Tensor>& ctr, int64_t site, double eps) {
-  check_bf16(a, "a");
-  check_bf16(w, "w");
-  check_bf16(x, "x");
-  check_bf16(y, "y");
-  check_bf16(hsave, "hsave");
-  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && x.dim() == 2, "gemm_ln: 2-D a, w, x");
-  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && x.stride(1) == 1, "gemm_ln: row-major");
-  const int64_t M = a.size(0), K = a.size(1), D = w.size(0);
-  TORCH_CHECK(w.size(1) == K && x.size(0) == M && x.size(1) == D, "gemm_ln: shapes");
-  TORCH_CHECK(y.is_contiguous() && hsave.is_contiguous() && y.numel() == M * D &&
-                  hsave.numel() == M * D, "gemm_ln: y / hsave must be contiguous [M, D]");
-  for (const Tensor* t : {&bias, &gamma, &beta}) {
-    check_f32(*t, "bias/gamma/beta");
-    TORCH_CHECK(t->numel() == D && t->is_contiguous(), "gemm_ln: vectors must hold D floats");
-  }
-  for (const Tensor* t : {&mean, &rstd}) {
-    check_f32(*t, "mean/rstd");
-    TORCH_CHECK(t->numel() == M, "gemm_ln: mean/rstd shape");
-  }
-  c10::DeviceGuard g(a.device());
-  return tdg_gemm_ln(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0),
-                     bias.data_ptr<float>(), x.data_ptr(), (int)x.stride(0), gamma.data_ptr<float>(),
-                     beta.data_ptr<float>(), y.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(),
-                     rstd.data_ptr<float>(), (int)M, (int)K, (int)D, (float)p, (uint64_t)seed,
-                     ctr_ptr(ctr), (uint64_t)site, (float)eps, stream_of(a));
-}
-
 void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Tensor& rstd,
             const Tensor& gamma, const Tensor& dh, const optional<Tensor>& ds,
             const optional<Tensor>& dres, const Tensor& dgamma, const Tensor& dbeta,
@@ -857,15 +819,6 @@ void transpose_grouped(const std::vector<Tensor>& srcs, const std::vector<Tensor
 }
 
 // diagnostic: nblocks workgroups streaming 1 MiB each of buf, iters times
-void cu_hog(const Tensor& buf, const Tensor& out, int64_t nblocks, int64_t iters) {
-  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous() && buf.nbytes() >= (size_t)nblocks << 20,
-              "cu_hog: buf needs nblocks MiB");
-  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= nblocks, "cu_hog: out");
-  check_err(tdg_cu_hog(buf.data_ptr(), out.data_ptr<float>(), (int)nblocks, (int)iters,
-                       stream_of(buf)),
-            "tdg cu_hog");
-}
-
 void to_bf16(const Tensor& p, const Tensor& o) {
   check_f32(p, "p");
   check_bf16(o, "o");
@@ -885,8 +838,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),
         py::arg("bias_out") = std::vector<c10::optional<Tensor>>{});
   m.def("colsum_grouped", &colsum_grouped);
-  m.def("set_gemm256_pp", [](bool on) { tdg_set_gemm256_pp(on ? 1 : 0); });
-  m.def("get_gemm256_pp", []() { return tdg_get_gemm256_pp() != 0; });
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_scale_update", &fp8_scale_update);
@@ -896,7 +847,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_probs", &attn_probs);
   m.def("ln_fwd", &ln_fwd);
-  m.def("gemm_ln", &gemm_ln);
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
@@ -909,6 +859,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("reduce_partials_multi", &reduce_partials_multi);
   m.def("to_bf16", &to_bf16);
-  m.def("cu_hog", &cu_hog);
   m.attr("ARCH") = "gfx950";
 }

@@ -209,35 +209,6 @@ extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, lo
   return 0;
 }
 
-// Diagnostic load generator (scripts/cu_contention.py): `nblocks`
-// workgroups stream their own 1 MiB slices of `buf` `iters` times -- stands in
-// for the RCCL workgroups that occupy CUs while a multi-GPU step's all-reduce
-// overlaps backward, so the step's sensitivity to losing those CUs can be
-// measured on one GPU.
-__global__ __launch_bounds__(256) void cu_hog_kernel(const float4* __restrict__ buf,
-                                                     float* __restrict__ out, int iters) {
-  const float4* b = buf + (size_t)blockIdx.x * (1 << 16);  // 1 MiB per block
-  float acc = 0.f;
-  if (iters < 0) {  // occupancy only: hold the CU without memory traffic
-    for (int it = 0; it < -iters; ++it) __builtin_amdgcn_s_sleep(127);
-    if (acc == 1234.5f) out[blockIdx.x] = acc;
-    return;
-  }
-  for (int it = 0; it < iters; ++it) {
-#pragma unroll 4
-    for (int i = threadIdx.x; i < (1 << 16); i += 256) {
-      const float4 v = b[i];
-      acc += v.x + v.y + v.z + v.w;
-    }
-  }
-  if (acc == 1234.5f) out[blockIdx.x] = acc;
-}
-
-extern "C" int tdg_cu_hog(const void* buf, float* out, int nblocks, int iters, hipStream_t st) {
-  hipLaunchKernelGGL(cu_hog_kernel, dim3(nblocks), dim3(256), 0, st, (const float4*)buf, out, iters);
-  return 0;
-}
-
 extern "C" int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st) {
   const int blocks = (int)std::min<long long>(8192, (n + 255) / 256);
   hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p,

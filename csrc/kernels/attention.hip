@@ -29,6 +29,32 @@
 namespace tdg {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+// Key window and logit scale of batch row b. A row with NO valid key
+// (kv_len == 0: an all-PAD sequence) gets the reference's numerics: its
+// padding mask adds -1e9 to every logit, which in fp32 leaves them all equal
+// (transformer_model.py:101-105), so the softmax is uniform over ALL Lk keys
+// (padding included) -- reproduced by attending to all Lk keys with a zero
+// logit scale for P. The backward is TF's autograd of that graph: dS =
+// P (dP - delta) with the uniform P, and dQ / dK keep the real scale (the
+// mask add passes the gradient through). In causal attention such a row's
+// look-ahead mask is covered by the padding mask too (the reference combines
+// them with a maximum, transformer_model.py:361-362): all keys, causal off.
+__device__ __forceinline__ void key_window(const AttnArgs& a, int b, int& klim, float& scale,
+                                           bool& causal) {
+  klim = a.Lk;
+  scale = a.scale;
+  causal = a.causal != 0;
+  if (a.kv_len) {
+    const int n = a.kv_len[b];
+    if (n > 0) {
+      klim = min(klim, n);
+    } else {
+      scale = 0.f;
+      causal = false;
+    }
+  }
+}
 constexpr int QB = 64;  // rows per workgroup
 constexpr int KB = 64;  // keys per tile
 
@@ -139,9 +165,11 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
   const int qrow = q0 + 16 * w + cl;
   const bool qvalid = qrow < a.Lq;
-  int klim = a.Lk;
-  if (a.kv_len) klim = min(klim, a.kv_len[b]);
-  if (a.causal) klim = min(klim, q0 + QBW);
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q0 + QBW);
 
   TDG_STAMP(0);
   const bf16_t* qp = a.q + b * a.q_sb + (long long)min(qrow, a.Lq - 1) * a.q_sl + h * a.q_sh;
@@ -151,7 +179,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
 
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
-  const float c = a.scale * LOG2E;
+  const float c = scl * LOG2E;
 
   f32x4 oacc[T::DT];
 #pragma unroll
@@ -194,7 +222,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + 16 * t + 4 * g + r;
-        const bool ok = key < klim && (!a.causal || key <= qrow);
+        const bool ok = key < klim && (!causal || key <= qrow);
         const float v = ok ? s[t][r] * c : -INFINITY;
         s[t][r] = v;
         tmax = fmaxf(tmax, v);
@@ -266,10 +294,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KB;
   const int key = k0 + 16 * w + cl;
-  int klim = a.Lk;
-  if (a.kv_len) klim = min(klim, a.kv_len[b]);
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
   const bool kvalid = key < klim;
-  const float c = a.scale * LOG2E;
+  const float c = scl * LOG2E;
 
   f32x4 dk[T::DT], dv[T::DT];
 #pragma unroll
@@ -289,7 +319,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
     const float* lse = a.lse + ((long long)b * a.H + h) * a.Lq;
     const float* del = a.delta + ((long long)b * a.H + h) * a.Lq;
-    const int qstart = a.causal ? (k0 / QB) * QB : 0;
+    const int qstart = causal ? (k0 / QB) * QB : 0;
     // Q / dO / lse / delta of query block q0+QB are loaded into registers
     // while block q0 is computed (register prefetch, single LDS buffer)
     typename T::template Chunks<256> cq, co;
@@ -327,7 +357,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int ql = 16 * t + 4 * g + r;
           const int q = q0 + ql;
-          const bool ok = kvalid && q < a.Lq && (!a.causal || key <= q);
+          const bool ok = kvalid && q < a.Lq && (!causal || key <= q);
           const float pv = ok ? exp2f(sv[r] * c - ldsL[ql]) : 0.f;
           p[t][r] = pv;
           ds[t][r] = pv * (dpv[r] - ldsD[ql]);
@@ -376,10 +406,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QB;
   const int qrow = q0 + 16 * w + cl;
   const bool qvalid = qrow < a.Lq;
-  int klim = a.Lk;
-  if (a.kv_len) klim = min(klim, a.kv_len[b]);
-  if (a.causal) klim = min(klim, q0 + QB);
-  const float c = a.scale * LOG2E;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q0 + QB);
+  const float c = scl * LOG2E;
   const int qr = min(qrow, a.Lq - 1);
   const bf16_t* qp = a.q + b * a.q_sb + (long long)qr * a.q_sl + h * a.q_sh;
   const bf16_t* dop = a.dout + b * a.do_sb + (long long)qr * a.do_sl + h * a.do_sh;
@@ -440,7 +472,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + 16 * t + 4 * g + r;
-        const bool ok = qvalid && key < klim && (!a.causal || key <= qrow);
+        const bool ok = qvalid && key < klim && (!causal || key <= qrow);
         const float pv = ok ? exp2f(sv[r] * c - L) : 0.f;
         ds[t][r] = pv * (dpv[r] - D);
       }
@@ -496,9 +528,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh % a.H;
-  int klim = a.Lk;
-  if (a.kv_len) klim = min(klim, a.kv_len[b]);
-  const float c = a.scale * LOG2E;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  const float c = scl * LOG2E;
 
   // ---- prologue. Every global load is issued before any is used (one
   // memory latency): this wave's K / V register fragments for phase 1, the
@@ -575,7 +609,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
-      const bool live = 16 * t < a.Lq && (!a.causal || 16 * t + 15 >= 16 * w);  // uniform
+      const bool live = 16 * t < a.Lq && (!causal || 16 * t + 15 >= 16 * w);  // uniform
       if (live) {
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
@@ -590,7 +624,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = 16 * t + 4 * g + r;
-        const bool ok = live && kvalid && q < a.Lq && (!a.causal || key <= q);
+        const bool ok = live && kvalid && q < a.Lq && (!causal || key <= q);
         pv[r] = ok ? exp2f(sv[r] * c - l4[r]) : 0.f;
         dv4[r] = pv[r] * (dpv[r] - d4[r]);
       }
@@ -681,9 +715,11 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
   const int q = (int)(row % a.Lq);
   const int h = (int)((row / a.Lq) % a.H);
   const int b = (int)(row / ((long long)a.Lq * a.H));
-  int klim = a.Lk;
-  if (a.kv_len) klim = min(klim, a.kv_len[b]);
-  if (a.causal) klim = min(klim, q + 1);
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q + 1);
   const bf16_t* qp = a.q + b * a.q_sb + (long long)q * a.q_sl + h * a.q_sh;
   float qv[HD];
 #pragma unroll
@@ -695,7 +731,7 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
     float s = 0.f;
 #pragma unroll
     for (int d = 0; d < HD; ++d) s += qv[d] * bf2f(kp[d]);
-    s *= a.scale;
+    s *= scl;
     out[k] = s;
     mx = fmaxf(mx, s);
   }
@@ -716,11 +752,6 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 using namespace tdg;
 
 namespace {
-bool getenv_flag(const char* name) {
-  const char* v = std::getenv(name);
-  return v != nullptr && v[0] != '\0' && v[0] != '0';
-}
-
 template <int HD>
 int fwd_hd(const AttnArgs& a, hipStream_t st) {
   // (64 queries per workgroup for Lq > 64 -- twice the workgroups, K / V
@@ -743,8 +774,7 @@ constexpr int fused_bwd_lds() {
 
 template <int HD>
 int bwd_hd(const AttnArgs& a, hipStream_t st) {
-  static const bool split_only = getenv_flag("TDG_ATTN_BWD_SPLIT");
-  if (a.Lq <= 128 && a.Lk <= 128 && !split_only) {
+  if (a.Lq <= 128 && a.Lk <= 128) {
     constexpr int lds = fused_bwd_lds<HD>();
     static bool attr = false;
     if (!attr) {

@@ -11,7 +11,7 @@
 // phase durations: prologue (entry -> first K tile in LDS), main loop,
 // epilogue store issue, store drain, plus the launch skew (spread of the
 // workgroups' entry times) and the whole kernel span.
-#include "../kernels/gemm.hip"
+#include "../kernels/gemm_impl.h"
 
 #include <hip/hip_runtime.h>
 

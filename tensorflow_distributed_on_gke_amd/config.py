@@ -84,6 +84,11 @@ class Settings:
     profile_steps: int = 5  # active profiled steps (after 1 wait + 1 warm-up step)
     kill_at_step: int = -1  # fault injection (tests): global step at which to exit
     kill_rank: int = -1  # rank that exits (-1: the last rank)
+    # "step": exit after the step; "backward": exit in the middle of that
+    # step's backward, once half of the gradients are final (peers are then
+    # blocked inside a gradient all-reduce; eager steps only -- a captured
+    # step runs no Python callbacks)
+    kill_point: str = "step"
     # "replica_mean": the reference's per-replica token mean / workers
     # (transformer_model.py:11-17); "global_mean": sum of all replicas' token
     # losses / all replicas' label count (equal to the single-process loss on

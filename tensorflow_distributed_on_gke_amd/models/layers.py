@@ -33,7 +33,6 @@ Reference semantics (distributed_training_transformer/transformer_model.py):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -41,13 +40,12 @@ import torch
 
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
-from tensorflow_distributed_on_gke_amd.ops.streams import offload
 from tensorflow_distributed_on_gke_amd.ops import fp8, philox
 
 LN_EPS = 1e-6
 # deferred weight gradients as ragged 256x256-tile launches (else per-shape
 # grouped launches of the tile table)
-RAGGED_WGRAD = os.environ.get("TDG_WGRAD_RAGGED", "1") != "0"
+RAGGED_WGRAD = True
 
 
 @dataclass
@@ -294,28 +292,19 @@ def _wgrad(rt: RunCtx, dy2, x2, N: int, w: Param, b: Optional[Param] = None) -> 
     if rt.wgrad is not None:
         rt.wgrad.add(dy2, x2, N, w, b, bt, rt)
         return
-    with offload(dy2, x2):
-        K.linear_wgrad(dy2, x2, N, w.grad, bt)
-        if b is not None:
-            K.colsum(dy2, N, b.grad, bt)
-        _ready(rt, w, *([b] if b is not None else []))
+    K.linear_wgrad(dy2, x2, N, w.grad, bt)
+    if b is not None:
+        K.colsum(dy2, N, b.grad, bt)
+    _ready(rt, w, *([b] if b is not None else []))
 
 
 # =============================================================================== LN helpers
 def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int, rt: RunCtx):
-    """GPU block tail y = LN(x + dropout(a2 @ w^T + b)) -> (y, saved): one fused
-    GEMM + LayerNorm launch when the shape is covered (ops.kernels.gemm_ln),
-    else the output-projection GEMM then _ln_fwd (same results bitwise)."""
-    fp8_ln = rt.fp8 is not None and rt.fp8.ln_slots.get(id(gamma)) is not None
-    if not fp8_ln:
-        x2 = x.reshape(-1, x.shape[-1])
-        if K.gemm_ln_ok(a2, w.compute, x2):
-            r = K.gemm_ln(a2, w.compute, b.master, x2, gamma.master, beta.master, rt.p, rt.seed,
-                          rt.ctr, site)
-            if r is not None:
-                y, h, mean, rstd = r
-                return y.view(x.shape), (h.view(x.shape), mean, rstd, None)
-    s = K.linear_fwd(a2, w.compute, b.master, bias_lp=b.compute)
+    """GPU block tail y = LN(x + dropout(a2 @ w^T + b)) -> (y, saved): the
+    output-projection GEMM (bias fused) then the fused dropout + residual +
+    LayerNorm kernel. (A single fused GEMM + LayerNorm launch measured slower
+    on MI355X: every workgroup then streams all of W; csrc/lab/gemm_ln.hip.)"""
+    s = K.linear_fwd(a2, w.compute, b.master)
     return _ln_fwd(x, s.view(x.shape), gamma, beta, site, rt)
 
 
@@ -394,10 +383,9 @@ class EmbedFn(torch.autograd.Function):
         table, rt = ctx.table, ctx.rt
         if dout.is_cuda:
             dc = dout.contiguous()
-            with offload(tok, dc):
-                K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site,
-                            accumulate=rt.accumulate)
-                _ready(rt, table)
+            K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site,
+                        accumulate=rt.accumulate)
+            _ready(rt, table)
             return None, None, None, None, None, None
         else:
             g = dout * ctx.ks if ctx.ks is not None else dout
@@ -455,7 +443,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
         if x.is_cuda:
             qkv = rt.fp8.linear(x2, wqkv, bqkv) if rt.fp8 is not None else None
             if qkv is None:
-                qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master, bias_lp=bqkv.compute)  # [M, 3d]
+                qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
             o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
             s = None  # projection fused with the LayerNorm below
@@ -525,7 +513,7 @@ class CrossKVFn(torch.autograd.Function):
         if enc.is_cuda:
             kv = rt.fp8.linear(e2.contiguous(), wkv, bkv) if rt.fp8 is not None else None
             if kv is None:
-                kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master, bias_lp=bkv.compute)
+                kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
         else:
             kv = e2 @ wkv.master.t() + bkv.master
         return kv.view(B, S, -1)
@@ -580,7 +568,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
         if x.is_cuda:
             q = rt.fp8.linear(x2, wq, bq) if rt.fp8 is not None else None
             if q is None:
-                q = K.linear_fwd(x2, wq.compute, bq.master, bias_lp=bq.compute)
+                q = K.linear_fwd(x2, wq.compute, bq.master)
             o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
                                 False)
             s = None  # projection fused with the LayerNorm below
@@ -663,9 +651,9 @@ class FFNBlockFn(torch.autograd.Function):
                 x8 = fp8.quantize(x2, st.meta, xs)
             x8 = x8.view(x2.shape)
             h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs)
-            f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2, bias_lp=b2.compute)
+            f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2)
         elif x.is_cuda:
-            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True, bias_lp=b1.compute)
+            h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
             f = None  # second projection fused with the LayerNorm below
         else:
             h = torch.relu(x2 @ w1.master.t() + b1.master)

@@ -15,7 +15,6 @@ kernels.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -28,7 +27,6 @@ from tensorflow_distributed_on_gke_amd.models.params import (ParamStore, TFSlot,
                                                               glorot_blocks, glorot_uniform,
                                                               uniform)
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
-from tensorflow_distributed_on_gke_amd.ops.streams import join, offload
 
 PAD_ID = 0
 
@@ -160,9 +158,9 @@ class DecoderLayer:
                                 self.ln3.beta, self.site3, rt)
 
 
-TRANSPOSED_FFN_DGRAD = os.environ.get("TDG_FFN_DGRAD_T", "1") != "0"
+TRANSPOSED_FFN_DGRAD = True
 # smallest d_model that keeps W2^T for the FFN relu-backward dgrad
-TRANSPOSED_FFN_MIN_D = int(os.environ.get("TDG_FFN_DGRAD_T_MIN_D", "1024"))
+TRANSPOSED_FFN_MIN_D = 1024
 
 
 def seq_lengths(tok: torch.Tensor, check: bool = True) -> torch.Tensor:
@@ -374,6 +372,4 @@ class Transformer:
         if rt.wgrad is not None:
             rt.wgrad.flush()
             rt.wgrad.step_done()
-        if dev.type == "cuda":
-            join(dev)  # weight gradients are final when this returns
         return step_out

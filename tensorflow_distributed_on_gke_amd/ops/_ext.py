@@ -4,8 +4,9 @@
 I/O, CRC32C, data loader). Both are built in-tree by `_build.py`.
 
 GPU ops never fall back to PyTorch: if `_C` is missing or was built for another
-architecture, the first GPU op raises. CPU tensors take the reference path in
-`ops/reference.py` (used by the CPU test-suite and the tiny CPU config).
+architecture, the first GPU op raises. CPU tensors take the plain-PyTorch
+reference paths inside the layer ops (`models/layers.py`, e.g.
+`_ref_attn_fwd`), used by the CPU test-suite and the tiny CPU config.
 """
 from __future__ import annotations
 

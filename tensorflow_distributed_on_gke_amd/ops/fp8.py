@@ -34,8 +34,6 @@ class Fp8Meta:
     def __init__(self, device, capacity: int = 256, margin: int = 0):
         self.device = torch.device(device)
         self.scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
-        # 1 / scale: the dequantisation factors the library fp8 GEMM takes
-        self.inv_scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
         # [slot, 64]: producers spread their atomics over 64 words (AMAX_SPREAD)
         self.amax = torch.zeros(capacity, 64, dtype=torch.int32, device=self.device)
         self.margin = margin
@@ -53,14 +51,10 @@ class Fp8Meta:
     def a(self, i: int) -> torch.Tensor:
         return self.amax[i]
 
-    def inv(self, i: int) -> torch.Tensor:
-        return self.inv_scale[i:i + 1]
-
     def update(self) -> None:
         n = len(self.names)
         if n:
             C().fp8_scale_update(self.scale[:n], self.amax[:n], float(2 ** self.margin))
-            torch.reciprocal(self.scale[:n], out=self.inv_scale[:n])
 
     def amax_values(self) -> torch.Tensor:
         return self.amax[: len(self.names)].view(torch.float32).amax(dim=1)
@@ -78,59 +72,51 @@ def dequantize(x8: torch.Tensor, scale: float) -> torch.Tensor:
     return x8.float() / scale
 
 
-LIBRARY = -1  # fp8 "config": hipBLASLt via torch._scaled_mm (per-tensor scales)
-
-
 def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
-             out8_slot: Optional[int] = None, cfg: Optional[int] = None,
-             bias_lp: Optional[torch.Tensor] = None
+             out8_slot: Optional[int] = None, cfg: Optional[int] = None
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """y[M,N] = dequant(a8[M,K] @ b8[N,K]^T) + bias (relu), bf16; with
-    out8_slot also y8 = e4m3(y * scale[out8_slot]) (amax recorded). bias_lp
-    (the bias's bf16 copy) lets the tuner also try hipBLASLt's fp8 GEMM for
-    plain / bias epilogues without an fp8 output."""
+    """y[M,N] = dequant(a8[M,K] @ b8[N,K]^T) + bias (relu), bf16, on the
+    block-scaled e4m3 MFMA (csrc/kernels/fp8.hip); with out8_slot also
+    y8 = e4m3(y * scale[out8_slot]) (amax recorded)."""
     M, Kd = a8.shape
     N = b8.shape[0]
     y8 = torch.empty(M, N, dtype=FP8, device=a8.device) if out8_slot is not None else None
     epi = 2 if relu else (1 if bias is not None else 0)
-    lib_ok = y8 is None and epi != 2 and (epi == 0 or bias_lp is not None)
-    out = {}
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device)
 
     def run(c):
-        if c == LIBRARY:
-            if not lib_ok:
-                raise RuntimeError("library fp8 GEMM not applicable")
-            out["y"] = torch._scaled_mm(a8, b8.t(), scale_a=meta.inv(ia), scale_b=meta.inv(ib),
-                                        bias=bias_lp if epi == 1 else None,
-                                        out_dtype=torch.bfloat16)
-            return
-        y = out.get("own")
-        if y is None:
-            y = out["own"] = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device)
         C().gemm_fp8(a8, b8, y, bias, meta.s(ia), meta.s(ib), y8,
                      meta.s(out8_slot) if y8 is not None else None,
                      meta.a(out8_slot) if y8 is not None else None,
                      M, N, Kd, a8.stride(0), b8.stride(0), N, N, epi, c)
-        out["y"] = y
 
     if cfg is None:
-        key = (M, N, Kd, epi, y8 is not None, lib_ok)
+        key = (M, N, Kd, epi, y8 is not None)
         cfg = _TUNED.get(key)
         if cfg is None:
             if K.AUTOTUNE and a8.is_cuda and not torch.cuda.is_current_stream_capturing():
-                cfg = _autotune(run, lib_ok)
+                cfg = _autotune(run)
             else:
-                cfg = 0 if M * N >= 256 * 128 * 128 else 5
+                cfg = choose_fp8(M, N, Kd)
             _TUNED[key] = cfg
     run(cfg)
-    return out["y"], y8
+    return y, y8
 
 
-def _autotune(run, lib_ok: bool = False) -> int:
+def choose_fp8(M: int, N: int, Kd: int) -> int:
+    """fp8 tile config without a timed search (csrc/kernels/fp8.hip table):
+    the largest tile that still gives every CU a tile."""
+    if -(-M // 256) * -(-N // 128) >= K.NUM_CU:
+        return 3  # 256x128, 8 waves
+    if -(-M // 128) * -(-N // 128) >= K.NUM_CU:
+        return 4  # 128x128, 8 waves
+    return 5
+
+
+def _autotune(run) -> int:
     times = {}
-    cands = list(_CANDS) + ([LIBRARY] if lib_ok else [])
     for rnd in range(2):
-        for c in cands:
+        for c in _CANDS:
             try:
                 run(c)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -231,7 +217,7 @@ class Fp8State:
         x8 = self.stash.pop(xs, None)
         if x8 is None:
             x8 = quantize(x2, self.meta, xs)
-        y, _ = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws, bias_lp=b.compute)
+        y, _ = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws)
         return y
 
     def after_step(self) -> None:

@@ -54,39 +54,44 @@ def set_gemm_config(M: int, N: int, K: int, a_kc: bool, b_kc: bool, cfg: int, sp
 
 
 def choose_gemm(M: int, N: int, K: int, a_kc: bool = True, b_kc: bool = True) -> Tuple[int, int]:
-    """Heuristic (tile config, split-K) when no autotuned entry exists.
-    Measured on MI355X (scripts/bench_gemm.py, profiles/gemm_bench.txt): the
-    64x128 / 64x64 4-wave tiles win on these skinny training shapes; weight
-    gradients (K = tokens, small output) need split-K to fill 256 CUs."""
+    """Tile config (and split-K) for a shape with no tuned entry -- no timed
+    search at run time. From the in-tree sweep on MI355X
+    (scripts/gemm_vs_blas.py, profiles/gemm/r3_tile_sweep_*.txt): 256x256
+    tiles once they fill the chip (>= 192 tiles, K % 64 == 0); for the
+    d_model-wide dgrads (N = 1024) 128x256 tiles, 8 waves; otherwise 128x128
+    tiles, 8 waves, 3-4 stages. Weight gradients (K = tokens, small output,
+    normally the ragged launch) split K to fill 256 CUs."""
     o = _CFG_OVERRIDE.get((M, N, K, a_kc, b_kc))
     if o is not None:
         return o
     if not a_kc and not b_kc:  # weight gradient: split K (= tokens)
-        t64 = math.ceil(M / 64) * math.ceil(N / 64)
+        t128 = math.ceil(M / 128) * math.ceil(N / 128)
         splits = 1
-        while t64 * splits < 2 * NUM_CU and K // (splits * 2) >= 512:
+        while t128 * splits < NUM_CU and K // (splits * 2) >= 512:
             splits *= 2
-        return 8, splits
-    if math.ceil(M / 64) * math.ceil(N / 128) >= NUM_CU:
-        return 7, 1
-    return 8, 1
+        return 0, splits
+    if K % 64 == 0 and math.ceil(M / 256) * math.ceil(N / 256) >= 192:
+        return 12, 1
+    if a_kc and not b_kc and N >= 1024 and math.ceil(M / 128) * math.ceil(N / 256) >= NUM_CU:
+        return 6, 1
+    return (13, 1) if not b_kc else (4, 1)
 
 
 _TUNED: Dict[tuple, Tuple[int, int]] = {}
-AUTOTUNE = True
-_CANDIDATES = [(0, 1), (2, 1), (7, 1), (8, 1), (4, 1), (10, 1), (12, 1), (13, 1), (14, 1)]
+# Timed tile search for shapes missing from the tuned table: a tool
+# (TDG_GEMM_AUTOTUNE=1, scripts/tune_in_model.py), never on in training runs,
+# where results must not depend on the timing noise of the box
+AUTOTUNE = os.environ.get("TDG_GEMM_AUTOTUNE", "0") == "1"
+_CANDIDATES = [(0, 1), (4, 1), (5, 1), (6, 1), (9, 1), (10, 1), (12, 1), (13, 1), (14, 1)]
 
 
-def _autotune(key, run, blas_ok=False) -> Tuple[int, int]:
-    """Time the candidate tile configs once for this problem (3 reps each, HIP
-    events on the current stream) and keep the fastest. Plain GEMMs also try
-    the library (hipBLASLt) path."""
+def _autotune(key, run) -> Tuple[int, int]:
+    """Time the candidate tile configs once for this problem (HIP events on
+    the current stream, two interleaved rounds, min) and keep the fastest."""
     M, N, K, a_kc, b_kc = key[:5]
     cands = list(_CANDIDATES)
     if not a_kc and not b_kc:
         cands = [(c, s) for c in (0, 7, 8) for s in (1, 2, 4, 8) if K // s >= 256] + [(12, 1)]
-    if blas_ok:
-        cands.append(BLAS)
     times: Dict[Tuple[int, int], float] = {}
     for rnd in range(2):  # two interleaved rounds, min per config: robust to clock noise
         for cfg in cands:
@@ -140,48 +145,7 @@ def load_tuned(path: str) -> int:
 
 TUNED_FILE = os.environ.get("TDG_GEMM_TUNED_FILE") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "gemm_tuned_gfx950.json")
-if os.environ.get("TDG_GEMM_TUNED", "1") != "0":
-    load_tuned(TUNED_FILE)
-
-
-BLAS = (-1, 1)  # "config" meaning: plain library GEMM (hipBLASLt via torch)
-ALLOW_BLAS = True
-
-
-def _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N, bias_lp=None) -> bool:
-    """Library candidates (hipBLASLt through torch): plain dgrad (KC x MC, bf16
-    out) and wgrad (MC x MC, f32 out), and forward (KC x KC, bf16 out) with the
-    bias / bias+ReLU epilogue when the bias's bf16 copy is supplied."""
-    if not ALLOW_BLAS or alpha != 1.0 or beta not in (0.0, 1.0) or ldc != N:
-        return False
-    if epi in (EPI_BIAS, EPI_BIAS_RELU):
-        return (bias_lp is not None and a_kc and b_kc and beta == 0.0
-                and Cout.dtype == torch.bfloat16 and bias_lp.dtype == torch.bfloat16)
-    if epi != EPI_NONE:
-        return False
-    if beta == 1.0:  # C += A B (standard GEMM beta; residual-gradient accumulation)
-        return a_kc and not b_kc and Cout.dtype == torch.bfloat16
-    return (a_kc and not b_kc and Cout.dtype == torch.bfloat16) or \
-        (not a_kc and not b_kc and Cout.dtype == torch.float32)
-
-
-def _blas(A, B, Cout, M, N, K, lda, ldb, a_kc, beta=0.0, epi=EPI_NONE, bias_lp=None):
-    a = A.as_strided((M, K), (lda, 1)) if a_kc else A.as_strided((K, M), (lda, 1)).t()
-    c = Cout.as_strided((M, N), (N, 1))
-    if epi in (EPI_BIAS, EPI_BIAS_RELU):  # forward: B is the [N, K] weight
-        wt = B.as_strided((N, K), (ldb, 1)).t()
-        if epi == EPI_BIAS_RELU:
-            torch._addmm_activation(bias_lp, a, wt, use_gelu=False, out=c)
-        else:
-            torch.addmm(bias_lp, a, wt, out=c)
-        return
-    b = B.as_strided((K, N), (ldb, 1))
-    if beta == 1.0:
-        c.addmm_(a, b)
-    elif Cout.dtype == torch.bfloat16:
-        torch.mm(a, b, out=c)
-    else:
-        torch.mm(a, b, out_dtype=torch.float32, out=c)
+load_tuned(TUNED_FILE)
 
 
 def _tok_bucket(v: int) -> int:
@@ -189,16 +153,11 @@ def _tok_bucket(v: int) -> int:
 
 
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None, aux=None,
-         ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None,
-         bias_lp: Optional[torch.Tensor] = None) -> torch.Tensor:
-    blas_ok = _blas_ok(a_kc, b_kc, epi, alpha, beta, Cout, ldc, N, bias_lp)
+         ldaux=0, alpha=1.0, beta=0.0, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """Every GEMM of the model: the in-tree MFMA kernels (csrc/kernels/gemm.hip)
+    with the tile config from the tuned table, else the heuristic."""
 
     def run(c, out=Cout):
-        if c == BLAS:
-            if not blas_ok:
-                raise RuntimeError("library GEMM not applicable")
-            _blas(A, B, out, M, N, K, lda, ldb, a_kc, beta, epi, bias_lp)
-            return
         tile, splits = c
         ws = workspace("splitk", splits * M * ldc, A.device) if splits > 1 else None
         C().gemm(A, B, out, bias, aux, M, N, K, lda, ldb, ldc, ldaux, a_kc, b_kc, epi, alpha,
@@ -220,9 +179,9 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None
                 # accumulate into C: tune on a scratch copy so C is untouched
                 scratch = workspace("tune_c", Cout.numel(), A.device, Cout.dtype)[: Cout.numel()]
                 scratch = scratch.view_as(Cout)
-                best = _autotune(key, lambda c: run(c, scratch), blas_ok)
+                best = _autotune(key, lambda c: run(c, scratch))
             else:
-                best = _autotune(key, run, blas_ok)
+                best = _autotune(key, run)
             ent = (best, best)
             _TUNED[key] = ent
         if ent is None:
@@ -234,23 +193,20 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_kc, b_kc, epi=EPI_NONE, bias=None
 
 
 def tuned_table() -> Dict[str, str]:
-    return {f"{k[0]}x{k[1]}x{k[2]} a_kc={k[3]} b_kc={k[4]} epi={k[5]}":
-            ("hipblaslt" if v == BLAS else f"cfg{v[0]} split{v[1]}") for k, v in _TUNED.items()}
+    return {f"{k[0]}x{k[1]}x{k[2]} a_kc={k[3]} b_kc={k[4]} epi={k[5]}": f"cfg{v[0]} split{v[1]}"
+            for k, v in _TUNED.items()}
 
 
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], relu: bool = False,
-               out: Optional[torch.Tensor] = None, ldc: Optional[int] = None,
-               bias_lp: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y[M,N] = x[M,K] @ w[N,K]^T + bias (bf16 out). bias_lp: the bias's bf16
-    compute copy -- lets the tuner also try hipBLASLt's bias(+ReLU) epilogue."""
+               out: Optional[torch.Tensor] = None, ldc: Optional[int] = None) -> torch.Tensor:
+    """y[M,N] = x[M,K] @ w[N,K]^T + bias (bf16 out)."""
     M, K = x2.shape
     N = w.shape[0]
     ldc = ldc or N
     if out is None:
         out = torch.empty(M, ldc, dtype=torch.bfloat16, device=x2.device)
     epi = EPI_BIAS_RELU if relu else (EPI_BIAS if bias is not None else EPI_NONE)
-    return gemm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), ldc, True, True, epi, bias=bias,
-                bias_lp=bias_lp)
+    return gemm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), ldc, True, True, epi, bias=bias)
 
 
 def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor, N: int, relu_aux: Optional[torch.Tensor] = None,
@@ -419,34 +375,6 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
     rstd = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
     C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps, y8, s8, amax8)
     return y, h, mean, rstd
-
-
-# Fused projection + LayerNorm (csrc/kernels/gemm_ln.hip) is opt-in: with one
-# workgroup per 32 full rows every workgroup streams all of W, and on MI355X
-# that measured slower than the 128x128-tile GEMM + standalone LayerNorm
-# (8192 rows: 35 vs 25 us at K=512, 97 vs 39 us at K=2048; profiles/
-# pmc_gemm_ln_v1.txt: 2.3x the L2 requests of the tiled GEMM).
-GEMM_LN = os.environ.get("TDG_GEMM_LN", "0") != "0"
-
-
-def gemm_ln_ok(a2, w, x2) -> bool:
-    """Shapes the fused projection + LayerNorm kernel covers (d_model 512)."""
-    return (GEMM_LN and w.shape[0] == 512 and a2.shape[1] % 64 == 0 and a2.stride(1) == 1
-            and x2.stride(1) == 1 and a2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
-            and w.stride(0) % 8 == 0)
-
-
-def gemm_ln(a2, w, bias, x2, gamma, beta, p, seed, ctr, site, eps=1e-6):
-    """y = LN(x + dropout(a @ w^T + bias)) in one launch (csrc/kernels/gemm_ln.hip).
-    Returns (y, h, mean, rstd) like ln_fwd, or None if the shape is not covered."""
-    M, D = x2.shape
-    y = torch.empty(M, D, dtype=torch.bfloat16, device=x2.device)
-    h = torch.empty_like(y)
-    stats = torch.empty(2, M, dtype=torch.float32, device=x2.device)
-    rc = C().gemm_ln(a2, w, bias, x2, gamma, beta, y, h, stats[0], stats[1], p, seed, ctr, site, eps)
-    if rc != 0:
-        return None
-    return y, h, stats[0], stats[1]
 
 
 def ln_bwd_nparts(M: int, D: int) -> int:

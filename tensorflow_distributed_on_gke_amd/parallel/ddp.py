@@ -32,6 +32,7 @@ from __future__ import annotations
 import math
 import os
 import queue
+import sys
 import threading
 from dataclasses import dataclass
 from typing import Callable, List, Optional
@@ -40,17 +41,23 @@ import torch
 import torch.distributed as dist
 
 from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
-from tensorflow_distributed_on_gke_amd.ops.streams import join, on_side
+from tensorflow_distributed_on_gke_amd.parallel.dist import PG_TIMEOUT_S
 
 
 # Issue GPU collectives from a host thread (CommThread) instead of making the
-# communication stream wait on the compute stream (TDG_DP_COMM_THREAD=0: the
-# process group's own stream handoff; "force": also over gloo with GPU tensors
-# -- the two-rank rehearsal on one GPU, tests/test_gpu_dp.py)
-COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1")
-# seconds the host waits for the comm thread to enqueue a collective (a GPU
-# that never reaches the issue point would otherwise hang the step silently)
-COMM_ISSUE_TIMEOUT_S = float(os.environ.get("TDG_DP_ISSUE_TIMEOUT_S", "1800"))
+# communication stream wait on the compute stream. Opt-in (TDG_DP_COMM_THREAD=1
+# on RCCL; "force": also over gloo with GPU tensors -- the multi-rank
+# rehearsals on one GPU, tests/test_gpu_dp.py). It measured 0.3 ms/step faster
+# on one rank (docs/PERF.md) but has not yet run on more than one GPU, so the
+# default is the process group's own stream handoff, the standard
+# torch.distributed issue path.
+COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "0")
+# seconds the host waits for the comm thread to enqueue a collective before
+# the data-parallel state is poisoned and the step raises (a GPU that never
+# reaches the issue point would otherwise hang); default: the process-group
+# timeout (parallel/dist.py). A stall is reported every ISSUE_REPORT_S.
+COMM_ISSUE_TIMEOUT_S = PG_TIMEOUT_S
+ISSUE_REPORT_S = 60.0
 
 
 class CommThread:
@@ -84,10 +91,20 @@ class CommThread:
     def submit(self, job: Callable[[], None]) -> None:
         self._q.put(job)
 
-    def close(self) -> None:
+    def abandon(self) -> None:
+        """Drop every queued job (after a failure the sequence is broken)."""
+        try:
+            while True:
+                self._q.get_nowait()
+        except queue.Empty:
+            pass
+
+    def close(self) -> bool:
+        """Stop the thread; False if it did not exit (a job is stuck)."""
         if self._t.is_alive():
             self._q.put(None)
             self._t.join(timeout=60)
+        return not self._t.is_alive()
 
 
 class Pending:
@@ -173,6 +190,14 @@ class DataParallel:
         if self.active and COMM_THREAD != "0" and store.flat.is_cuda and \
                 (dist.get_backend(group) == "nccl" or COMM_THREAD == "force"):
             self._thread = CommThread(store.flat.device)
+        # collectives issued but not yet waited for (any issue path): a
+        # main-thread collective issued meanwhile could interleave differently
+        # on different ranks, so those check this is zero (check_quiescent)
+        self._outstanding = 0
+        # set (with the reason) once a collective failed or was not issued in
+        # time: every later collective raises instead of risking a mismatched
+        # sequence across ranks
+        self.poisoned: Optional[str] = None
         self.buckets: List[Bucket] = []       # this step's launched spans
         self.last_buckets: List[Bucket] = []  # the previous step's (introspection)
         if self.active:
@@ -201,6 +226,7 @@ class DataParallel:
     def broadcast_params(self, src: int = 0) -> None:
         """Rank `src`'s initial weights to everyone (MWMS variable broadcast)."""
         if self.active:
+            self.check_quiescent("broadcast_params")
             dist.broadcast(self.store.flat, src, group=self.group)
             self.store.refresh_compute()
 
@@ -229,10 +255,7 @@ class DataParallel:
         self._launch(b)
 
     def _launch(self, b: Bucket) -> None:
-        # gradients come from both the compute stream and the weight-gradient
-        # side stream: collect on the side stream after it caught up
-        with on_side(self.store.flat_grad.device):
-            self._launch_now(b)
+        self._launch_now(b)
 
     def _launch_now(self, b: Bucket) -> None:
         view = self.store.flat_grad[b.start:b.end]
@@ -256,6 +279,8 @@ class DataParallel:
         th = self._thread
 
         def issue():
+            self._check_poison()
+            self._outstanding += 1
             if th is None:
                 h.work = dist.all_reduce(t, group=grp, async_op=True)
                 return
@@ -286,19 +311,49 @@ class DataParallel:
             issue()
         return h
 
-    @staticmethod
-    def _wait_now(h: Pending) -> None:
+    def _check_poison(self) -> None:
+        if self.poisoned is not None:
+            raise RuntimeError(f"data-parallel state is poisoned ({self.poisoned}); refusing further "
+                               "collectives -- exit and restart the job")
+
+    def _poison(self, reason: str) -> None:
+        self.poisoned = reason
+        if self._thread is not None:
+            # a stuck job keeps later ones queued behind it: drop them all
+            self._thread.abandon()
+
+    def check_quiescent(self, what: str) -> None:
+        """Every collective this object issued has been waited for: `what` (a
+        main-thread collective) cannot interleave with them differently on
+        different ranks. Raises otherwise, and when poisoned."""
+        self._check_poison()
+        if self._outstanding:
+            raise RuntimeError(f"{what}: {self._outstanding} data-parallel collective(s) issued but not "
+                               "waited for (call finish() first)")
+
+    def _wait_now(self, h: Pending) -> None:
         """Current stream waits for the collective (device-side; the host only
         waits until a thread-issued collective has been enqueued)."""
+        self._check_poison()
         if h.issued is None:
             h.work.wait()
+            self._outstanding -= 1
             return
-        if not h.issued.wait(timeout=COMM_ISSUE_TIMEOUT_S):
-            raise RuntimeError(f"data-parallel collective not issued within {COMM_ISSUE_TIMEOUT_S:.0f} s "
-                               "(the compute stream never reached its issue point)")
+        waited = 0.0
+        while not h.issued.wait(timeout=min(ISSUE_REPORT_S, COMM_ISSUE_TIMEOUT_S - waited)):
+            waited += ISSUE_REPORT_S
+            if waited >= COMM_ISSUE_TIMEOUT_S:
+                msg = (f"collective not issued within {COMM_ISSUE_TIMEOUT_S:.0f} s (the compute stream "
+                       "never reached its issue point)")
+                self._poison(msg)
+                raise RuntimeError("data-parallel " + msg)
+            print(f"[rank {self.rank}] data-parallel: waiting {waited:.0f} s for a collective to be "
+                  "issued", file=sys.stderr, flush=True)
         if h.error is not None:
+            self._poison(f"collective failed on the comm thread: {h.error!r}")
             raise RuntimeError("data-parallel collective failed on the comm thread") from h.error
         torch.cuda.current_stream().wait_event(h.done)
+        self._outstanding -= 1
 
     def _wait(self, h: Pending) -> None:
         if self.recorder is not None:
@@ -359,7 +414,6 @@ class DataParallel:
         every collective (device-side wait; no host sync). With an attached
         optimizer, also update every span not yet updated and advance the
         optimizer step."""
-        join(self.store.flat_grad.device)
         if not self.active:
             self.reset()
             return
@@ -393,6 +447,7 @@ class DataParallel:
         checksum (sum of the int32 bit patterns, int64) across ranks."""
         if self.world <= 1:
             return
+        self.check_quiescent("verify_replicas")
         bits = self.store.flat.detach().view(torch.int32)
         local = torch.stack([bits.sum(dtype=torch.int64), (bits.to(torch.int64) * 2654435761).sum()])
         allv = [torch.zeros_like(local) for _ in range(self.world)]
@@ -404,12 +459,23 @@ class DataParallel:
                                f"({[tuple(v.tolist()) for v in allv]})")
 
     def close(self) -> None:
-        """Stop the comm thread (all its collectives have been waited for)."""
+        """Stop the comm thread (all its collectives have been waited for).
+        Raises if it is stuck, so the process exits non-zero instead of
+        tearing the process group down under a collective."""
         if self._thread is not None:
-            self._thread.close()
+            ok = self._thread.close()
             self._thread = None
+            if not ok:
+                raise RuntimeError("data-parallel comm thread did not stop (a collective is stuck)")
 
     def allreduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
+            self.check_quiescent("allreduce_metrics")
             dist.all_reduce(t, group=self.group)
         return t
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            self.check_quiescent("barrier")
+            from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
+            tdist.barrier()

@@ -16,6 +16,11 @@ import torch
 import torch.distributed as dist
 
 
+# process-group timeout (seconds): a collective that does not complete within
+# it aborts the process (RCCL async error handling) instead of hanging
+PG_TIMEOUT_S = float(os.environ.get("TDG_DIST_TIMEOUT_S", "600"))
+
+
 @dataclass
 class DistInfo:
     rank: int
@@ -29,7 +34,7 @@ class DistInfo:
         return self.rank == 0
 
 
-def init_distributed(device: str = "auto", timeout_s: float = 900.0, force: bool = False) -> DistInfo:
+def init_distributed(device: str = "auto", timeout_s: float = PG_TIMEOUT_S, force: bool = False) -> DistInfo:
     """`force`: create the process group even for a single rank (exercises the
     RCCL data-parallel path on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))

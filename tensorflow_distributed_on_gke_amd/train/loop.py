@@ -44,7 +44,6 @@ from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.parallel.dist import DistInfo
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep
-from tensorflow_distributed_on_gke_amd.utils.gcpolicy import ManualGC
 from tensorflow_distributed_on_gke_amd.utils.profiling import MetricsWriter, StepTimer, summarize, torch_profile
 
 RESUME_DIR = "resume"
@@ -142,8 +141,15 @@ class Trainer:
     def resume_prefix(self) -> str:
         return os.path.join(self.settings.temporary_directory, RESUME_DIR, RESUME_PREFIX)
 
+    def _quiet(self, what: str) -> None:
+        """No data-parallel collective may be in flight when the main thread
+        issues one (parallel/ddp.py check_quiescent)."""
+        if self.ddp is not None:
+            self.ddp.check_quiescent(what)
+
     def _broadcast_state(self) -> None:
         if self.info.world > 1:
+            self._quiet("broadcast")
             for t in (self.model.store.flat, self.opt.m, self.opt.v, self.opt.step):
                 dist.broadcast(t, 0)
             self.model.store.refresh_compute()
@@ -187,6 +193,7 @@ class Trainer:
     def _reduce(self, t: torch.Tensor) -> torch.Tensor:
         t = t.clone()
         if self.info.world > 1:
+            self._quiet("metrics all-reduce")
             dist.all_reduce(t)
         return t.cpu()
 
@@ -209,6 +216,30 @@ class Trainer:
         n = max(float(a[2]), 1.0)
         return {"loss": float(a[0]) / n, "acc": float(a[1]) / n}
 
+    def _arm_backward_fault(self) -> None:
+        """kill_point=backward: this rank exits inside the backward of step
+        kill_at_step, after half of the parameters' gradients are final (the
+        failure-detection test of a peer dying mid-collective)."""
+        s, info = self.settings, self.info
+        if s.kill_point not in ("step", "backward"):
+            raise ValueError(f"kill_point must be step or backward, got {s.kill_point!r}")
+        if s.kill_at_step < 0 or s.kill_point != "backward" or info.rank != (s.kill_rank % info.world):
+            return
+        seen = [0]
+        half = len(self.model.store.params) // 2
+
+        def hook(_p):
+            if self.global_step + 1 != s.kill_at_step:
+                return
+            seen[0] += 1
+            if seen[0] == half:
+                self.log(f"fault injection: rank {info.rank} exiting in the backward of step "
+                         f"{s.kill_at_step}")
+                sys.stdout.flush()
+                os._exit(17)
+
+        self.model.store.on_grad_ready(hook)
+
     # ------------------------------------------------------------------ loop
     def fit(self) -> List[EpochStats]:
         s, info = self.settings, self.info
@@ -224,7 +255,7 @@ class Trainer:
         prof_cm = torch_profile(s.profile_dir if info.chief else None, active=s.profile_steps)
         prof = prof_cm.__enter__()
         prof_left = s.profile_steps + 2 if s.profile_dir and info.chief else 0
-        mgc = ManualGC.from_env()  # no cyclic-GC pass inside a step
+        self._arm_backward_fault()
         for epoch in range(self.start_epoch, s.epochs):
             t0 = time.time()
             self.step_fn.accum.zero_()
@@ -245,7 +276,6 @@ class Trainer:
                 self.timer.start()
                 self.step_fn(src, tgt)
                 self.timer.stop()
-                mgc.step()
                 self.global_step += 1
                 if prof_left:
                     prof.step()
@@ -255,7 +285,7 @@ class Trainer:
                 if self.ddp is not None and s.check_replicas_every > 0 and \
                         self.global_step % s.check_replicas_every == 0:
                     self.ddp.verify_replicas()
-                if s.kill_at_step >= 0 and self.global_step == s.kill_at_step and \
+                if s.kill_at_step >= 0 and self.global_step == s.kill_at_step and s.kill_point == "step" and \
                         info.rank == (s.kill_rank % info.world):
                     self.log(f"fault injection: rank {info.rank} exiting at step {self.global_step}")
                     sys.stdout.flush()
@@ -296,8 +326,8 @@ class Trainer:
                          f"Test Loss {val['loss']:.4f} Test Accuracy {val['acc']:.4f}")
                 self.log(f"Time taken for 1 epoch: {dt:.2f} secs ({st.tokens_per_s:,.0f} tokens/s)\n")
             if info.world > 1:
+                self._quiet("epoch barrier")
                 dist.barrier()
-        mgc.close()
         if prof_left:  # fewer steps than the profile window
             prof_cm.__exit__(None, None, None)
         return self.history

@@ -23,19 +23,17 @@ from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
-from tensorflow_distributed_on_gke_amd.ops import streams
-from tensorflow_distributed_on_gke_amd.ops.streams import join
 from tensorflow_distributed_on_gke_amd.train.graphs import SegmentedGraph, prepare_capture
 from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
 
 # data parallel: weight gradients flushed in wave-sized chunks at layer ends
-CHUNKED_WGRAD = os.environ.get("TDG_DP_CHUNKED_WGRAD", "1") != "0"
-# tiles per wave of the chunked schedule (one whole-K 256x256 tile per CU);
-# overridable so tests can force problems to be cut across launches
-WAVE_TILES = int(os.environ.get("TDG_DP_WAVE_TILES", "0"))
+CHUNKED_WGRAD = True
+# tiles per wave of the chunked schedule (0: one whole-K 256x256 tile per CU);
+# tests set small values to force problems to be cut across launches
+WAVE_TILES = 0
 # skip the optimizer's gradient zeroing (all GPU gradient writers overwrite)
-ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
+ZERO_GRAD_FREE = True
 # how a data-parallel step is captured (TrainStep.capture):
 #   "seg"  -- chain of HIP graphs cut at the collectives, which stay eager
 #             RCCL calls between the segments (train/graphs.py; default)
@@ -44,8 +42,15 @@ ZERO_GRAD_FREE = os.environ.get("TDG_ZERO_GRAD_FREE", "1") != "0"
 # failed capture under PyTorch 2.10's process-group watchdog and was removed)
 DP_GRAPH = os.environ.get("TDG_DP_GRAPH", "seg")
 # data parallel: time the segmented graph against the eager step once and keep
-# the faster (TrainStep.choose_dp_mode); 0 keeps the segmented graph
-DP_AUTOSELECT = os.environ.get("TDG_DP_AUTOSELECT", "1") != "0"
+# the faster (TrainStep.choose_dp_mode); False keeps the segmented graph
+DP_AUTOSELECT = True
+# data parallel: each bucket's Adam runs as soon as its all-reduce is done.
+# "tail": at the end of the step, so the last bucket's all-reduce overlaps the
+# Adam of the others. "1": also mid-backward (decoder side during the
+# encoder's backward) -- on one MI355X with --force-dp that concurrent Adam
+# contended with the encoder backward for more than it hid (6.45 vs 6.34 ms).
+# "0": one Adam after finish.
+DP_OVERLAP_OPT = "tail"
 
 
 class TrainStep:
@@ -85,13 +90,7 @@ class TrainStep:
         self.fp8 = fp8_state
         if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
             opt.zero_grad = False  # every GPU gradient writer overwrites
-        # data parallel: each bucket's Adam runs as soon as its all-reduce is
-        # done. Default "tail": at the end of the step, so the last bucket's
-        # all-reduce overlaps the Adam of the others. "1": also mid-backward
-        # (decoder side during the encoder's backward) -- on one MI355X with
-        # --force-dp that concurrent Adam contended with the encoder backward
-        # for more than it hid (6.45 vs 6.34 ms). "0": one Adam after finish.
-        mode = os.environ.get("TDG_DP_OVERLAP_OPT", "tail")
+        mode = DP_OVERLAP_OPT
         if ddp is not None and ddp.active and fp8_state is None and mode != "0":
             ddp.attach_optimizer(opt, release=mode != "tail")
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
@@ -112,9 +111,9 @@ class TrainStep:
             return "single"
         if DP_GRAPH not in ("seg", "0"):
             raise ValueError(f"TDG_DP_GRAPH must be seg or 0, got {DP_GRAPH!r}")
-        if self.ddp._upd_stream is not None or streams.ENABLED:
-            # mid-backward Adam on its own stream / the weight-gradient side
-            # stream would leave unjoined work at a cut
+        if self.ddp._upd_stream is not None:
+            # mid-backward Adam on its own stream would leave unjoined work
+            # at a cut
             return "0"
         return DP_GRAPH
 
@@ -124,7 +123,7 @@ class TrainStep:
         ts = [self.model.store.flat, self.opt.m, self.opt.v, self.opt.step, self.rt.ctr,
               self.accum, self.last]
         if self.fp8 is not None:
-            ts += [self.fp8.meta.scale, self.fp8.meta.inv_scale]
+            ts += [self.fp8.meta.scale]
         return ts
 
     def snapshot(self):
@@ -149,8 +148,6 @@ class TrainStep:
                                      step_out=self.last, bump_ctr=True, ntok_sum=self._ntok_sum)
         if self.ddp is not None:
             self.ddp.finish()
-        else:
-            join(self.model.device)  # weight gradients from the side stream
         if self.ddp is None or self.ddp.opt is None:
             self.opt.apply()
         if self.fp8 is not None:
@@ -186,6 +183,7 @@ class TrainStep:
             # no collective of the warm-up may still be pending in the process
             # group's watchdog when the capture starts
             torch.cuda.synchronize()
+            self.ddp.check_quiescent("capture")
             dist.barrier(group=self.ddp.group)
             torch.cuda.synchronize()
         if mode == "seg":
@@ -237,6 +235,7 @@ class TrainStep:
             for _ in range(2):
                 run()
             torch.cuda.synchronize()
+            self.ddp.check_quiescent("choose_dp_mode")
             dist.barrier(group=self.ddp.group)
             t0 = time.perf_counter()
             for _ in range(steps):
@@ -251,6 +250,7 @@ class TrainStep:
             self.segments = None
             best["0"] = min(best["0"], timed(lambda: self.eager(src, tgt)))
         t = torch.tensor([best["seg"], best["0"]], dtype=torch.float64, device=dev)
+        self.ddp.check_quiescent("choose_dp_mode")
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ddp.group)
         seg_s, eager_s = float(t[0]), float(t[1])
         self.restore(saved)

@@ -29,8 +29,16 @@ def pytest_collection_modifyitems(config, items):
 
 @pytest.fixture(scope="session", autouse=True)
 def _native_build():
-    """Incremental in-tree build of the native extensions (no-op when fresh)."""
+    """Incremental in-tree build of the native extensions (no-op when fresh).
+    On a GPU box the extensions built here travel with the tree (build/ does
+    not): use them as they are instead of rebuilding inside the test run."""
+    import glob
+
+    import torch
+
     from tensorflow_distributed_on_gke_amd import _build
 
-    _build.build()
+    built = len(glob.glob(os.path.join(ROOT, "tensorflow_distributed_on_gke_amd", "_*.so"))) >= 2
+    if not (torch.cuda.is_available() and built):
+        _build.build()
     yield

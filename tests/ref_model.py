@@ -67,7 +67,9 @@ def mha(W, prefix, v, k, q, mask, heads):
 
     Q, Kk, V = split(Q), split(Kk), split(V)
     logits = Q @ Kk.transpose(-1, -2) / math.sqrt(hd)
-    logits = logits + mask * -1e9
+    # the mask add happens in fp32 as in TF (a fully masked row's logits all
+    # round to -1e9: uniform softmax); autograd passes the gradient through
+    logits = (logits.float() + (mask * -1e9).float()).double()
     w = torch.softmax(logits, -1)
     o = (w @ V).transpose(1, 2).reshape(B, -1, d)
     return dense(W, prefix + "/dense", o), w

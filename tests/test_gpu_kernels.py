@@ -233,6 +233,53 @@ def test_attention_fwd_bwd(hd, causal, Lq, Lk):
     _close(dq, qr.grad, 3e-2, "attn dq")
 
 
+def _tf_attn(q, k, v, kv_len, causal, scale):
+    """The reference's attention in fp32: -1e9 * mask added to the logits,
+    padding and look-ahead masks combined by a maximum
+    (transformer_model.py:94-108, 350-363)."""
+    q, k, v = q.float(), k.float(), v.float()
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    B, H, Lq, Lk = s.shape
+    keys = torch.arange(Lk)
+    mask = (keys.view(1, 1, 1, Lk) >= kv_len.view(B, 1, 1, 1)).float().expand(B, 1, Lq, Lk)
+    if causal:
+        mask = torch.maximum(mask, (keys.view(1, Lk) > torch.arange(Lq).view(Lq, 1)).float().view(1, 1, Lq, Lk))
+    p = torch.softmax(s + mask * -1e9, -1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, v), p
+
+
+@pytest.mark.parametrize("causal,Lq,Lk,hd", [(False, 128, 128, 64), (True, 128, 128, 64), (False, 70, 100, 64),
+                                             (False, 512, 512, 64), (True, 512, 512, 64), (False, 40, 33, 16)])
+def test_attention_fully_masked_rows(causal, Lq, Lk, hd):
+    """kv_len = 0 rows (an all-PAD sequence) follow the reference's fp32
+    numerics: uniform attention over ALL keys (the look-ahead limit included
+    in the mask), and TF's autograd through the mask add (dS from the uniform
+    P, dQ / dK with the real scale). Short (fused backward) and long
+    (dQ + dK/dV kernels) sequence paths, and the probabilities kernel."""
+    B, H = 4, 2
+    torch.manual_seed(3)
+    q = _bf(torch.randn(B, Lq, H, hd))
+    k = _bf(torch.randn(B, Lk, H, hd))
+    v = _bf(torch.randn(B, Lk, H, hd))
+    kv_len = torch.tensor([Lk, 0, max(1, Lk // 3), 0], dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref, pref = _tf_attn(qr, kr, vr, kv_len, causal, scale)
+    out, lse = kk.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), kv_len.to(DEV), scale, causal)
+    _close(out, ref.detach(), 2e-2, "attn fwd (masked rows)")
+    dout = _bf(torch.randn(B, Lq, H, hd))
+    ref.backward(dout.float())
+    dq, dk, dv = (torch.empty_like(t, device=DEV) for t in (q, k, v))
+    kk.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), out, dout.to(DEV), lse, dq, dk, dv, kv_len.to(DEV),
+               scale, causal)
+    _close(dv, vr.grad, 3e-2, "attn dv (masked rows)")
+    _close(dk, kr.grad, 3e-2, "attn dk (masked rows)")
+    _close(dq, qr.grad, 3e-2, "attn dq (masked rows)")
+    if Lq <= 128:
+        pr = kk.attn_probs(q.to(DEV), k.to(DEV), kv_len.to(DEV), scale, causal)
+        _close(pr, pref.detach(), 1e-3, "probs (masked rows)")
+
+
 @pytest.mark.parametrize("causal,Lq,Lk", [(False, 128, 128), (True, 128, 128), (False, 70, 100)])
 def test_attention_bwd_more_items_than_cus(causal, Lq, Lk):
     """B*H = 267 (batch, head) items, more than the 256 CUs, ragged key lengths."""
@@ -425,14 +472,14 @@ def test_grouped_wgrad_and_colsum(G, M, N, Kd):
         _close(outs[i], dys[i].float().sum(0), 1e-3, f"grouped colsum {i}")
 
 
-def test_gemm_library_beta_accumulate():
-    """hipBLASLt candidate for C += A B (bf16) matches the HIP kernel."""
+def test_gemm_beta_accumulate():
+    """C += A B (bf16 out, the residual-gradient accumulation) vs fp32."""
     M, N, Kd = 512, 256, 384
     A = _bf(torch.randn(M, Kd)).to(DEV)
     B = _bf(torch.randn(Kd, N)).to(DEV)
     C0 = _bf(torch.randn(M, N)).to(DEV)
     ref = C0.float() + A.float() @ B.float()
-    for cfg in (kk.BLAS, (8, 1)):
+    for cfg in ((8, 1), (13, 1), (6, 1)):
         C = C0.clone()
         kk.gemm(A, B, C, M, N, Kd, Kd, N, N, True, False, beta=1.0, cfg=cfg)
         _close(C, ref, 2e-2, f"beta=1 {cfg}")
@@ -470,59 +517,69 @@ def test_prep_batch(dtype):
     assert kk.interior_pad_rows() == 0  # reset by the check
 
 
-@pytest.mark.parametrize("M,K", [(300, 512), (8192, 512), (1000, 2048)])
-def test_gemm_ln_matches_unfused(M, K):
-    """Fused projection + bias + dropout + residual + LayerNorm (one launch)
-    vs the GEMM then the standalone LayerNorm: the fused epilogue runs the same
-    row code on the same bf16 s, so the outputs must agree bitwise; and both
-    against an fp32 torch reference."""
-    D, p, seed, site = 512, 0.1, 1234, 9
-    a = _bf(_rand(M, K, seed=61)).to(DEV)
-    w = _bf(_rand(D, K, scale=1.0 / math.sqrt(K), seed=62)).to(DEV)
-    b = _rand(D, scale=0.1, seed=63).to(DEV)
-    x = _bf(_rand(M, D, seed=64)).to(DEV)
-    gamma = (1.0 + 0.1 * _rand(D, seed=65)).to(DEV)
-    beta = (0.1 * _rand(D, seed=66)).to(DEV)
-    ctr = torch.tensor([7], dtype=torch.int64, device=DEV)
-    r = kk.gemm_ln(a, w, b, x, gamma, beta, p, seed, ctr, site)
-    assert r is not None
-    y, h, mean, rstd = r
-    s = kk.linear_fwd(a, w, b)
-    y2, h2, mean2, rstd2 = kk.ln_fwd(x, s, gamma, beta, p, seed, ctr, site)
-    torch.cuda.synchronize()
-    assert torch.equal(h, h2), "hsave differs from GEMM + ln_fwd"
-    assert torch.equal(y, y2), "y differs from GEMM + ln_fwd"
-    assert torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
-    # fp32 reference with the same dropout keep mask (dropped s -> h == x exactly where masked)
-    sf = (a.float() @ w.float().t() + b).to(torch.bfloat16).float()
-    keep = (h.float() - x.float()).abs() > 0
-    hf = x.float() + torch.where(keep, sf / (1 - p), torch.zeros_like(sf))
-    mu = hf.mean(-1, keepdim=True)
-    yf = (hf - mu) * torch.rsqrt(((hf - mu) ** 2).mean(-1, keepdim=True) + 1e-6) * gamma + beta
-    _close(y, yf, 3e-2, "gemm_ln vs fp32")
-    frac = keep.float().mean().item()
-    assert 0.85 < frac < 0.95, f"dropout keep fraction {frac}"
-
-
+@pytest.mark.parametrize("cfg", [0, 4, 5, 6, 9, 10, 12, 13, 14])
 @pytest.mark.parametrize("relu", [False, True])
-def test_linear_fwd_library_bias_epilogue(relu):
-    """The hipBLASLt bias(+ReLU) candidate (bf16 bias copy) agrees with the
-    in-tree epilogue GEMM to bf16 rounding."""
-    M, N, K = 1000, 768, 512
+def test_linear_fwd_tile_configs(relu, cfg):
+    """Every forward tile config of the table (the big preset's 256x128 /
+    128x256 ones included) with the bias / bias+ReLU epilogue vs fp32, on
+    ragged edges (M, N not tile multiples)."""
+    M, N, K = 1000, 776, 512
     x = _bf(_rand(M, K, seed=71)).to(DEV)
     w = _bf(_rand(N, K, scale=1.0 / math.sqrt(K), seed=72)).to(DEV)
     b = _rand(N, scale=0.5, seed=73).to(DEV)
-    out_lib = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    out_own = torch.empty_like(out_lib)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     epi = kk.EPI_BIAS_RELU if relu else kk.EPI_BIAS
-    kk.gemm(x, w, out_lib, M, N, K, K, K, N, True, True, epi, bias=b, cfg=kk.BLAS,
-            bias_lp=b.to(torch.bfloat16))
-    kk.gemm(x, w, out_own, M, N, K, K, K, N, True, True, epi, bias=b, cfg=(0, 1))
+    kk.gemm(x, w, out, M, N, K, K, K, N, True, True, epi, bias=b, cfg=(cfg, 1))
     ref = x.float() @ w.float().t() + b
     if relu:
         ref = torch.relu(ref)
-    _close(out_lib, ref, 1e-2, "hipBLASLt bias epilogue")
-    _close(out_own, ref, 1e-2, "in-tree bias epilogue")
+    _close(out, ref, 1e-2, f"cfg{cfg} bias epilogue")
+
+
+@pytest.mark.parametrize("cfg", [4, 5, 6, 9, 10, 13])
+def test_dgrad_tile_configs(cfg):
+    """dgrad (NN: weight N-contiguous) for the tile configs the tuned table
+    uses for d_model-wide outputs, with the beta = 1 accumulation."""
+    M, N, K = 1000, 1024, 768
+    dy = _bf(_rand(M, K, seed=81)).to(DEV)
+    w = _bf(_rand(K, N, scale=1.0 / math.sqrt(K), seed=82)).to(DEV)
+    c0 = _bf(_rand(M, N, seed=83)).to(DEV)
+    out = c0.clone()
+    kk.gemm(dy, w, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=1.0, cfg=(cfg, 1))
+    ref = dy.float() @ w.float() + c0.float()
+    _close(out, ref, 1e-2, f"cfg{cfg} dgrad beta=1")
+
+
+def test_no_library_gemm_in_training_step():
+    """The training step runs only in-tree kernels: no hipBLASLt / rocBLAS
+    (Cijk_* / rocblas_*) kernel in a profiled eager step of the base model,
+    bf16 or fp8."""
+    from torch.profiler import ProfilerActivity, profile
+
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.ops.fp8 import Fp8State
+    from tensorflow_distributed_on_gke_amd.train.optim import Adam
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    for fp8 in (False, True):
+        cfg = model_config("base")
+        m = Transformer(cfg).build(DEV, seed=0)
+        st = TrainStep(m, Adam(m.store, cfg.d_model), None, workers=1.0, seed=1,
+                       fp8_state=Fp8State(m) if fp8 else None)
+        data = SyntheticPairs(batch=16, src_len=64, tgt_len=65, src_vocab=cfg.src_vocab,
+                              tgt_vocab=cfg.tgt_vocab, min_len=8)
+        s, t = data.batch(0)
+        st(s.to(DEV), t.to(DEV))
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            st(s.to(DEV), t.to(DEV))
+            torch.cuda.synchronize()
+        names = {e.name for e in prof.events() if e.device_type.name == "CUDA"}
+        lib = sorted(n for n in names if n.startswith("Cijk") or "rocblas" in n.lower()
+                     or "hipblaslt" in n.lower() or "Custom_Cijk" in n)
+        assert not lib, f"library kernels in the step (fp8={fp8}): {lib[:5]}"
+        assert any("gemm" in n for n in names), sorted(names)[:20]
 
 
 def test_transpose_grouped_and_dgrad_t():

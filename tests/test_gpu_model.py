@@ -202,3 +202,51 @@ def test_gpu_trainer_hip_graph_matches_eager(tmp_path, monkeypatch):
         out[graph] = tr.model.store.flat.detach().clone()
     assert torch.equal(out[False], out[True]), \
         f"graph vs eager weights differ: max {(out[False] - out[True]).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("dev", ["cuda", "cpu"])
+def test_zero_length_source_row_matches_reference(dev):
+    """An all-PAD source sentence (every key masked): the reference's -1e9
+    mask add in fp32 makes that row's attention uniform over all keys
+    (transformer_model.py:101-105), with the gradient passed through the mask
+    add. The GPU kernels and the CPU path must both match the f64 oracle
+    (tests/ref_model.py, mask add in fp32 like TF): loss, accuracy and every
+    parameter gradient."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import ref_model
+
+    cfg = model_config("tiny", d_model=64, heads=4, d_ff=128, src_vocab=60, tgt_vocab=50, dropout=0.0)
+    m = Transformer(cfg).build(dev, seed=7)
+    src, tgt = _batch(4, 12, 10, 60, 50, seed=3)
+    src[1, :] = 0  # an empty source sentence
+    rt = RunCtx(training=True, dropout=0.0, store=m.store,
+                ctr=torch.zeros(1, dtype=torch.int64, device=dev))
+    out = m.loss_and_backward(src.to(dev), tgt.to(dev), rt, workers=1.0).cpu()
+    if dev == "cuda":  # the oracle sees the bf16 weights the GPU computed with
+        m.store.flat.copy_(m.store.flat_compute.float())
+    W = {k: v.cpu().detach().requires_grad_(True) for k, v in ref_model.tf_weights(m).items()}
+    loss, acc, _ = ref_model.loss_fn(W, src, tgt, cfg, 1.0)
+    loss.backward()
+    tol = 2e-2 if dev == "cuda" else 1e-4
+    assert abs(out[0].item() - loss.item()) < tol * abs(loss.item()), (out, loss)
+    ours = ref_model.internal_grads_tf(m)
+    # (the key biases' exact gradient is zero -- softmax is shift-invariant --
+    # so theirs is rounding noise: compared in absolute terms)
+    scale = max(t.grad.norm().item() for t in W.values())
+    errs = {k: (ours[k].double() - t.grad).norm().item() / max(t.grad.norm().item(), 1e-3 * scale)
+            for k, t in W.items()}
+    worst = max(errs, key=errs.get)
+    assert errs[worst] < (0.2 if dev == "cuda" else 1e-3), f"{worst}: {errs[worst]:.3e}"
+    # the cross-attention of the empty row really is uniform over all keys
+    if dev == "cuda":
+        from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+        B, L, H, hd = 2, 12, 4, 16
+        q = torch.randn(B, 5, H, hd, device=dev).bfloat16()
+        k = torch.randn(B, L, H, hd, device=dev).bfloat16()
+        v = torch.randn(B, L, H, hd, device=dev).bfloat16()
+        kv = torch.tensor([0, 7], dtype=torch.int32, device=dev)
+        o, _ = kk.attn_fwd(q, k, v, kv, 0.25, False)
+        want = v[0].float().mean(0, keepdim=True).expand(5, H, hd)
+        assert (o[0].float() - want).abs().max().item() < 1e-2

@@ -42,8 +42,9 @@ def _data(rank, world):
 
 def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mode="replica_mean"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      TDG_DP_OVERLAP_OPT=str(overlap_opt))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from tensorflow_distributed_on_gke_amd.train import step as step_mod
+    step_mod.DP_OVERLAP_OPT = str(overlap_opt)
     torch.set_num_threads(2)
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.train.step import TrainStep
@@ -276,6 +277,44 @@ def test_train_cli_fault_injection_and_resume(tmp_path):
     snaps = tmp_path / "snapshots" / "kubernetes-transformer-training"
     assert (snaps / "training-snapshots" / "initial_model" / "variables" / "variables.index").exists()
     assert (snaps / "training-snapshots_2" / "weights_snapshot_2" / "model_weights.index").exists()
+
+
+def test_rank_dying_mid_backward_stops_the_job(tmp_path):
+    """Failure detection: rank 1 exits inside step 4's backward, after some
+    gradient all-reduce spans were launched, while rank 0 is blocked in the
+    matching collective. The launcher must see the exit, stop rank 0 and exit
+    with rank 1's code well within the process-group timeout -- no hang."""
+    import time
+
+    t0 = time.time()
+    r = _cli(tmp_path, "epochs=2", "kill_at_step=4", "kill_point=backward", "kill_rank=1",
+             "bucket_mb=0.02", "resume=false")
+    dt = time.time() - t0
+    assert r.returncode == 17, r.stdout + r.stderr
+    assert "exiting in the backward of step 4" in r.stdout, r.stdout
+    assert "Epoch 1 Loss" not in r.stdout  # died inside epoch 1 (6 steps)
+    assert dt < 120, dt
+
+
+def test_main_thread_collective_refused_while_spans_in_flight():
+    """A main-thread collective (metrics, barrier, broadcast) issued while a
+    gradient span is still in flight could interleave differently on
+    different ranks: DataParallel refuses it, and a poisoned instance (a
+    collective failed or was never issued) refuses everything."""
+    m = Transformer(model_config("tiny", **CFG)).build("cpu", seed=0)
+    dp = DataParallel(m.store, bucket_mb=100.0)
+    dp.world = 2
+    dp._outstanding = 1
+    with pytest.raises(RuntimeError, match="not waited for"):
+        dp.allreduce_metrics(torch.zeros(2))
+    with pytest.raises(RuntimeError, match="not waited for"):
+        dp.barrier()
+    dp._outstanding = 0
+    dp.poisoned = "test"
+    with pytest.raises(RuntimeError, match="poisoned"):
+        dp.check_quiescent("x")
+    with pytest.raises(RuntimeError, match="poisoned"):
+        dp.all_reduce_async(torch.zeros(4))
 
 
 def test_segmented_capture_defers_collectives(monkeypatch):
