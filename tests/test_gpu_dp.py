@@ -168,6 +168,9 @@ def test_gpu_rank_dying_mid_backward_with_comm_thread(tmp_path):
     env.pop("RANK", None)
     t0 = time.time()
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 17, r.stdout[-3000:] + r.stderr[-3000:]
+    # either exit may be seen first: rank 1's injected one (17), or rank 0
+    # failing its collective (the comm thread surfaces the peer loss)
+    assert r.returncode != 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "exiting in the backward of step 3" in r.stdout
+    assert "Epoch 1 Loss" not in r.stdout
     assert time.time() - t0 < 180

