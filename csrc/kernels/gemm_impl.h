@@ -25,6 +25,7 @@
 #include "tdg_common.h"
 #include "tdg_gemm.h"
 #include "tdg_reduce.h"
+#include "gemm_pipe.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -636,11 +637,53 @@ inline int r256_single(R256Args& a, const bf16_t* const* A, const bf16_t* const*
   return G * c.tiles_m * c.tiles_n;
 }
 
+// Pipelined kernel (gemm_pipe.h): single problem, K % 32 == 0, operands
+// addressable with 31-bit byte offsets. Returns false if not applicable.
+template <int BM, int BN, int NS, bool AK, bool BKc, int EPI, bool F32>
+bool launch_pipe(const bf16_t* A, const bf16_t* B, void* C, const float* bias, const bf16_t* aux,
+                 int M, int N, int K, int lda, int ldb, int ldc, int ldaux, float alpha, float beta,
+                 hipStream_t st) {
+  if (K % PK != 0 || K <= 0) return false;
+  const long long ab = AK ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M;
+  const long long bb = BKc ? (long long)(N - 1) * ldb + K : (long long)(K - 1) * ldb + N;
+  if (ab * 2 >= 0x7fffffffLL || bb * 2 >= 0x7fffffffLL) return false;
+  if ((!AK && lda % 8) || (!BKc && ldb % 8)) return false;
+  constexpr int lds = NS * (BM + BN) * PK * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_pipe_kernel<BM, BN, NS, AK, BKc, EPI, F32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, NS, AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds,
+                     st, A, B, C, bias, aux, M, N, K, lda, ldb, ldc, ldaux, alpha, beta,
+                     (int)(ab * 2), (int)(bb * 2));
+  return true;
+}
+
 template <bool AK, bool BKc, int EPI, bool F32>
 void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const float* bias,
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st,
                   const GemmGroup* grp = nullptr, int G = 1) {
+  if (tile_cfg >= 20 && tile_cfg <= 22) {
+    // software-pipelined kernel (one problem, no split-K); else cfg 0
+    if (!grp && splits <= 1) {
+      bool ok = false;
+      if (tile_cfg == 20)
+        ok = launch_pipe<256, 256, 4, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
+                                                         ldaux, alpha, beta, st);
+      else if (tile_cfg == 21)
+        ok = launch_pipe<256, 128, 6, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
+                                                         ldaux, alpha, beta, st);
+      else
+        ok = launch_pipe<128, 256, 6, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
+                                                         ldaux, alpha, beta, st);
+      if (ok) return;
+    }
+    tile_cfg = 0;
+  }
   if (tile_cfg == 12) {
     // 256x256 tiles (K % 64 == 0, no split-K; MN-contiguous operands need
     // ld % 8 == 0); otherwise cfg 0

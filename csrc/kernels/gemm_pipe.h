@@ -1,0 +1,251 @@
+// Software-pipelined MFMA GEMM main loop (tile configs 20-22, gemm_impl.h).
+//
+// Why a second main loop: measured with csrc/lab/stream_lab.cpp
+// (profiles/gemm/r3_stream_lab_work_modes_clock.txt), the LDS-DMA operand
+// stream of a 128x128-tile GEMM alone moves 83-85 GB/s per CU, but with the
+// MFMAs OR the fragment reads of the k-step added in the lock-step form of
+// the older kernels (barrier -> reads -> wait -> MFMAs) it drops by ~25 %,
+// with both by ~70 % -- at an unchanged clock, also from L2-resident operands:
+// the phases of a K tile serialise. Here nothing waits in bulk:
+//   * K tiles are 32 deep (one MFMA k-step) in an NS-slot LDS ring, NS-2 .. NS-1
+//     tiles in flight, one barrier per K tile and no LDS drain at it (the
+//     slot refilled in iteration kt is tile kt-1's, whose reads every wave has
+//     consumed -- waited for -- before the barrier);
+//   * the MFMAs of tile kt are issued per A fragment row i (TN MFMAs each);
+//     behind each row the wave requests that row's fragment of tile kt+1
+//     into the same registers (the B fragments of kt+1 are double-buffered)
+//     and, spread over the rows, its share of tile kt+NS-1's LDS-DMA pieces,
+//     so LDS reads, DMA issue and address arithmetic all run in the MFMA
+//     shadow; the compiler-visible LDS reads get exact counted lgkmcnt waits
+//     (the k-step's last MFMA row waits only for its own fragment);
+//   * the DMA goes through buffer_load ... lds with per-lane byte offsets
+//     computed once and a scalar per-K-tile offset (no per-issue VALU).
+// 8 waves as 2 (M) x 4 (N); tiles 256x256 (wave tile 128x64), 256x128
+// (128x32), 128x256 (64x64). Same operand layouts (K- or MN-contiguous,
+// XOR-swizzled images, conflict-free fragment reads) and the same epilogue
+// (EpiLds) as the other kernels. K % 32 == 0; one problem per launch.
+#pragma once
+#include "tdg_common.h"
+#include "tdg_gemm.h"
+
+namespace tdg {
+
+constexpr int PK = 32;  // K-tile depth of the pipelined kernel
+
+// Byte offset of (row, byte) in a PK-deep tile image.
+//  KC: [R rows][32 k] -> 64-B rows; 16-B chunk ^= ((row >> 3) & 1) << 1
+//      (every ds_read_b128 lane group of a 16-row fragment read then covers
+//      all 16 bank slots: found by exhaustive search over row-bit XORs)
+//  MC: [32 k rows][R]: the 32-B segment swizzle of the BK = 64 images
+//      (lds_off<false, R>), rows are k.
+template <bool KC, int R>
+__device__ __forceinline__ int plds_off(int row, int byte) {
+  if constexpr (KC) {
+    const int ch = (byte >> 4) ^ (((row >> 3) & 1) << 1);
+    return row * 64 + (ch << 4) + (byte & 15);
+  } else {
+    return lds_off<false, R>(row, byte);
+  }
+}
+
+// LDS-DMA staging of one PK-deep operand tile through a buffer resource:
+// per lane and piece a byte offset fixed for the whole K loop (rows /
+// columns clamped to the operand), per K tile one scalar offset.
+template <bool KC, int R, int NW>
+struct PStage {
+  static constexpr int BYTES = R * PK * 2;
+  static constexpr int P = BYTES / (NW * 1024);  // pieces per wave per tile
+  static_assert(BYTES % (NW * 1024) == 0, "tile must split into 1 KiB pieces per wave");
+  uint32_t voff[P];
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t kstep;  // bytes per K tile
+  // X: operand base; ld in elements; len = rows (KC) / columns (MC) valid
+  __device__ __forceinline__ void init(const bf16_t* X, int ld, int len, int mn0, int nrec_bytes,
+                                       int wid, int lane) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), (short)0, nrec_bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int piece = wid * P + i;
+      if constexpr (KC) {
+        const int r = piece * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ (((r >> 3) & 1) << 1);
+        int mn = mn0 + r;
+        mn = mn < len ? mn : len - 1;
+        voff[i] = (uint32_t)(((long long)mn * ld + c * 8) * 2);
+      } else {
+        constexpr int RPP = 1024 / (R * 2);  // k rows per piece
+        constexpr int CPR = R / 8;           // 16-B chunks per row
+        const int r = piece * RPP + lane / CPR;
+        const int pc = lane % CPR;
+        const int c = (((pc >> 1) ^ ((r & 3) | (((r >> 3) & 1) << 2))) << 1) | (pc & 1);
+        int mn = mn0 + c * 8;
+        mn = mn < len ? mn : 0;  // fully past len: never stored
+        voff[i] = (uint32_t)(((long long)r * ld + mn) * 2);
+      }
+    }
+    kstep = KC ? PK * 2 : (uint32_t)PK * (uint32_t)ld * 2u;
+  }
+  __device__ __forceinline__ void issue(int i, int kt, char* lds, int wid) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsrc, (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, voff[i],
+        (int)(kstep * (uint32_t)kt), 0, 0);
+  }
+};
+
+// MFMA operand fragment (16 rows / columns at `base`) of a PK-deep image:
+// lane l holds X(base + (l & 15), 8 (l >> 4) + j), j < 8. Compiler-tracked
+// reads (counted lgkmcnt waits, hazards handled).
+template <bool KC, int R>
+__device__ __forceinline__ short8_t pfrag(const char* lds, int base, int lane) {
+  typedef __attribute__((address_space(3))) short4_t lds4;
+  if constexpr (KC) {
+    const int row = base + (lane & 15);
+    return *reinterpret_cast<const short8_t*>(lds + plds_off<true, R>(row, (lane >> 4) * 16));
+  } else {
+    const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+    const int krow = 8 * g + q;
+    const int byte = (base + 4 * p) * 2;
+    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(lds + plds_off<false, R>(krow, byte)));
+    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(lds + plds_off<false, R>(krow + 4, byte)));
+    return cat4(lo, hi);
+  }
+}
+
+// vmcnt wait leaving `n` younger tiles (PT LDS-DMA each) in flight
+template <int PT, int NMAX>
+__device__ __forceinline__ void wait_tiles(int n) {
+  static_assert(NMAX <= 4 && PT * NMAX <= 63, "vmcnt range");
+  if (NMAX >= 4 && n >= 4) { wait_vmcnt<(NMAX >= 4 ? 4 * PT : 0)>(); return; }
+  if (NMAX >= 3 && n >= 3) { wait_vmcnt<(NMAX >= 3 ? 3 * PT : 0)>(); return; }
+  if (NMAX >= 2 && n >= 2) { wait_vmcnt<(NMAX >= 2 ? 2 * PT : 0)>(); return; }
+  if (NMAX >= 1 && n >= 1) { wait_vmcnt<PT>(); return; }
+  wait_vmcnt<0>();
+}
+
+template <int BM, int BN, int NS, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm_pipe_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+    const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
+    int ldb, int ldc, int ldaux, float alpha, float beta, int a_bytes, int b_bytes) {
+  constexpr int NW = 8;
+  constexpr int WTM = BM / 2, WTN = BN / 4;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * PK * 2, B_BYTES = BN * PK * 2;
+  constexpr int SB = A_BYTES + B_BYTES;
+  using SA = PStage<A_KC, BM, NW>;
+  using SBt = PStage<B_KC, BN, NW>;
+  constexpr int PT = SA::P + SBt::P;  // LDS-DMA per wave per K tile
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / PK;
+
+  SA sa;
+  SBt sb;
+  sa.init(A, lda, M, m0, a_bytes, wid, lane);
+  sb.init(B, ldb, N, n0, b_bytes, wid, lane);
+  auto stage = [&](int kt) {  // whole tile (prologue)
+    char* st = smem + (kt % NS) * SB;
+#pragma unroll
+    for (int i = 0; i < SA::P; ++i) sa.issue(i, kt, st, wid);
+#pragma unroll
+    for (int i = 0; i < SBt::P; ++i) sb.issue(i, kt, st + A_BYTES, wid);
+  };
+  auto stage_piece = [&](int q, int kt) {  // piece q of PT (interleaved)
+    char* st = smem + (kt % NS) * SB;
+    if (q < SA::P) sa.issue(q, kt, st, wid);
+    else sb.issue(q - SA::P, kt, st + A_BYTES, wid);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int abase = wm * WTM, bbase = wn * WTN;
+  // prologue: NS-1 tiles in flight, tile 0 landed, its fragments requested
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s);
+  wait_tiles<PT, NS - 2>(min(NS - 1, nk) - 1);
+  __builtin_amdgcn_s_barrier();
+  short8_t fa[TM], fb[TN], fbn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb[j] = pfrag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa[i] = pfrag<A_KC, BM>(smem, abase + 16 * i, lane);
+
+  // one K tile: MFMAs of tile kt with tile kt+1's fragment reads and tile
+  // kt+NS-1's DMA pieces behind the MFMA rows. FB: this tile's B fragments,
+  // FN: receives the next tile's (named buffers: the loop below is unrolled
+  // by two so every array index stays a compile-time constant).
+  auto ktile = [&](int kt, short8_t(&FB)[TN], short8_t(&FN)[TN]) {
+    const bool nxt = kt + 1 < nk;
+    if (nxt) {
+      // tile kt+1 landed (this wave's pieces), then everyone's; every wave
+      // also finished reading tile kt-1, whose slot is refilled below.
+      // In flight after kt+1: tiles up to kt+NS-2 (kt = 0: NS-1)
+      wait_tiles<PT, NS - 2>(kt == 0 ? min(NS - 2, nk - 2) : min(NS - 3, nk - 2 - kt));
+      __builtin_amdgcn_s_barrier();
+    }
+    const char* nx = smem + ((kt + 1) % NS) * SB;
+    const int rt = kt - 1 + NS;  // tile refilled into tile kt-1's slot
+    const bool refill = rt < nk && kt >= 1;
+    // (the next tile's fragments are read unconditionally -- after the last
+    // tile from a stale slot, never used -- so the compiler's lgkmcnt
+    // bookkeeping stays exact: no branch around an LDS read)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) FN[j] = pfrag<B_KC, BN>(nx + A_BYTES, bbase + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(FB[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      fa[i] = pfrag<A_KC, BM>(nx, abase + 16 * i, lane);
+      // this wave's DMA pieces of tile rt, spread over the MFMA rows
+#pragma unroll
+      for (int q = 0; q < PT; ++q)
+        if (q * TM / PT == i && refill) stage_piece(q, rt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // kt = 0 refills nothing (tile NS-1's slot was never used): issue it now
+  if (NS - 1 < nk) stage(NS - 1);
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    ktile(kt, fb, fbn);
+    ktile(kt + 1, fbn, fb);
+  }
+  if (kt < nk) ktile(kt, fb, fbn);
+
+  // ---------------- epilogue: per-wave LDS image over the pipeline stages
+  wait_vmcnt<0>();
+  lds_barrier();
+  {
+    using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
+    (void)sizeof(OutT);
+    constexpr int RPASS = OUT_F32 ? (WTM < 32 ? WTM : 32) : (WTM > 64 ? 64 : WTM);
+    using Epi = EpiLds<EPI, OUT_F32, TM, TN, RPASS>;
+    static_assert(NW * Epi::BYTES <= NS * SB, "epilogue images fit in the stages");
+    Epi::run(smem + wid * Epi::BYTES, acc, lane, Cv, ldc, M, N, m0 + wm * WTM, n0 + wn * WTN, alpha,
+             beta, bias, aux, ldaux, epi_vec_ok<EPI, OUT_F32>(Cv, ldc, aux, ldaux));
+  }
+}
+
+}  // namespace tdg

@@ -45,7 +45,8 @@ def reset_workspace() -> None:
 # tile configs (see csrc/kernels/gemm.hip): 0=128x128, 1=128x64, 2=64x128, 3=64x64
 _TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128), 5: (256, 128),
           6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (256, 128), 10: (128, 256), 11: (128, 128),
-          12: (256, 256), 13: (128, 128), 14: (128, 128)}
+          12: (256, 256), 13: (128, 128), 14: (128, 128),
+          20: (256, 256), 21: (256, 128), 22: (128, 256)}
 _CFG_OVERRIDE: Dict[Tuple[int, int, int, bool, bool], Tuple[int, int]] = {}
 
 

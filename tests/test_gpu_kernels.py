@@ -517,7 +517,7 @@ def test_prep_batch(dtype):
     assert kk.interior_pad_rows() == 0  # reset by the check
 
 
-@pytest.mark.parametrize("cfg", [0, 4, 5, 6, 9, 10, 12, 13, 14])
+@pytest.mark.parametrize("cfg", [0, 4, 5, 6, 9, 10, 12, 13, 14, 20, 21, 22])
 @pytest.mark.parametrize("relu", [False, True])
 def test_linear_fwd_tile_configs(relu, cfg):
     """Every forward tile config of the table (the big preset's 256x128 /
@@ -536,7 +536,7 @@ def test_linear_fwd_tile_configs(relu, cfg):
     _close(out, ref, 1e-2, f"cfg{cfg} bias epilogue")
 
 
-@pytest.mark.parametrize("cfg", [4, 5, 6, 9, 10, 13])
+@pytest.mark.parametrize("cfg", [4, 5, 6, 9, 10, 13, 20, 21, 22])
 def test_dgrad_tile_configs(cfg):
     """dgrad (NN: weight N-contiguous) for the tile configs the tuned table
     uses for d_model-wide outputs, with the beta = 1 accumulation."""

@@ -217,7 +217,7 @@ def test_zero_length_source_row_matches_reference(dev):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import ref_model
 
-    cfg = model_config("tiny", d_model=64, heads=4, d_ff=128, src_vocab=60, tgt_vocab=50, dropout=0.0)
+    cfg = model_config("tiny", d_model=128, heads=4, d_ff=256, src_vocab=60, tgt_vocab=50, dropout=0.0)
     m = Transformer(cfg).build(dev, seed=7)
     src, tgt = _batch(4, 12, 10, 60, 50, seed=3)
     src[1, :] = 0  # an empty source sentence
