@@ -56,13 +56,17 @@ struct PStage {
   static constexpr int BYTES = R * PK * 2;
   static constexpr int P = BYTES / (NW * 1024);  // pieces per wave per tile
   static_assert(BYTES % (NW * 1024) == 0, "tile must split into 1 KiB pieces per wave");
+  // (the buffer descriptor is rebuilt per issue from uniform values: the
+  // compiler hoists it, and the struct stays host-compilable)
   uint32_t voff[P];
-  __amdgpu_buffer_rsrc_t rsrc;
+  const bf16_t* base;
+  int nrec;
   uint32_t kstep;  // bytes per K tile
   // X: operand base; ld in elements; len = rows (KC) / columns (MC) valid
   __device__ __forceinline__ void init(const bf16_t* X, int ld, int len, int mn0, int nrec_bytes,
                                        int wid, int lane) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), (short)0, nrec_bytes, 0x00020000);
+    base = X;
+    nrec = nrec_bytes;
 #pragma unroll
     for (int i = 0; i < P; ++i) {
       const int piece = wid * P + i;
@@ -87,7 +91,7 @@ struct PStage {
   }
   __device__ __forceinline__ void issue(int i, int kt, char* lds, int wid) const {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rsrc, (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, voff[i],
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), (short)0, nrec, 0x00020000), (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, voff[i],
         (int)(kstep * (uint32_t)kt), 0, 0);
   }
 };
@@ -122,81 +126,46 @@ __device__ __forceinline__ void wait_tiles(int n) {
   wait_vmcnt<0>();
 }
 
-template <int BM, int BN, int NS, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_pipe_kernel(
-    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
-    const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
-    int ldb, int ldc, int ldaux, float alpha, float beta, int a_bytes, int b_bytes) {
-  constexpr int NW = 8;
-  constexpr int WTM = BM / 2, WTN = BN / 4;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * PK * 2, B_BYTES = BN * PK * 2;
-  constexpr int SB = A_BYTES + B_BYTES;
+// The K loop's pieces as static members of one class template (the pattern
+// of EpiLds): clang's host pass failed substitution of free function templates
+// taking the kernel's local operand-stage types for every kernel instantiation
+// but the first, silently dropping those kernels' host handles.
+template <int BM, int BN, int NS, bool A_KC, bool B_KC>
+struct Pipe {
+  static constexpr int NW = 8;
+  static constexpr int TM = BM / 32, TN = BN / 64;  // 16x16 fragments per wave (2 x 4 waves)
+  static constexpr int A_BYTES = BM * PK * 2, SB = A_BYTES + BN * PK * 2;
   using SA = PStage<A_KC, BM, NW>;
   using SBt = PStage<B_KC, BN, NW>;
-  constexpr int PT = SA::P + SBt::P;  // LDS-DMA per wave per K tile
-  static_assert(NS >= 3, "ring: refilled, being read, landed");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  static constexpr int PT = SA::P + SBt::P;  // LDS-DMA per wave per K tile
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  if (tiles_n <= tiles_m) {
-    tn = t % tiles_n;
-    tm = t / tiles_n;
-  } else {
-    tm = t % tiles_m;
-    tn = t / tiles_m;
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = K / PK;
-
-  SA sa;
-  SBt sb;
-  sa.init(A, lda, M, m0, a_bytes, wid, lane);
-  sb.init(B, ldb, N, n0, b_bytes, wid, lane);
-  auto stage = [&](int kt) {  // whole tile (prologue)
+  // whole A+B tile kt into its ring slot (prologue), or piece q of this
+  // wave's PT pieces (interleaved with the MFMAs)
+  static __device__ __forceinline__ void stage(const SA& sa, const SBt& sb, char* smem, int kt,
+                                               int wid) {
     char* st = smem + (kt % NS) * SB;
 #pragma unroll
     for (int i = 0; i < SA::P; ++i) sa.issue(i, kt, st, wid);
 #pragma unroll
     for (int i = 0; i < SBt::P; ++i) sb.issue(i, kt, st + A_BYTES, wid);
-  };
-  auto stage_piece = [&](int q, int kt) {  // piece q of PT (interleaved)
+  }
+  static __device__ __forceinline__ void stage_piece(const SA& sa, const SBt& sb, char* smem, int q,
+                                                     int kt, int wid) {
     char* st = smem + (kt % NS) * SB;
     if (q < SA::P) sa.issue(q, kt, st, wid);
     else sb.issue(q - SA::P, kt, st + A_BYTES, wid);
-  };
+  }
 
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int abase = wm * WTM, bbase = wn * WTN;
-  // prologue: NS-1 tiles in flight, tile 0 landed, its fragments requested
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) stage(s);
-  wait_tiles<PT, NS - 2>(min(NS - 1, nk) - 1);
-  __builtin_amdgcn_s_barrier();
-  short8_t fa[TM], fb[TN], fbn[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) fb[j] = pfrag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, lane);
-#pragma unroll
-  for (int i = 0; i < TM; ++i) fa[i] = pfrag<A_KC, BM>(smem, abase + 16 * i, lane);
-
-  // one K tile: MFMAs of tile kt with tile kt+1's fragment reads and tile
+  // One K tile: MFMAs of tile kt with tile kt+1's fragment reads and tile
   // kt+NS-1's DMA pieces behind the MFMA rows. FB: this tile's B fragments,
-  // FN: receives the next tile's (named buffers: the loop below is unrolled
-  // by two so every array index stays a compile-time constant).
-  auto ktile = [&](int kt, short8_t(&FB)[TN], short8_t(&FN)[TN]) {
-    const bool nxt = kt + 1 < nk;
-    if (nxt) {
+  // FN: receives the next tile's (named buffers: the caller unrolls by two so
+  // every array index stays a compile-time constant).
+  static __device__ __forceinline__ void ktile(int kt, int nk, short8_t (&FB)[TN],
+                                               short8_t (&FN)[TN], short8_t (&fa)[TM],
+                                               f32x4 (&acc)[TM][TN], const SA& sa, const SBt& sb,
+                                               char* smem, int lane, int wid, int abase,
+                                               int bbase) {
+    if (kt + 1 < nk) {
       // tile kt+1 landed (this wave's pieces), then everyone's; every wave
       // also finished reading tile kt-1, whose slot is refilled below.
       // In flight after kt+1: tiles up to kt+NS-2 (kt = 0: NS-1)
@@ -221,18 +190,70 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(
       // this wave's DMA pieces of tile rt, spread over the MFMA rows
 #pragma unroll
       for (int q = 0; q < PT; ++q)
-        if (q * TM / PT == i && refill) stage_piece(q, rt);
+        if (q * TM / PT == i && refill) stage_piece(sa, sb, smem, q, rt, wid);
       __builtin_amdgcn_sched_barrier(0);
     }
-  };
+  }
+};
+
+template <int BM, int BN, int NS, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(512) void gemm_pipe_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+    const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
+    int ldb, int ldc, int ldaux, float alpha, float beta, int a_bytes, int b_bytes) {
+  using P = Pipe<BM, BN, NS, A_KC, B_KC>;
+  constexpr int NW = P::NW, TM = P::TM, TN = P::TN, A_BYTES = P::A_BYTES, SB = P::SB, PT = P::PT;
+  constexpr int WTM = BM / 2, WTN = BN / 4;
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / PK;
+
+  typename P::SA sa;
+  typename P::SBt sb;
+  sa.init(A, lda, M, m0, a_bytes, wid, lane);
+  sb.init(B, ldb, N, n0, b_bytes, wid, lane);
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int abase = wm * WTM, bbase = wn * WTN;
+  // prologue: NS-1 tiles in flight, tile 0 landed, its fragments requested
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) P::stage(sa, sb, smem, s, wid);
+  wait_tiles<PT, NS - 2>(min(NS - 1, nk) - 1);
+  __builtin_amdgcn_s_barrier();
+  short8_t fa[TM], fb[TN], fbn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb[j] = pfrag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa[i] = pfrag<A_KC, BM>(smem, abase + 16 * i, lane);
+
   // kt = 0 refills nothing (tile NS-1's slot was never used): issue it now
-  if (NS - 1 < nk) stage(NS - 1);
+  if (NS - 1 < nk) P::stage(sa, sb, smem, NS - 1, wid);
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    ktile(kt, fb, fbn);
-    ktile(kt + 1, fbn, fb);
+    P::ktile(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+    P::ktile(kt + 1, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
   }
-  if (kt < nk) ktile(kt, fb, fbn);
+  if (kt < nk) P::ktile(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
 
   // ---------------- epilogue: per-wave LDS image over the pipeline stages
   wait_vmcnt<0>();
