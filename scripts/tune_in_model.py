@@ -25,7 +25,7 @@ from tensorflow_distributed_on_gke_amd.ops import kernels as kk  # noqa: E402
 from tensorflow_distributed_on_gke_amd.train.optim import Adam  # noqa: E402
 from tensorflow_distributed_on_gke_amd.train.step import TrainStep  # noqa: E402
 
-CANDS = [(c, 1) for c in (0, 4, 5, 6, 9, 10, 12, 13, 14)]
+CANDS = [(c, 1) for c in (0, 4, 5, 6, 9, 10, 12, 13, 14, 20, 21, 22)]
 
 
 def main():

@@ -83,7 +83,8 @@ _TUNED: Dict[tuple, Tuple[int, int]] = {}
 # (TDG_GEMM_AUTOTUNE=1, scripts/tune_in_model.py), never on in training runs,
 # where results must not depend on the timing noise of the box
 AUTOTUNE = os.environ.get("TDG_GEMM_AUTOTUNE", "0") == "1"
-_CANDIDATES = [(0, 1), (4, 1), (5, 1), (6, 1), (9, 1), (10, 1), (12, 1), (13, 1), (14, 1)]
+_CANDIDATES = [(0, 1), (4, 1), (5, 1), (6, 1), (9, 1), (10, 1), (12, 1), (13, 1), (14, 1),
+               (20, 1), (21, 1), (22, 1)]
 
 
 def _autotune(key, run) -> Tuple[int, int]:
