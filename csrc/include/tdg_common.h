@@ -93,14 +93,23 @@ struct Philox {
   }
 };
 
-// Keep-mask for element `e` of a dropout site. One Philox call covers 4
-// consecutive elements (e/4); word e%4 compared against the threshold.
-// keep iff u32 >= p * 2^32.
+// Keep-mask for element `e` of a dropout site: one Philox call covers 8
+// consecutive elements (block e/8); element e draws the 16-bit half (e % 2)
+// of word (e % 8) / 2 and is kept iff it is >= thresh = rint(p * 2^16)
+// (dropout_thresh; keep probability within 2^-17 of 1 - p). Half-word draws
+// halve the generator work per element: at D = 1024 the mask's Philox rounds,
+// not memory, bounded the LayerNorm kernels.
+__host__ __device__ __forceinline__ uint32_t dropout_thresh(float p) {
+  return (uint32_t)fminf(65536.f, rintf(p * 65536.f));
+}
+__device__ __forceinline__ uint32_t half_draw(const uint32_t r[4], int j) {  // j in [0, 8)
+  return (r[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+}
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t offset, uint64_t e,
                                              uint32_t thresh) {
   uint32_t r[4];
-  Philox::gen(seed, offset, e >> 2, r);
-  return r[e & 3] >= thresh;
+  Philox::gen(seed, offset, e >> 3, r);
+  return half_draw(r, (int)(e & 7)) >= thresh;
 }
 
 // Dropout stream offset: a device-resident counter (advanced once per forward,
@@ -113,17 +122,17 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, const long long* ctr
   return dropout_keep(seed, rng_offset(ctr, site), e, thresh);
 }
 
-// 8 consecutive keep bits for elements e0..e0+7 (e0 % 8 == 0): 2 Philox calls.
-__device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset, uint64_t e0,
-                                                  uint32_t thresh) {
-  uint32_t r[4], s[4];
-  Philox::gen(seed, offset, e0 >> 2, r);
-  Philox::gen(seed, offset, (e0 >> 2) + 1, s);
+// keep bits of the n (<= 8) consecutive elements e0.. (all in one 8-block:
+// e0 % 8 + n <= 8), bit i = element e0 + i: one Philox call
+template <int N>
+__device__ __forceinline__ uint32_t dropout_keep_run(uint64_t seed, uint64_t offset, uint64_t e0,
+                                                     uint32_t thresh) {
+  uint32_t r[4];
+  Philox::gen(seed, offset, e0 >> 3, r);
+  const int j0 = (int)(e0 & 7);
   uint32_t m = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) m |= (r[i] >= thresh ? 1u : 0u) << i;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) m |= (s[i] >= thresh ? 1u : 0u) << (4 + i);
+  for (int i = 0; i < N; ++i) m |= (half_draw(r, j0 + i) >= thresh ? 1u : 0u) << i;
   return m;
 }
 

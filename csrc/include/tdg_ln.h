@@ -1,16 +1,33 @@
-// Row helpers of the fused residual + dropout + LayerNorm kernels (norm.hip,
-// gemm_ln.hip): one wave per D-wide row, VEC = D/64 contiguous elements per
-// lane, and the per-element Philox dropout keep bits (the same mask in
-// forward and backward, regenerated instead of stored).
+// Row helpers of the fused residual + dropout + LayerNorm kernels (norm.hip):
+// one wave per D-wide row, VEC = D/64 elements per lane (RowMap), and the
+// per-element Philox dropout keep bits (the same mask in forward and
+// backward, regenerated instead of stored).
 #pragma once
 #include "tdg_common.h"
 
 namespace tdg {
 
+// Lane -> column map of a D = 64*VEC row: lanes own W = min(VEC, 8)
+// consecutive elements per chunk and the CH = VEC/W chunks sit 64*W apart, so
+// every wave-wide load / store instruction covers one contiguous 64*W*2-byte
+// span (D = 1024: two fully used 1 KiB accesses instead of two 32-byte-strided
+// half-used ones).
+template <int VEC>
+struct RowMap {
+  static constexpr int W = VEC < 8 ? VEC : 8;
+  static constexpr int CH = VEC / W;
+  __device__ static __forceinline__ int col(int lane, int i) {
+    return (i / W) * (64 * W) + lane * W + (i % W);
+  }
+};
+
 template <int VEC>
 struct RowVec {
+  using Map = RowMap<VEC>;
   float v[VEC];
-  __device__ __forceinline__ void load_bf(const bf16_t* p) {
+  // row: the row's first element; lane's slots at Map::col(lane, i)
+  __device__ __forceinline__ void load_row(const bf16_t* row, int lane) {
+    const bf16_t* p = row + lane * Map::W;
     if constexpr (VEC == 2) {
       const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
       v[0] = bf2f((bf16_t)(w & 0xffff));
@@ -21,15 +38,16 @@ struct RowVec {
       for (int i = 0; i < 4; ++i) v[i] = bf2f((bf16_t)w[i]);
     } else {
 #pragma unroll
-      for (int c = 0; c < VEC / 8; ++c) {
-        const short8_t w = *reinterpret_cast<const short8_t*>(p + 8 * c);
+      for (int c = 0; c < Map::CH; ++c) {
+        const short8_t w = *reinterpret_cast<const short8_t*>(p + 512 * c);
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[8 * c + i] = bf2f((bf16_t)w[i]);
       }
     }
   }
   // write-through variant (tdg_common.h WtBuf)
-  __device__ __forceinline__ void store_bf(bf16_t* p, const WtBuf& wt) const {
+  __device__ __forceinline__ void store_row(bf16_t* row, int lane, const WtBuf& wt) const {
+    bf16_t* p = row + lane * Map::W;
     if constexpr (VEC == 2) {
       wt.st4(p, (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16));
     } else if constexpr (VEC == 4) {
@@ -39,15 +57,16 @@ struct RowVec {
       wt.st8(p, w);
     } else {
 #pragma unroll
-      for (int c = 0; c < VEC / 8; ++c) {
+      for (int c = 0; c < Map::CH; ++c) {
         short8_t w;
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = (short)f2bf(v[8 * c + i]);
-        wt.st16(p + 8 * c, w);
+        wt.st16(p + 512 * c, w);
       }
     }
   }
-  __device__ __forceinline__ void store_bf(bf16_t* p) const {
+  __device__ __forceinline__ void store_row(bf16_t* row, int lane) const {
+    bf16_t* p = row + lane * Map::W;
     if constexpr (VEC == 2) {
       *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     } else if constexpr (VEC == 4) {
@@ -57,36 +76,30 @@ struct RowVec {
       *reinterpret_cast<short4_t*>(p) = w;
     } else {
 #pragma unroll
-      for (int c = 0; c < VEC / 8; ++c) {
+      for (int c = 0; c < Map::CH; ++c) {
         short8_t w;
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = (short)f2bf(v[8 * c + i]);
-        *reinterpret_cast<short8_t*>(p + 8 * c) = w;
+        *reinterpret_cast<short8_t*>(p + 512 * c) = w;
       }
     }
   }
 };
 
-// keep bits for VEC consecutive elements starting at e0 (e0 % min(VEC,4) == 0)
+// Keep bits of the lane's VEC slots (bit i = slot i, RowMap order) of the row
+// starting at element e_row (a multiple of 8: D >= 128) of the flat [M, D]
+// tensor: per element the same draw whatever the lane map (tdg_common.h
+// dropout_keep); a lane's runs of W <= 8 elements never straddle an 8-block.
 template <int VEC>
 __device__ __forceinline__ uint32_t keep_bits(uint64_t seed, const long long* ctr, uint64_t site,
-                                              uint64_t e0, uint32_t thresh) {
+                                              uint64_t e_row, int lane, uint32_t thresh) {
+  using Map = RowMap<VEC>;
   const uint64_t off = rng_offset(ctr, site);
   uint32_t m = 0;
-  if constexpr (VEC == 2) {
-    uint32_t r[4];
-    Philox::gen(seed, off, e0 >> 2, r);
-    const int o = (int)(e0 & 3);
-    m = (r[o] >= thresh ? 1u : 0u) | ((r[o + 1] >= thresh ? 1u : 0u) << 1);
-  } else {
 #pragma unroll
-    for (int c = 0; c < VEC / 4; ++c) {
-      uint32_t r[4];
-      Philox::gen(seed, off, (e0 >> 2) + c, r);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) m |= (r[i] >= thresh ? 1u : 0u) << (4 * c + i);
-    }
-  }
+  for (int c = 0; c < Map::CH; ++c)
+    m |= dropout_keep_run<Map::W>(seed, off, e_row + Map::col(lane, Map::W * c), thresh)
+         << (Map::W * c);
   return m;
 }
 
@@ -98,7 +111,7 @@ __device__ __forceinline__ uint32_t keep_bits(uint64_t seed, const long long* ct
 // bitwise-identical results.
 template <int D>
 __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t, bool has_t,
-                                           size_t base, int row, int lane,
+                                           size_t rbase, int row, int lane,
                                            const float* __restrict__ gamma,
                                            const float* __restrict__ beta, bf16_t* __restrict__ y,
                                            bf16_t* __restrict__ hsave, float* __restrict__ mean_out,
@@ -108,7 +121,7 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
   constexpr int VEC = D / 64;
   if (has_t) {
     if (p > 0.f) {
-      const uint32_t km = keep_bits<VEC>(seed, ctr, site, base, thresh);
+      const uint32_t km = keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
       const float sc = 1.f / (1.f - p);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) t.v[i] = ((km >> i) & 1u) ? t.v[i] * sc : 0.f;
@@ -118,8 +131,8 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
   }
   // wt_bytes > 0: y / hsave (that many bytes each) stored write-through
   if (hsave) {
-    if (wt_bytes) h.store_bf(hsave + base, WtBuf(hsave, wt_bytes));
-    else h.store_bf(hsave + base);
+    if (wt_bytes) h.store_row(hsave + rbase, lane, WtBuf(hsave, wt_bytes));
+    else h.store_row(hsave + rbase, lane);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h.v[i] = bf2f(f2bf(h.v[i]));
   }
@@ -137,11 +150,11 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
   const float rstd = rsqrtf(var + eps);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
-    const int col = lane * VEC + i;
+    const int col = RowMap<VEC>::col(lane, i);
     o.v[i] = (h.v[i] - mean) * rstd * gamma[col] + beta[col];
   }
-  if (wt_bytes) o.store_bf(y + base, WtBuf(y, wt_bytes));
-  else o.store_bf(y + base);
+  if (wt_bytes) o.store_row(y + rbase, lane, WtBuf(y, wt_bytes));
+  else o.store_row(y + rbase, lane);
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;

@@ -7,13 +7,14 @@
 // at model build (f32, [max_len, d], as the reference does) and read here; it
 // stays L2-resident.
 #include "tdg_common.h"
+#include "tdg_ln.h"
 
 #include <algorithm>
 
 namespace tdg {
 
 // out[row, :] = drop(table[tok[row]] * scale + pe[row % L])
-// One wave per row, VEC = D/64 elements per lane.
+// One wave per row, VEC = D/64 elements per lane (tdg_ln.h RowMap).
 template <int D, typename TokT>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(
     const TokT* __restrict__ tok, const bf16_t* __restrict__ table, const float* __restrict__ pe,
@@ -25,23 +26,42 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(
   if (row >= M) return;
   const int pos = row % L;
   const long long t = (long long)tok[row];
-  const bf16_t* src = table + t * D + lane * VEC;
-  const float* pr = pe + (size_t)pos * D + lane * VEC;
-  const size_t base = (size_t)row * D + lane * VEC;
-  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const float* pr = pe + (size_t)pos * D;
+  RowVec<VEC> v;
+  v.load_row(table + t * D, lane);
 #pragma unroll
-  for (int c = 0; c < VEC; c += 2) {
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(src + c);
-    float v0 = bf2f((bf16_t)(w & 0xffff)) * scale + pr[c];
-    float v1 = bf2f((bf16_t)(w >> 16)) * scale + pr[c + 1];
-    if (p > 0.f) {
-      v0 = dropout_keep(seed, ctr, site, base + c, thresh) ? v0 * sc : 0.f;
-      v1 = dropout_keep(seed, ctr, site, base + c + 1, thresh) ? v1 * sc : 0.f;
-    }
-    *reinterpret_cast<uint32_t*>(out + base + c) =
-        (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+  for (int i = 0; i < VEC; ++i) v.v[i] = v.v[i] * scale + pr[RowMap<VEC>::col(lane, i)];
+  if (p > 0.f) {
+    const float sc = 1.f / (1.f - p);
+    const uint32_t km = keep_bits<VEC>(seed, ctr, site, (size_t)row * D, lane, thresh);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v.v[i] = ((km >> i) & 1u) ? v.v[i] * sc : 0.f;
   }
+  v.store_row(out + (size_t)row * D, lane);
 }
+
+// Keep bit of column lane + 64 c of a row for the backward kernels below, whose
+// lanes own strided columns (coalesced atomics): each lane draws the 8-element
+// run 8 lane + 512 s once (one Philox call per 8 elements instead of one per
+// element) and the bits are fetched from the owning lane.
+template <int D>
+struct RowKeep {
+  static constexpr int NS = (D + 511) / 512;
+  uint32_t m[NS];
+  __device__ __forceinline__ void draw(uint64_t seed, const long long* ctr, uint64_t site,
+                                       size_t rbase, int lane, uint32_t thresh) {
+    const uint64_t off = rng_offset(ctr, site);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      m[s] = dropout_keep_run<8>(seed, off, rbase + 512 * s + 8 * lane, thresh);
+  }
+  // c: a constant after unrolling, so m[] stays in registers
+  __device__ __forceinline__ bool keep(int c, int lane) const {
+    const int col = c * 64 + lane;
+    const uint32_t mm = (uint32_t)__shfl((int)m[c >> 3], (col >> 3) & 63, 64);
+    return (mm >> (col & 7)) & 1u;
+  }
+};
 
 // dtable[tok[row]] += drop_mask * dout[row] * scale  (f32 atomics into the
 // f32 master-gradient buffer; rows of 2*D bytes per wave-instruction pair).
@@ -56,12 +76,14 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
   const long long t = (long long)tok[row];
   const size_t rbase = (size_t)row * D;
   const float sc = p > 0.f ? scale / (1.f - p) : scale;
+  RowKeep<D> rk;
+  if (p > 0.f) rk.draw(seed, ctr, site, rbase, lane, thresh);
   // column c*64+lane: every atomic wave-instruction covers 256 contiguous bytes
 #pragma unroll
   for (int c = 0; c < VEC; ++c) {
     const int col = c * 64 + lane;
     float g = bf2f(dout[rbase + col]) * sc;
-    if (p > 0.f && !dropout_keep(seed, ctr, site, rbase + col, thresh)) g = 0.f;
+    if (p > 0.f && !rk.keep(c, lane)) g = 0.f;
     atomicAdd(dtable + t * D + col, g);
   }
 }
@@ -83,11 +105,13 @@ __global__ __launch_bounds__(256) void embed_bwd_fx_kernel(
   const long long t = (long long)tok[row];
   const size_t rbase = (size_t)row * D;
   const float sc = p > 0.f ? scale / (1.f - p) : scale;
+  RowKeep<D> rk;
+  if (p > 0.f) rk.draw(seed, ctr, site, rbase, lane, thresh);
 #pragma unroll
   for (int c = 0; c < D / 64; ++c) {
     const int col = c * 64 + lane;
     float g = bf2f(dout[rbase + col]) * sc;
-    if (p > 0.f && !dropout_keep(seed, ctr, site, rbase + col, thresh)) g = 0.f;
+    if (p > 0.f && !rk.keep(c, lane)) g = 0.f;
     const long long fx = (long long)rintf(g * FX_SCALE);
     if (fx != 0) atomicAdd(acc + t * D + col, (unsigned long long)fx);
   }
@@ -129,7 +153,7 @@ namespace {
 template <int D, typename TT>
 void fwd_d(const void* tok, const void* table, const float* pe, void* out, int M, int L,
            float scale, float p, uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
-  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  const uint32_t thresh = dropout_thresh(p);
   hipLaunchKernelGGL((embed_fwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
                      (const TT*)tok, (const bf16_t*)table, pe, (bf16_t*)out, M, L, scale, p,
                      thresh, seed, ctr, site);
@@ -137,14 +161,14 @@ void fwd_d(const void* tok, const void* table, const float* pe, void* out, int M
 template <int D, typename TT>
 void bwd_d(const void* tok, const void* dout, float* dtable, int M, float scale, float p,
            uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
-  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  const uint32_t thresh = dropout_thresh(p);
   hipLaunchKernelGGL((embed_bwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
                      (const TT*)tok, (const bf16_t*)dout, dtable, M, scale, p, thresh, seed, ctr, site);
 }
 template <int D, typename TT>
 void bwd_fx_d(const void* tok, const void* dout, unsigned long long* acc, int M, float scale, float p,
               uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
-  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  const uint32_t thresh = dropout_thresh(p);
   hipLaunchKernelGGL((embed_bwd_fx_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
                      (const TT*)tok, (const bf16_t*)dout, acc, M, scale, p, thresh, seed, ctr, site);
 }

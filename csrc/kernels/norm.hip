@@ -9,15 +9,19 @@
 //
 // Replaces the reference's `LayerNormalization(epsilon=1e-6)(x + Dropout(...))`
 // (reference: distributed_training_transformer/transformer_model.py:187-204,
-// 219-248). One wave per row; each lane owns D/64 contiguous elements
-// (vectorised 4..32-byte accesses), so D in {128, 256, 512, 1024}.
+// 219-248). One wave per row; each lane owns D/64 elements in runs of up to
+// 8 (tdg_ln.h RowMap: every access instruction is contiguous across the
+// wave), so D in {128, 256, 512, 1024}.
 #include "tdg_common.h"
 #include "tdg_ln.h"
 #include "tdg_reduce.h"
 
 namespace tdg {
 
-template <int D>
+// RPW rows per wave (4 waves per block): the loads of all of a wave's rows
+// are issued before the first row is reduced, so a row's stores overlap the
+// next rows' loads still in flight.
+template <int D, int RPW>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ s, const float* __restrict__ gamma,
     const float* __restrict__ beta, bf16_t* __restrict__ y, bf16_t* __restrict__ hsave,
@@ -26,47 +30,49 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const float* __restrict__ s8p, unsigned* __restrict__ amax8) {
   constexpr int VEC = D / 64;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   __shared__ float red8[4];
-  if (row >= M) {
-    if (y8 && lane == 0) red8[threadIdx.x >> 6] = 0.f;
-    if (y8) {
-      __syncthreads();
-      if (threadIdx.x == 0 && amax8)
-        atomic_amax(amax8 + (blockIdx.x & (AMAX_SPREAD - 1)),
-                    fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
-    }
-    return;
+  RowVec<VEC> h[RPW], t[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const size_t rbase = (size_t)min(r0 + k, M - 1) * D;
+    h[k].load_row(x + rbase, lane);
+    if (s) t[k].load_row(s + rbase, lane);
   }
-  const size_t base = (size_t)row * D + lane * VEC;
-  RowVec<VEC> h, t, o;
-  h.load_bf(x + base);
-  if (s) t.load_bf(s + base);
-  ln_row_fwd<D>(h, t, s != nullptr, base, row, lane, gamma, beta, y, hsave, mean_out, rstd_out, p,
-                thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t));
-  if (y8) {  // fused e4m3 copy of y for an fp8 GEMM (delayed per-tensor scale)
-    const float s8 = s8p[0];
-    float am = 0.f;
-    int w[(VEC + 3) / 4];
+  float am = 0.f;
 #pragma unroll
-    for (int i = 0; i < (VEC + 3) / 4; ++i) w[i] = 0;
+  for (int k = 0; k < RPW; ++k) {
+    const int row = r0 + k;
+    if (row >= M) break;
+    const size_t rbase = (size_t)row * D;
+    RowVec<VEC> o;
+    ln_row_fwd<D>(h[k], t[k], s != nullptr, rbase, row, lane, gamma, beta, y, hsave, mean_out,
+                  rstd_out, p, thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t));
+    if (y8) {  // fused e4m3 copy of y for an fp8 GEMM (delayed per-tensor scale)
+      const float s8 = s8p[0];
+      int w[(VEC + 3) / 4];
 #pragma unroll
-    for (int i = 0; i < VEC; i += 2) {
-      const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
-      am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
-      if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
-      else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+      for (int i = 0; i < (VEC + 3) / 4; ++i) w[i] = 0;
+#pragma unroll
+      for (int i = 0; i < VEC; i += 2) {
+        const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
+        am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
+        if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
+        else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+      }
+      uint8_t* dst = y8 + rbase + lane * RowMap<VEC>::W;
+      if constexpr (VEC == 2) {
+        *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
+      } else if constexpr (VEC == 4) {
+        *reinterpret_cast<int*>(dst) = w[0];
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC / 8; ++i)
+          *reinterpret_cast<int2*>(dst + 512 * i) = make_int2(w[2 * i], w[2 * i + 1]);
+      }
     }
-    uint8_t* dst = y8 + base;
-    if constexpr (VEC == 2) {
-      *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
-    } else if constexpr (VEC == 4) {
-      *reinterpret_cast<int*>(dst) = w[0];
-    } else {
-#pragma unroll
-      for (int i = 0; i < VEC / 8; ++i)
-        *reinterpret_cast<int2*>(dst + 8 * i) = make_int2(w[2 * i], w[2 * i + 1]);
-    }
+  }
+  if (y8) {
     am = wave_max(am);
     if (lane == 0) red8[threadIdx.x >> 6] = am;
     __syncthreads();
@@ -80,8 +86,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 // a wave's rows are issued before any of them is used (one memory latency per
 // wave instead of one per row). Partial column sums go to part_g / part_b /
 // part_s [gridDim.x, D].
-template <int D, int RPW>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(
+template <int D, int RPW, int NWV>
+__global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const float* __restrict__ gamma, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ ds_out,
@@ -89,14 +95,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
     const long long* ctr, uint64_t site, int iters) {
   constexpr int VEC = D / 64;
-  __shared__ float red[3][4][D];
+  __shared__ float red[3][NWV][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float ag[VEC], ab[VEC], as[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) ag[i] = ab[i] = as[i] = 0.f;
   float gm[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) gm[i] = gamma[lane * VEC + i];
+  for (int i = 0; i < VEC; ++i) gm[i] = gamma[RowMap<VEC>::col(lane, i)];
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const WtBuf wdh(dh_out, (size_t)M * D * sizeof(bf16_t));  // write-through outputs
   const WtBuf wds(ds_out ? ds_out : dh_out, (size_t)M * D * sizeof(bf16_t));
@@ -104,17 +110,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   // (fewer partial rows for the fold: D = 1024 uses 2)
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
-  const int r0 = (blockIdx.x * iters + it) * (4 * RPW) + w * RPW;
+  const int r0 = (blockIdx.x * iters + it) * (NWV * RPW) + w * RPW;
   if (r0 >= M) break;
   RowVec<VEC> g[RPW], h[RPW], e[RPW];
   float mean[RPW], rstd[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
     const int row = min(r0 + k, M - 1);
-    const size_t base = (size_t)row * D + lane * VEC;
-    g[k].load_bf(dy + base);
-    h[k].load_bf(hsave + base);
-    if (dres_in) e[k].load_bf(dres_in + base);
+    const size_t rbase = (size_t)row * D;
+    g[k].load_row(dy + rbase, lane);
+    h[k].load_row(hsave + rbase, lane);
+    if (dres_in) e[k].load_row(dres_in + rbase, lane);
     mean[k] = mean_in[row];
     rstd[k] = rstd_in[row];
   }
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int k = 0; k < RPW; ++k) {
     const int row = r0 + k;
     if (row >= M) break;
-    const size_t base = (size_t)row * D + lane * VEC;
+    const size_t rbase = (size_t)row * D;
     float sg = 0.f, sgx = 0.f;
     float xh[VEC];
 #pragma unroll
@@ -141,12 +147,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int i = 0; i < VEC; ++i) dh.v[i] = rstd[k] * (g[k].v[i] * gm[i] - sg - xh[i] * sgx);
     RowVec<VEC> ds = dh;
     if (p > 0.f) {
-      const uint32_t km = keep_bits<VEC>(seed, ctr, site, base, thresh);
+      const uint32_t km = keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) ds.v[i] = ((km >> i) & 1u) ? dh.v[i] * sc : 0.f;
     }
     if (ds_out) {
-      ds.store_bf(ds_out + base, wds);
+      ds.store_row(ds_out + rbase, lane, wds);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
     }
@@ -154,20 +160,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < VEC; ++i) dh.v[i] += e[k].v[i];
     }
-    dh.store_bf(dh_out + base, wdh);
+    dh.store_row(dh_out + rbase, lane, wdh);
   }
   }  // row groups
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
-    red[0][w][lane * VEC + i] = ag[i];
-    red[1][w][lane * VEC + i] = ab[i];
-    red[2][w][lane * VEC + i] = as[i];
+    const int col = RowMap<VEC>::col(lane, i);
+    red[0][w][col] = ag[i];
+    red[1][w][col] = ab[i];
+    red[2][w][col] = as[i];
   }
   __syncthreads();
-  for (int col = threadIdx.x; col < D; col += 256) {
+  for (int col = threadIdx.x; col < D; col += NWV * 64) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NWV; ++k) {
       a0 += red[0][k][col];
       a1 += red[1][k][col];
       a2 += red[2][k][col];
@@ -188,8 +195,10 @@ void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* bet
               void* hsave, float* mean, float* rstd, int M, float p, uint64_t seed,
               const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
               unsigned* amax8, hipStream_t st) {
-  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
-  hipLaunchKernelGGL(ln_fwd_kernel<D>, dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
+  const uint32_t thresh = dropout_thresh(p);
+  // one row per wave measured best with dropout (2 rows: 8.1 vs 8.2 us
+  // without, 11.1 vs 9.3 us with, D = 1024 x 8192 rows)
+  hipLaunchKernelGGL((ln_fwd_kernel<D, 1>), dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)s, gamma, beta, (bf16_t*)y, (bf16_t*)hsave, mean, rstd, M, p,
                      thresh, seed, ctr, site, eps, (uint8_t*)y8, s8, amax8);
 }
@@ -198,17 +207,18 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
               int accumulate, int skip_reduce, hipStream_t st) {
-  const uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
-  constexpr int RPW = D >= 1024 ? 2 : 4;
-  constexpr int ITERS = D >= 1024 ? 2 : 1;  // keep in sync with kernels.py ln_bwd_nparts
-  const int rpb = 4 * RPW * ITERS;
+  const uint32_t thresh = dropout_thresh(p);
+  // 16 rows per block whatever the variant (kernels.py ln_bwd_nparts)
+  // (2 or 1 rows per wave on 8 or 16 waves per block measured within +-10 %)
+  constexpr int RPW = D >= 1024 ? 2 : 4, NWV = 4, rpb = 16;
   const int nb = cdiv(M, rpb);
   float* pg = ws;
   float* pb = ws + (size_t)nb * D;
   float* ps = dbias ? ws + 2 * (size_t)nb * D : nullptr;
-  hipLaunchKernelGGL((ln_bwd_kernel<D, RPW>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
-                     (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site, ITERS);
+  hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, NWV>), dim3(nb), dim3(NWV * 64), 0, st,
+                     (const bf16_t*)dy, (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh,
+                     (bf16_t*)ds, (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
+                     rpb / (RPW * NWV));
   if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};

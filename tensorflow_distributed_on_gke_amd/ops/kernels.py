@@ -380,10 +380,8 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
 
 
 def ln_bwd_nparts(M: int, D: int) -> int:
-    """Partial-sum rows ln_bwd writes (norm.hip ln_bwd_d: 4 waves x RPW rows x
-    ITERS row groups per block)."""
-    rpw, iters = (2, 2) if D >= 1024 else (4, 1)
-    return math.ceil(M / (4 * rpw * iters))
+    """Partial-sum rows ln_bwd writes (norm.hip ln_bwd_d: 16 rows per block)."""
+    return math.ceil(M / 16)
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,

@@ -1,8 +1,9 @@
 """Host/CPU reference of the device dropout RNG (Philox4x32-10).
 
 Bit-identical to `csrc/include/tdg_common.h`: the keep decision for element
-`e` of a dropout site is word `e % 4` of Philox(counter=(e//4, offset),
-key=seed) compared against `p * 2**32`, with offset = ctr * 4096 + site.
+`e` of a dropout site is the 16-bit half `e % 2` of word `(e % 8) // 2` of
+Philox(counter=(e//8, offset), key=seed), kept iff >= rint(p * 2**16) (f32
+arithmetic, as on the device), with offset = ctr * 4096 + site.
 Used by the CPU reference ops so that CPU and GPU runs draw identical masks.
 """
 from __future__ import annotations
@@ -58,13 +59,20 @@ def philox4x32(seed: int, offset: int, idx: torch.Tensor):
     return c0, c1, c2, c3
 
 
+def dropout_thresh(p: float) -> int:
+    """rint(p * 2**16) in f32, clamped to 2**16 (tdg_common.h dropout_thresh)."""
+    t = torch.tensor(p, dtype=torch.float32) * torch.tensor(65536.0, dtype=torch.float32)
+    return int(min(65536.0, float(torch.round(t))))
+
+
 def keep_mask(seed: int, offset: int, n: int, p: float) -> torch.Tensor:
     """Boolean keep mask for elements 0..n-1 of a dropout site."""
-    thresh = min(0xFFFFFFFF, int(p * 4294967296.0))
-    groups = (n + 3) // 4
+    thresh = dropout_thresh(p)
+    groups = (n + 7) // 8
     w = philox4x32(seed, offset, torch.arange(groups, dtype=torch.int64))
-    words = torch.stack(w, dim=1).reshape(-1)[:n]
-    return words >= thresh
+    words = torch.stack(w, dim=1)  # [groups, 4]
+    halves = torch.stack([words & 0xFFFF, words >> 16], dim=2).reshape(-1)[:n]
+    return halves >= thresh
 
 
 def rng_offset(ctr: int, site: int) -> int:
