@@ -135,6 +135,27 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// The same vmcnt wait as a builtin: unlike the asm form, the compiler's
+// waitcnt pass sees it, so registers loaded from global memory before the N
+// younger operations are known complete after it (no vmcnt(0) of its own
+// before their first use, e.g. inside a loop that also has LDS-DMA in flight).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_known() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// vmcnt wait leaving `n` younger tiles (PT LDS-DMA each) in flight
+template <int PT, int NMAX>
+__device__ __forceinline__ void wait_tiles(int n) {
+  static_assert(NMAX <= 4 && PT * NMAX <= 63, "vmcnt range");
+  if (NMAX >= 4 && n >= 4) { wait_vmcnt<(NMAX >= 4 ? 4 * PT : 0)>(); return; }
+  if (NMAX >= 3 && n >= 3) { wait_vmcnt<(NMAX >= 3 ? 3 * PT : 0)>(); return; }
+  if (NMAX >= 2 && n >= 2) { wait_vmcnt<(NMAX >= 2 ? 2 * PT : 0)>(); return; }
+  if (NMAX >= 1 && n >= 1) { wait_vmcnt<PT>(); return; }
+  wait_vmcnt<0>();
+}
+
 // Workgroup barrier that does NOT drain in-flight LDS-DMA (no vmcnt(0)).
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

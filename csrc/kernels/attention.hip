@@ -23,12 +23,18 @@
 // gradients are bitwise deterministic.
 #include "tdg_common.h"
 #include "tdg_attn.h"
+#include "tdg_gemm.h"
 
 #include <cstdlib>
 
 namespace tdg {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+// v_exp_f32 as is: libm's exp2f wraps it in a denormal-range fix-up (compare,
+// select, ldexp: 4 more VALU per element); softmax weights below 2^-126
+// flushed to zero change nothing at bf16 P.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // Key window and logit scale of batch row b. A row with NO valid key
 // (kv_len == 0: an all-PAD sequence) gets the reference's numerics: its
@@ -124,6 +130,25 @@ struct ATile {
       return *reinterpret_cast<const short8_t*>(lds + off(row, c * 16));
     }
   }
+  // The same row fragment read untracked (tdg_common.h lds_read_b128_async):
+  // for loops with LDS-DMA in flight, where the compiler would put a
+  // vmcnt(0) before a tracked read; the caller waits (lgkm_wait) and ties.
+  __device__ static __forceinline__ short8_t frag_row_async(const char* lds, int rbase, int s, int lane) {
+    static_assert(HD >= 32, "untracked row fragments: hd >= 32");
+    const int row = rbase + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return lds_read_b128_async(lds + off(row, c * 16));
+  }
+  // Transposed fragment, untracked, as its two 8-byte halves (tie both
+  // after the wait, then cat4)
+  __device__ static __forceinline__ void frag_tr_async(const char* lds, int s2, int dt, int lane,
+                                                       short4_t& lo, short4_t& hi) {
+    const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+    const int r1 = 32 * s2 + 4 * g + q;
+    const int byte = (16 * dt + 4 * p) * 2;
+    lo = lds_read_tr_async(lds + off(r1, byte));
+    hi = lds_read_tr_async(lds + off(r1 + 16, byte));
+  }
   // Transposed fragment over 32 rows (k-step s2 of a 64-row tile), head-dim
   // columns 16dt..16dt+15. Element j of lane group g is row
   // 32s2 + (j<4 ? 4g+j : 16+4g+j-4) (the key/query permutation that matches
@@ -148,23 +173,104 @@ __device__ __forceinline__ short8_t gfrag(const bf16_t* __restrict__ rowp, bool 
 
 
 
+// One key tile of the online softmax for the lane's query row (swapped
+// QK^T: s[t][r] = S[key = k0 + 16t + 4g + r][row], raw logits). m is the
+// running max in the scaled log2 domain (max of c*S), l the running sum.
+// Per element: a max, one FMA, one exp2, one add (and the mask compare only
+// on tiles that need it: the key-window edge, the causal diagonal); the
+// O rescale runs only when some lane's max grew (exact: alpha = 1 otherwise).
+// Writes the tile's P as bf16 MFMA operands (pairs of 16-key tiles).
+// Does the key tile [k0, k0 + kt) need the per-element mask for a wave whose
+// first query row is wq0 (wave-uniform)?
+__device__ __forceinline__ bool tile_masked(int k0, int kt, int klim, bool causal, int wq0) {
+  return k0 + kt > klim || (causal && k0 + kt - 1 > wq0);
+}
+
+// (split in two so that LDS reads can be issued between them: the max part
+// has the cross-lane shuffles, the exp part no LDS access)
+// (a masked tile is scaled while masking -- masked logits -inf, the others
+// c*S -- so that c = 0, the zero logit scale of a kv_len = 0 row, never meets
+// an infinity in a product; unmasked tiles keep raw logits and fold c into
+// the exp's FMA)
+template <int NT16, int DT>
+__device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l, f32x4 (&oacc)[DT],
+                                            bool masked, int k0, int klim, bool causal, int qrow,
+                                            int g, float c) {
+  if (masked) {
+#pragma unroll
+    for (int t = 0; t < NT16; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * t + 4 * g + r;
+        s[t][r] = key < klim && (!causal || key <= qrow) ? s[t][r] * c : -INFINITY;
+      }
+  }
+  float tmax = s[0][0];
+#pragma unroll
+  for (int t = 0; t < NT16; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[t][r]);
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  const float mn = fmaxf(m, masked ? tmax : tmax * c);
+  if (__ballot(mn > m)) {  // wave-uniform: rescale only when a row max grew
+    const float alpha = fast_exp2(m - mn);  // m = -inf (nothing yet): 0, and O, l are 0
+#pragma unroll
+    for (int i = 0; i < DT; ++i) oacc[i] *= alpha;
+    l *= alpha;
+    m = mn;
+  }
+}
+// cs: c for a raw (unmasked) tile, 1 for a masked (already scaled) one
+template <int NT16>
+__device__ __forceinline__ void softmax_exp(f32x4 (&s)[NT16], float m, float& l,
+                                            short8_t (&pf)[NT16 / 2], float cs) {
+  const float nm = m == -INFINITY ? 0.f : -m;  // all masked so far: exp2(-inf) = 0, no NaN
+  float rs = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT16; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = fast_exp2(fmaf(s[t][r], cs, nm));
+      s[t][r] = p;
+      rs += p;
+    }
+  l += rs;
+#pragma unroll
+  for (int s2 = 0; s2 < NT16 / 2; ++s2)
+    pf[s2] = pack8(s[2 * s2][0], s[2 * s2][1], s[2 * s2][2], s[2 * s2][3], s[2 * s2 + 1][0],
+                   s[2 * s2 + 1][1], s[2 * s2 + 1][2], s[2 * s2 + 1][3]);
+}
+template <int NT16, int DT>
+__device__ __forceinline__ void softmax_tile(f32x4 (&s)[NT16], float& m, float& l,
+                                             f32x4 (&oacc)[DT], short8_t (&pf)[NT16 / 2],
+                                             bool masked, int k0, int klim, bool causal, int qrow,
+                                             int g, float c) {
+  softmax_max<NT16, DT>(s, m, l, oacc, masked, k0, klim, causal, qrow, g, c);
+  softmax_exp<NT16>(s, m, l, pf, masked ? 1.f : c);
+}
+
 // ============================================================================ forward
-// NWV waves per workgroup, 16 query rows per wave (NWV = 8 covers a whole
-// <= 128-query sequence, so K/V are read from HBM once per (batch, head)).
+// NWV waves per workgroup, U 16-query subtiles per wave (16 U NWV queries per
+// workgroup; 8 x 1 covers a whole <= 128-query sequence, so K/V are read from
+// HBM once per (batch, head)). Each K / V fragment read from LDS feeds U
+// MFMAs: with U = 1 the fragment reads alone saturate the LDS at the MFMA
+// rate (1 KiB per 16-cycle MFMA per wave), U = 2 halves them.
 // KT keys per LDS tile (64 or 128: one load phase and one barrier pair for a
 // whole <= 128-key sequence).
-template <int HD, int NWV, int KT>
-__global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
+template <int HD, int NWV, int KT, int U>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(AttnArgs a) {
   using T = ATile<HD>;
-  constexpr int QBW = 16 * NWV;
+  constexpr int QBW = 16 * NWV * U;
   constexpr int NT16 = KT / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
   char* ldsV = smem + (KT / 64) * T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
-  const int qrow = q0 + 16 * w + cl;
-  const bool qvalid = qrow < a.Lq;
+  int qrow[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
   int klim;
   float scl;
   bool causal;
@@ -172,19 +278,29 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
   if (causal) klim = min(klim, q0 + QBW);
 
   TDG_STAMP(0);
-  const bf16_t* qp = a.q + b * a.q_sb + (long long)min(qrow, a.Lq - 1) * a.q_sl + h * a.q_sh;
-  short8_t qf[T::KS];
+  short8_t qf[U][T::KS];
 #pragma unroll
-  for (int s = 0; s < T::KS; ++s) qf[s] = gfrag<HD>(qp, qvalid, s, lane);
+  for (int u = 0; u < U; ++u) {
+    const bf16_t* qp = a.q + b * a.q_sb + (long long)min(qrow[u], a.Lq - 1) * a.q_sl + h * a.q_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) qf[u][s] = gfrag<HD>(qp, qrow[u] < a.Lq, s, lane);
+  }
 
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
   const float c = scl * LOG2E;
+  constexpr int KTILE = KT;
+  const int wq0 = q0 + 16 * U * w;
 
-  f32x4 oacc[T::DT];
+  f32x4 oacc[U][T::DT];
+  float m[U], l[U];
 #pragma unroll
-  for (int i = 0; i < T::DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int u = 0; u < U; ++u) {
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) oacc[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // K / V tiles staged global -> registers -> LDS; the NEXT tile's loads are
   // issued right after the current one is in LDS, so they are in flight
@@ -208,73 +324,53 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
     if (k0 == 0) TDG_STAMP(1);
     if (k0 + KT < klim) fetch_kv(k0 + KT);
-    f32x4 s[NT16];
+    f32x4 s[U][NT16];
 #pragma unroll
     for (int t = 0; t < NT16; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < T::KS; ++ks) s[t] = mfma16(T::frag_row(ldsK, 16 * t, ks, lane), qf[ks], s[t]);
+      for (int u = 0; u < U; ++u) s[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) {
+        const short8_t kfr = T::frag_row(ldsK, 16 * t, ks, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u][t] = mfma16(kfr, qf[u][ks], s[u][t]);
+      }
     }
-    // mask + scale (log2 domain); s[t][r] = S[key=k0+16t+4g+r][q=qrow]
-    float tmax = -INFINITY;
+    short8_t pf[U][NT16 / 2];
 #pragma unroll
-    for (int t = 0; t < NT16; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * t + 4 * g + r;
-        const bool ok = key < klim && (!causal || key <= qrow);
-        const float v = ok ? s[t][r] * c : -INFINITY;
-        s[t][r] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-    float rs = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT16; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mn == -INFINITY) ? 0.f : exp2f(s[t][r] - mn);
-        s[t][r] = p;
-        rs += p;
-      }
-    l = l * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int i = 0; i < T::DT; ++i) oacc[i] *= alpha;
+    for (int u = 0; u < U; ++u)
+      softmax_tile<NT16, T::DT>(s[u], m[u], l[u], oacc[u], pf[u], tile_masked(k0, KTILE, klim, causal, wq0),
+                                k0, klim, causal, qrow[u], g, c);
 #pragma unroll
     for (int s2 = 0; s2 < NT16 / 2; ++s2) {
-      const short8_t pf = pack8(s[2 * s2][0], s[2 * s2][1], s[2 * s2][2], s[2 * s2][3],
-                                s[2 * s2 + 1][0], s[2 * s2 + 1][1], s[2 * s2 + 1][2],
-                                s[2 * s2 + 1][3]);
 #pragma unroll
-      for (int dt = 0; dt < T::DT; ++dt) oacc[dt] = mfma16(T::frag_tr(ldsV, s2, dt, lane), pf, oacc[dt]);
+      for (int dt = 0; dt < T::DT; ++dt) {
+        const short8_t vfr = T::frag_tr(ldsV, s2, dt, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) oacc[u][dt] = mfma16(vfr, pf[u][s2], oacc[u][dt]);
+      }
     }
     __syncthreads();
   }
   TDG_STAMP(2);
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-#ifdef TDG_STAMPS
-  if (!qvalid) {
-    TDG_STAMP(3);
-    TDG_STAMP(4);
-    return;
-  }
-#endif
-  if (!qvalid) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16_t* op = a.out + b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
 #pragma unroll
-  for (int dt = 0; dt < T::DT; ++dt) {
-    // rows d = 16dt + 4g + r
-    uint32_t lo = (uint32_t)f2bf(oacc[dt][0] * inv) | ((uint32_t)f2bf(oacc[dt][1] * inv) << 16);
-    uint32_t hi = (uint32_t)f2bf(oacc[dt][2] * inv) | ((uint32_t)f2bf(oacc[dt][3] * inv) << 16);
-    *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+  for (int u = 0; u < U; ++u) {
+    float lu = l[u];
+    lu += __shfl_xor(lu, 16, 64);
+    lu += __shfl_xor(lu, 32, 64);
+    if (qrow[u] >= a.Lq) continue;
+    const float inv = lu > 0.f ? 1.f / lu : 0.f;
+    bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      // rows d = 16dt + 4g + r
+      uint32_t lo = (uint32_t)f2bf(oacc[u][dt][0] * inv) | ((uint32_t)f2bf(oacc[u][dt][1] * inv) << 16);
+      uint32_t hi = (uint32_t)f2bf(oacc[u][dt][2] * inv) | ((uint32_t)f2bf(oacc[u][dt][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+    if (g == 0)
+      a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + log2f(lu) : INFINITY;
   }
-  if (g == 0) a.lse[((long long)b * a.H + h) * a.Lq + qrow] = l > 0.f ? m + log2f(l) : INFINITY;
 #ifdef TDG_STAMPS
   TDG_STAMP(3);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -282,38 +378,192 @@ __global__ __launch_bounds__(NWV * 64) void attn_fwd_kernel(AttnArgs a) {
 #endif
 }
 
-// ============================================================================ dK, dV
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+// ============================================================================ forward, long sequences
+// hd = 64, Lq > 128. The K / V tiles (64 keys) stream through an NS-slot LDS
+// ring by LDS-DMA (Glds: the ATile<64> image is the GEMM's K-contiguous
+// 64-row image), NS-1 tiles in flight and one barrier per tile -- instead of
+// global -> register -> LDS with one tile of register prefetch, which left
+// the 512-key sequences latency-bound (0.31 PF/s). NWV waves x U 16-query
+// subtiles per wave; the K / V fragment reads are shared by the U subtiles.
+template <int NWV, int U, int NS>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_pipe_kernel(AttnArgs a) {
+  constexpr int HD = 64;
   using T = ATile<HD>;
+  using G = Glds<true, 64, NWV>;  // 64 rows x 64 head-dim elements
+  constexpr int QBW = 16 * NWV * U;
+  constexpr int NT16 = 4;             // 16-key tiles per 64-key tile
+  constexpr int SLOT = 2 * T::BYTES;  // K image, V image
+  constexpr int PT = 2 * G::P;        // LDS-DMA per wave per tile
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int qrow[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q0 + QBW);
+  const int nkt = (klim + 63) / 64;
+
+  short8_t qf[U][T::KS];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bf16_t* qp = a.q + b * a.q_sb + (long long)min(qrow[u], a.Lq - 1) * a.q_sl + h * a.q_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) qf[u][s] = gfrag<HD>(qp, qrow[u] < a.Lq, s, lane);
+  }
+  const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+  G gs;
+  gs.init(w, lane);
+  auto issue = [&](int kt) {
+    char* slot = smem + (kt % NS) * SLOT;
+    gs.issue(kb, (int)a.k_sl, a.Lk, HD, 64 * kt, 0, slot, w);
+    gs.issue(vb, (int)a.v_sl, a.Lk, HD, 64 * kt, 0, slot + T::BYTES, w);
+  };
+  // prologue tiles issued unconditionally (clamped rows past the sequence,
+  // never read) so the DMA count behind the Q loads is a constant
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  wait_vmcnt_known<(NS - 1) * PT>();  // Q fragments in registers
+
+  const float c = scl * LOG2E;
+  constexpr int KTILE = 64;
+  const int wq0 = q0 + 16 * U * w;
+  f32x4 oacc[U][T::DT];
+  float m[U], l[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) oacc[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    // tile kt landed (this wave's DMA, then everyone's); every wave is past
+    // its reads of tile kt-1, whose slot takes tile kt+NS-1
+    wait_tiles<PT, NS - 2>(min(NS - 2, nkt - 1 - kt));
+    lds_barrier();
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+    const char* ldsK = smem + (kt % NS) * SLOT;
+    const char* ldsV = ldsK + T::BYTES;
+    const int k0 = 64 * kt;
+    // all LDS reads of the tile untracked (a tracked read would get a
+    // vmcnt(0) for the DMA in flight), with counted waits: K fragments in
+    // two halves, V fragments issued between the softmax's max and exp parts
+    short8_t kfr[NT16][T::KS];
+#pragma unroll
+    for (int t = 0; t < NT16; ++t)
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) kfr[t][ks] = T::frag_row_async(ldsK, 16 * t, ks, lane);
+    f32x4 s[U][NT16];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half == 0) lgkm_wait<NT16 * T::KS / 2>();
+      else lgkm_wait<0>();
+#pragma unroll
+      for (int t = half * NT16 / 2; t < (half + 1) * NT16 / 2; ++t) {
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) tie(kfr[t][ks]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          s[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < T::KS; ++ks) s[u][t] = mfma16(kfr[t][ks], qf[u][ks], s[u][t]);
+        }
+      }
+    }
+    const bool msk = tile_masked(k0, KTILE, klim, causal, wq0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      softmax_max<NT16, T::DT>(s[u], m[u], l[u], oacc[u], msk, k0, klim, causal, qrow[u], g, c);
+    short4_t vlo[NT16 / 2][T::DT], vhi[NT16 / 2][T::DT];
+#pragma unroll
+    for (int s2 = 0; s2 < NT16 / 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) T::frag_tr_async(ldsV, s2, dt, lane, vlo[s2][dt], vhi[s2][dt]);
+    short8_t pf[U][NT16 / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) softmax_exp<NT16>(s[u], m[u], l[u], pf[u], msk ? 1.f : c);
+#pragma unroll
+    for (int s2 = 0; s2 < NT16 / 2; ++s2) {
+      if (s2 == 0) lgkm_wait<2 * T::DT>();
+      else lgkm_wait<0>();
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) {
+        tie(vlo[s2][dt]);
+        tie(vhi[s2][dt]);
+        const short8_t vfr = cat4(vlo[s2][dt], vhi[s2][dt]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) oacc[u][dt] = mfma16(vfr, pf[u][s2], oacc[u][dt]);
+      }
+    }
+  }
+  wait_vmcnt<0>();  // (nothing in flight on the exit paths; keeps the grid drained)
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float lu = l[u];
+    lu += __shfl_xor(lu, 16, 64);
+    lu += __shfl_xor(lu, 32, 64);
+    if (qrow[u] >= a.Lq) continue;
+    const float inv = lu > 0.f ? 1.f / lu : 0.f;
+    bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      uint32_t lo = (uint32_t)f2bf(oacc[u][dt][0] * inv) | ((uint32_t)f2bf(oacc[u][dt][1] * inv) << 16);
+      uint32_t hi = (uint32_t)f2bf(oacc[u][dt][2] * inv) | ((uint32_t)f2bf(oacc[u][dt][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+    if (g == 0)
+      a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + log2f(lu) : INFINITY;
+  }
+}
+
+// ============================================================================ dK, dV
+// 4 waves, U 16-key subtiles per wave (64 U keys per workgroup): every Q / dO
+// fragment read from LDS feeds U MFMAs.
+template <int HD, int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  using T = ATile<HD>;
+  constexpr int KBW = 64 * U;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsQ = smem;
   char* ldsO = smem + T::BYTES;  // dO tile
   float* ldsL = reinterpret_cast<float*>(smem + 2 * T::BYTES);
   float* ldsD = ldsL + QB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KB;
-  const int key = k0 + 16 * w + cl;
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KBW;
+  int key[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) key[u] = k0 + 16 * (U * w + u) + cl;
   int klim;
   float scl;
   bool causal;
   key_window(a, b, klim, scl, causal);
-  const bool kvalid = key < klim;
   const float c = scl * LOG2E;
 
-  f32x4 dk[T::DT], dv[T::DT];
+  f32x4 dk[U][T::DT], dv[U][T::DT];
 #pragma unroll
-  for (int i = 0; i < T::DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dk[u][i] = dv[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (k0 < klim) {
-    const int krow = min(key, a.Lk - 1);
-    const bf16_t* kp = a.k + b * a.k_sb + (long long)krow * a.k_sl + h * a.k_sh;
-    const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
-    short8_t kf[T::KS], vf[T::KS];
+    short8_t kf[U][T::KS], vf[U][T::KS];
 #pragma unroll
-    for (int s = 0; s < T::KS; ++s) {
-      kf[s] = gfrag<HD>(kp, key < a.Lk, s, lane);
-      vf[s] = gfrag<HD>(vp, key < a.Lk, s, lane);
+    for (int u = 0; u < U; ++u) {
+      const int krow = min(key[u], a.Lk - 1);
+      const bf16_t* kp = a.k + b * a.k_sb + (long long)krow * a.k_sl + h * a.k_sh;
+      const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
+#pragma unroll
+      for (int s = 0; s < T::KS; ++s) {
+        kf[u][s] = gfrag<HD>(kp, key[u] < a.Lk, s, lane);
+        vf[u][s] = gfrag<HD>(vp, key[u] < a.Lk, s, lane);
+      }
     }
     const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
     const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
@@ -344,107 +594,142 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
       __syncthreads();
       if (q0 + QB < a.Lq) fetch_q(q0 + QB);
       // S[q][key] and dP[q][key]: rows q = q0 + 16t + 4g + r, col key (lane)
-      f32x4 p[4], ds[4];
+      short8_t pf[U][2], dsf[U][2];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f32x4 p[U][2], ds[U][2];
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) {
-          sv = mfma16(T::frag_row(ldsQ, 16 * t, ks, lane), kf[ks], sv);
-          dpv = mfma16(T::frag_row(ldsO, 16 * t, ks, lane), vf[ks], dpv);
+        for (int tt = 0; tt < 2; ++tt) {
+          const int t = 2 * s2 + tt;
+          f32x4 sv[U], dpv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < T::KS; ++ks) {
+            const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
+            const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
+              dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * t + 4 * g + r;
+            const int q = q0 + ql;
+            const float lq = ldsL[ql], dq = ldsD[ql];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
+              const float pv = ok ? fast_exp2(sv[u][r] * c - lq) : 0.f;
+              p[u][tt][r] = pv;
+              ds[u][tt][r] = pv * (dpv[u][r] - dq);
+            }
+          }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = 16 * t + 4 * g + r;
-          const int q = q0 + ql;
-          const bool ok = kvalid && q < a.Lq && (!causal || key <= q);
-          const float pv = ok ? exp2f(sv[r] * c - ldsL[ql]) : 0.f;
-          p[t][r] = pv;
-          ds[t][r] = pv * (dpv[r] - ldsD[ql]);
+        for (int u = 0; u < U; ++u) {
+          pf[u][s2] = pack8(p[u][0][0], p[u][0][1], p[u][0][2], p[u][0][3], p[u][1][0], p[u][1][1],
+                            p[u][1][2], p[u][1][3]);
+          dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                             ds[u][1][1], ds[u][1][2], ds[u][1][3]);
         }
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const short8_t pf = pack8(p[2 * s2][0], p[2 * s2][1], p[2 * s2][2], p[2 * s2][3],
-                                  p[2 * s2 + 1][0], p[2 * s2 + 1][1], p[2 * s2 + 1][2],
-                                  p[2 * s2 + 1][3]);
-        const short8_t dsf = pack8(ds[2 * s2][0], ds[2 * s2][1], ds[2 * s2][2], ds[2 * s2][3],
-                                   ds[2 * s2 + 1][0], ds[2 * s2 + 1][1], ds[2 * s2 + 1][2],
-                                   ds[2 * s2 + 1][3]);
 #pragma unroll
         for (int dt = 0; dt < T::DT; ++dt) {
-          dv[dt] = mfma16(T::frag_tr(ldsO, s2, dt, lane), pf, dv[dt]);
-          dk[dt] = mfma16(T::frag_tr(ldsQ, s2, dt, lane), dsf, dk[dt]);
+          const short8_t ot = T::frag_tr(ldsO, s2, dt, lane);
+          const short8_t qt = T::frag_tr(ldsQ, s2, dt, lane);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            dv[u][dt] = mfma16(ot, pf[u][s2], dv[u][dt]);
+            dk[u][dt] = mfma16(qt, dsf[u][s2], dk[u][dt]);
+          }
         }
       }
       __syncthreads();
     }
   }
-  if (key >= a.Lk) return;
-  bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key * a.dk_sl + h * a.dk_sh;
-  bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key * a.dv_sl + h * a.dv_sh;
 #pragma unroll
-  for (int dt = 0; dt < T::DT; ++dt) {
+  for (int u = 0; u < U; ++u) {
+    if (key[u] >= a.Lk) continue;
+    bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
+    bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
     const float sc = a.scale;
-    uint32_t lo = (uint32_t)f2bf(dk[dt][0] * sc) | ((uint32_t)f2bf(dk[dt][1] * sc) << 16);
-    uint32_t hi = (uint32_t)f2bf(dk[dt][2] * sc) | ((uint32_t)f2bf(dk[dt][3] * sc) << 16);
-    *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    lo = (uint32_t)f2bf(dv[dt][0]) | ((uint32_t)f2bf(dv[dt][1]) << 16);
-    hi = (uint32_t)f2bf(dv[dt][2]) | ((uint32_t)f2bf(dv[dt][3]) << 16);
-    *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
+      uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+      lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
+      hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
+      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
   }
 }
 
 // ============================================================================ dQ
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+// 4 waves, U 16-query subtiles per wave (64 U queries per workgroup): every
+// K / V fragment read from LDS feeds U MFMAs.
+template <int HD, int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(AttnArgs a) {
   using T = ATile<HD>;
+  constexpr int QBW = 64 * U;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
   char* ldsV = smem + T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QB;
-  const int qrow = q0 + 16 * w + cl;
-  const bool qvalid = qrow < a.Lq;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int qrow[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
   int klim;
   float scl;
   bool causal;
   key_window(a, b, klim, scl, causal);
-  if (causal) klim = min(klim, q0 + QB);
+  if (causal) klim = min(klim, q0 + QBW);
   const float c = scl * LOG2E;
-  const int qr = min(qrow, a.Lq - 1);
-  const bf16_t* qp = a.q + b * a.q_sb + (long long)qr * a.q_sl + h * a.q_sh;
-  const bf16_t* dop = a.dout + b * a.do_sb + (long long)qr * a.do_sl + h * a.do_sh;
-  short8_t qf[T::KS], of[T::KS];
+  short8_t qf[U][T::KS], of[U][T::KS];
+  float L[U], D[U];
 #pragma unroll
-  for (int s = 0; s < T::KS; ++s) {
-    qf[s] = gfrag<HD>(qp, qvalid, s, lane);
-    of[s] = gfrag<HD>(dop, qvalid, s, lane);
-  }
-  const long long bh = ((long long)b * a.H + h) * a.Lq + qr;
-  const float L = a.lse[bh];
-  // delta = rowsum(dO * O) of this lane's query row, from the dO fragments
-  // already in registers and the matching O fragments (the 4 lane groups g
-  // hold disjoint head-dim slices); written for the dK/dV kernel, which runs
-  // after this one -- no separate delta pass over O and dO
-  float D = 0.f;
-  {
+  for (int u = 0; u < U; ++u) {
+    const bool qvalid = qrow[u] < a.Lq;
+    const int qr = min(qrow[u], a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.q_sb + (long long)qr * a.q_sl + h * a.q_sh;
+    const bf16_t* dop = a.dout + b * a.do_sb + (long long)qr * a.do_sl + h * a.do_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) {
+      qf[u][s] = gfrag<HD>(qp, qvalid, s, lane);
+      of[u][s] = gfrag<HD>(dop, qvalid, s, lane);
+    }
+    const long long bh = ((long long)b * a.H + h) * a.Lq + qr;
+    L[u] = a.lse[bh];
+    // delta = rowsum(dO * O) of this lane's query row, from the dO fragments
+    // already in registers and the matching O fragments (the 4 lane groups g
+    // hold disjoint head-dim slices); written for the dK/dV kernel, which runs
+    // after this one -- no separate delta pass over O and dO
+    float d = 0.f;
     const bf16_t* opr = a.o + b * a.o_sb + (long long)qr * a.o_sl + h * a.o_sh;
 #pragma unroll
     for (int s = 0; s < T::KS; ++s) {
       const short8_t ov = gfrag<HD>(opr, qvalid, s, lane);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) D += bf2f((bf16_t)of[s][e]) * bf2f((bf16_t)ov[e]);
+      for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[e]);
     }
-    D += __shfl_xor(D, 16, 64);
-    D += __shfl_xor(D, 32, 64);
-    if (qvalid && g == 0) a.delta[bh] = D;
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    if (qvalid && g == 0) a.delta[bh] = d;
+    D[u] = d;
   }
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
-  f32x4 dq[T::DT];
+  f32x4 dq[U][T::DT];
 #pragma unroll
-  for (int i = 0; i < T::DT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dq[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // K / V of key block k0+KB in registers while block k0 is computed
   typename T::template Chunks<256> ck, cv;
@@ -460,41 +745,353 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       T::template fetch<256>(ck, kb, a.k_sl, k0 + KB, a.Lk, tid);
       T::template fetch<256>(cv, vb, a.v_sl, k0 + KB, a.Lk, tid);
     }
-    f32x4 ds[4];
+    short8_t dsf[U][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f32x4 ds[U][2];
 #pragma unroll
-      for (int ks = 0; ks < T::KS; ++ks) {
-        sv = mfma16(T::frag_row(ldsK, 16 * t, ks, lane), qf[ks], sv);
-        dpv = mfma16(T::frag_row(ldsV, 16 * t, ks, lane), of[ks], dpv);
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * s2 + tt;
+        f32x4 sv[U], dpv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          const short8_t kfr = T::frag_row(ldsK, 16 * t, ks, lane);
+          const short8_t vfr = T::frag_row(ldsV, 16 * t, ks, lane);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            sv[u] = mfma16(kfr, qf[u][ks], sv[u]);
+            dpv[u] = mfma16(vfr, of[u][ks], dpv[u]);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * t + 4 * g + r;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
+            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+            ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
+          }
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * t + 4 * g + r;
-        const bool ok = qvalid && key < klim && (!causal || key <= qrow);
-        const float pv = ok ? exp2f(sv[r] * c - L) : 0.f;
-        ds[t][r] = pv * (dpv[r] - D);
+      for (int u = 0; u < U; ++u)
+        dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                           ds[u][1][1], ds[u][1][2], ds[u][1][3]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) {
+        const short8_t kt = T::frag_tr(ldsK, s2, dt, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(kt, dsf[u][s2], dq[u][dt]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (qrow[u] >= a.Lq) continue;
+    bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow[u] * a.dq_sl + h * a.dq_sh;
+    const float sc = a.scale;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
+      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+  }
+}
+
+// ============================================================================ backward, long sequences, pipelined
+// hd = 64, the dQ / dK,dV kernels above with their streamed operand tiles in
+// an NS-slot LDS-DMA ring (as attn_fwd_pipe_kernel): dK/dV streams Q, dO and
+// the tile's lse / delta (one 4-byte-per-lane DMA per wave: wave 0 lse, wave 1
+// delta, the others a scratch copy so every wave's DMA count is the same),
+// dQ streams K and V.
+template <int U, int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_pipe_kernel(AttnArgs a) {
+  constexpr int HD = 64;
+  using T = ATile<HD>;
+  using G = Glds<true, 64, 4>;
+  constexpr int KBW = 64 * U;
+  constexpr int SLOT = 2 * T::BYTES + 3 * 256;  // Q, dO images, lse, delta, scratch
+  constexpr int PT = 2 * G::P + 1;
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KBW;
+  int key[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) key[u] = k0 + 16 * (U * w + u) + cl;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  const float c = scl * LOG2E;
+
+  f32x4 dk[U][T::DT], dv[U][T::DT];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dk[u][i] = dv[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int qstart = causal ? (k0 / 64) * 64 : 0;
+  const int nqt = k0 < klim && qstart < a.Lq ? (a.Lq - qstart + 63) / 64 : 0;
+  short8_t kf[U][T::KS], vf[U][T::KS];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int krow = min(key[u], a.Lk - 1);
+    const bf16_t* kp = a.k + b * a.k_sb + (long long)krow * a.k_sl + h * a.k_sh;
+    const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) {
+      kf[u][s] = gfrag<HD>(kp, key[u] < a.Lk, s, lane);
+      vf[u][s] = gfrag<HD>(vp, key[u] < a.Lk, s, lane);
+    }
+  }
+  const bf16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
+  const float* vecs = (w == 1 ? a.delta : a.lse) + ((long long)b * a.H + h) * a.Lq;
+  const int voff = 2 * T::BYTES + 256 * min(w, 2);
+  G gs;
+  gs.init(w, lane);
+  auto issue = [&](int it) {
+    const int q0 = qstart + 64 * it;
+    char* slot = smem + (it % NS) * SLOT;
+    gs.issue(qb, (int)a.q_sl, a.Lq, HD, q0, 0, slot, w);
+    gs.issue(ob, (int)a.do_sl, a.Lq, HD, q0, 0, slot + T::BYTES, w);
+    __builtin_amdgcn_global_load_lds((const void*)(vecs + min(q0 + lane, a.Lq - 1)),
+                                     (__attribute__((address_space(3))) void*)(slot + voff), 4, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nqt) issue(s);
+
+  for (int it = 0; it < nqt; ++it) {
+    wait_tiles<PT, NS - 2>(min(NS - 2, nqt - 1 - it));
+    lds_barrier();
+    if (it + NS - 1 < nqt) issue(it + NS - 1);
+    const char* ldsQ = smem + (it % NS) * SLOT;
+    const char* ldsO = ldsQ + T::BYTES;
+    const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * T::BYTES);
+    const float* ldsD = ldsL + 64;
+    const int q0 = qstart + 64 * it;
+    // S[q][key] and dP[q][key]: rows q = q0 + 16t + 4g + r, col key (lane)
+    short8_t pf[U][2], dsf[U][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f32x4 p[U][2], ds[U][2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * s2 + tt;
+        f32x4 sv[U], dpv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
+          const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
+            dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
+          }
+        }
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 16 * t + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 16 * t + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = q0 + 16 * t + 4 * g + r;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
+            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
+            p[u][tt][r] = pv;
+            ds[u][tt][r] = pv * (dpv[u][r] - d4[r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pf[u][s2] = pack8(p[u][0][0], p[u][0][1], p[u][0][2], p[u][0][3], p[u][1][0], p[u][1][1],
+                          p[u][1][2], p[u][1][3]);
+        dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                           ds[u][1][1], ds[u][1][2], ds[u][1][3]);
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const short8_t dsf = pack8(ds[2 * s2][0], ds[2 * s2][1], ds[2 * s2][2], ds[2 * s2][3],
-                                 ds[2 * s2 + 1][0], ds[2 * s2 + 1][1], ds[2 * s2 + 1][2],
-                                 ds[2 * s2 + 1][3]);
 #pragma unroll
-      for (int dt = 0; dt < T::DT; ++dt) dq[dt] = mfma16(T::frag_tr(ldsK, s2, dt, lane), dsf, dq[dt]);
+      for (int dt = 0; dt < T::DT; ++dt) {
+        const short8_t ot = T::frag_tr(ldsO, s2, dt, lane);
+        const short8_t qt = T::frag_tr(ldsQ, s2, dt, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          dv[u][dt] = mfma16(ot, pf[u][s2], dv[u][dt]);
+          dk[u][dt] = mfma16(qt, dsf[u][s2], dk[u][dt]);
+        }
+      }
     }
-    __syncthreads();
   }
-  if (!qvalid) return;
-  bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow * a.dq_sl + h * a.dq_sh;
+  wait_vmcnt<0>();
 #pragma unroll
-  for (int dt = 0; dt < T::DT; ++dt) {
+  for (int u = 0; u < U; ++u) {
+    if (key[u] >= a.Lk) continue;
+    bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
+    bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
     const float sc = a.scale;
-    uint32_t lo = (uint32_t)f2bf(dq[dt][0] * sc) | ((uint32_t)f2bf(dq[dt][1] * sc) << 16);
-    uint32_t hi = (uint32_t)f2bf(dq[dt][2] * sc) | ((uint32_t)f2bf(dq[dt][3] * sc) << 16);
-    *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
+      uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+      lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
+      hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
+      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+  }
+}
+
+template <int U, int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_pipe_kernel(AttnArgs a) {
+  constexpr int HD = 64;
+  using T = ATile<HD>;
+  using G = Glds<true, 64, 4>;
+  constexpr int QBW = 64 * U;
+  constexpr int SLOT = 2 * T::BYTES;
+  constexpr int PT = 2 * G::P;
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int qrow[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q0 + QBW);
+  const float c = scl * LOG2E;
+  const int nkt = (klim + 63) / 64;
+  const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+  G gs;
+  gs.init(w, lane);
+  auto issue = [&](int kt) {
+    char* slot = smem + (kt % NS) * SLOT;
+    gs.issue(kb, (int)a.k_sl, a.Lk, HD, 64 * kt, 0, slot, w);
+    gs.issue(vb, (int)a.v_sl, a.Lk, HD, 64 * kt, 0, slot + T::BYTES, w);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkt) issue(s);
+
+  short8_t qf[U][T::KS], of[U][T::KS];
+  float L[U], D[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool qvalid = qrow[u] < a.Lq;
+    const int qr = min(qrow[u], a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.q_sb + (long long)qr * a.q_sl + h * a.q_sh;
+    const bf16_t* dop = a.dout + b * a.do_sb + (long long)qr * a.do_sl + h * a.do_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) {
+      qf[u][s] = gfrag<HD>(qp, qvalid, s, lane);
+      of[u][s] = gfrag<HD>(dop, qvalid, s, lane);
+    }
+    const long long bh = ((long long)b * a.H + h) * a.Lq + qr;
+    L[u] = a.lse[bh];
+    float d = 0.f;
+    const bf16_t* opr = a.o + b * a.o_sb + (long long)qr * a.o_sl + h * a.o_sh;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s) {
+      const short8_t ov = gfrag<HD>(opr, qvalid, s, lane);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[e]);
+    }
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    if (qvalid && g == 0) a.delta[bh] = d;  // for the dK/dV kernel, which runs after this one
+    D[u] = d;
+  }
+  f32x4 dq[U][T::DT];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dq[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_tiles<PT, NS - 2>(min(NS - 2, nkt - 1 - kt));
+    lds_barrier();
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+    const char* ldsK = smem + (kt % NS) * SLOT;
+    const char* ldsV = ldsK + T::BYTES;
+    const int k0 = 64 * kt;
+    short8_t dsf[U][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f32x4 ds[U][2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * s2 + tt;
+        f32x4 sv[U], dpv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          const short8_t kfr = T::frag_row(ldsK, 16 * t, ks, lane);
+          const short8_t vfr = T::frag_row(ldsV, 16 * t, ks, lane);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            sv[u] = mfma16(kfr, qf[u][ks], sv[u]);
+            dpv[u] = mfma16(vfr, of[u][ks], dpv[u]);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * t + 4 * g + r;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
+            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+            ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                           ds[u][1][1], ds[u][1][2], ds[u][1][3]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) {
+        const short8_t kt2 = T::frag_tr(ldsK, s2, dt, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(kt2, dsf[u][s2], dq[u][dt]);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (qrow[u] >= a.Lq) continue;
+    bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow[u] * a.dq_sl + h * a.dq_sh;
+    const float sc = a.scale;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
+      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
   }
 }
 
@@ -625,7 +1222,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
       for (int r = 0; r < 4; ++r) {
         const int q = 16 * t + 4 * g + r;
         const bool ok = live && kvalid && q < a.Lq && (!causal || key <= q);
-        pv[r] = ok ? exp2f(sv[r] * c - l4[r]) : 0.f;
+        pv[r] = ok ? fast_exp2(sv[r] * c - l4[r]) : 0.f;
         dv4[r] = pv[r] * (dpv[r] - d4[r]);
       }
       pk[t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
@@ -752,17 +1349,43 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 using namespace tdg;
 
 namespace {
+// experiment switch: subtiles per wave of the long-sequence kernels
+int attn_u() { return getenv("TDG_ATTN_U") ? atoi(getenv("TDG_ATTN_U")) : 2; }
+
 template <int HD>
 int fwd_hd(const AttnArgs& a, hipStream_t st) {
   // (64 queries per workgroup for Lq > 64 -- twice the workgroups, K / V
   // staged by both halves -- measured 17.2 vs 12.2 us at B 64, H 8, L 128:
   // csrc/lab/attn_lab.cpp, profiles/attn_lab/)
+  static const int var = getenv("TDG_ATTN_FWD") ? atoi(getenv("TDG_ATTN_FWD")) : 1;  // experiment
+  if constexpr (HD == 64) {
+    if (a.Lq > 128 && var > 0) {
+#define TDG_AFP(NWV, U, NS)                                                                     \
+  {                                                                                             \
+    static bool attr = false;                                                                   \
+    if (!attr) {                                                                                \
+      hipFuncSetAttribute((const void*)attn_fwd_pipe_kernel<NWV, U, NS>,                        \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
+      attr = true;                                                                              \
+    }                                                                                           \
+    hipLaunchKernelGGL((attn_fwd_pipe_kernel<NWV, U, NS>), dim3(cdiv(a.Lq, 16 * NWV * U), a.H, a.B), \
+                       dim3(NWV * 64), NS * 2 * ATile<64>::BYTES, st, a);                       \
+    return 0;                                                                                   \
+  }
+      if (var == 1) TDG_AFP(8, 1, 4)
+      if (var == 2) TDG_AFP(4, 2, 4)
+      if (var == 3) TDG_AFP(8, 2, 4)
+      if (var == 4) TDG_AFP(4, 1, 4)
+      if (var == 5) TDG_AFP(8, 1, 3)
+#undef TDG_AFP
+    }
+  }
   if (a.Lq > 64) {
     dim3 grid(cdiv(a.Lq, 128), a.H, a.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8, 128>), grid, dim3(512), 4 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8, 128, 1>), grid, dim3(512), 4 * ATile<HD>::BYTES, st, a);
   } else {
     dim3 grid(cdiv(a.Lq, 64), a.H, a.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 4, 64>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 4, 64, 1>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
   }
   return 0;
 }
@@ -786,10 +1409,45 @@ int bwd_hd(const AttnArgs& a, hipStream_t st) {
     return 0;
   }
   // dQ first: it also writes delta = rowsum(dO * O), which dK/dV reads
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, dim3(cdiv(a.Lq, QB), a.H, a.B), dim3(256),
-                     2 * ATile<HD>::BYTES, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
-                     2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
+  static const int bvar = getenv("TDG_ATTN_BWD") ? atoi(getenv("TDG_ATTN_BWD")) : 1;  // experiment
+  if constexpr (HD == 64) {
+    if (bvar > 0) {
+#define TDG_ABP(K, U, NS, GRID)                                                                \
+  {                                                                                            \
+    constexpr int lds = NS * (K == 0 ? 2 * ATile<64>::BYTES : 2 * ATile<64>::BYTES + 768);    \
+    static bool attr = false;                                                                  \
+    if (!attr) {                                                                               \
+      hipFuncSetAttribute(K == 0 ? (const void*)attn_bwd_dq_pipe_kernel<U, NS>                 \
+                                 : (const void*)attn_bwd_dkdv_pipe_kernel<U, NS>,              \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
+      attr = true;                                                                             \
+    }                                                                                          \
+    if (K == 0)                                                                                \
+      hipLaunchKernelGGL((attn_bwd_dq_pipe_kernel<U, NS>), GRID, dim3(256), lds, st, a);       \
+    else                                                                                       \
+      hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<U, NS>), GRID, dim3(256), lds, st, a);     \
+  }
+      const int uq = bvar == 2 ? 1 : 2, uk = bvar == 3 ? 1 : 2;
+      if (uq == 2) TDG_ABP(0, 2, 4, dim3(cdiv(a.Lq, 128), a.H, a.B))
+      else TDG_ABP(0, 1, 4, dim3(cdiv(a.Lq, 64), a.H, a.B))
+      if (uk == 2) TDG_ABP(1, 2, 4, dim3(cdiv(a.Lk, 128), a.H, a.B))
+      else TDG_ABP(1, 1, 4, dim3(cdiv(a.Lk, 64), a.H, a.B))
+#undef TDG_ABP
+      return 0;
+    }
+  }
+  static const int U = attn_u();
+  if (U == 2) {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 2>), dim3(cdiv(a.Lq, 128), a.H, a.B), dim3(256),
+                       2 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), dim3(cdiv(a.Lk, 128), a.H, a.B), dim3(256),
+                       2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), dim3(cdiv(a.Lq, QB), a.H, a.B), dim3(256),
+                       2 * ATile<HD>::BYTES, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
+                       2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
+  }
   return 0;
 }
 template <int HD>

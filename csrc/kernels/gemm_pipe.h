@@ -115,17 +115,6 @@ __device__ __forceinline__ short8_t pfrag(const char* lds, int base, int lane) {
   }
 }
 
-// vmcnt wait leaving `n` younger tiles (PT LDS-DMA each) in flight
-template <int PT, int NMAX>
-__device__ __forceinline__ void wait_tiles(int n) {
-  static_assert(NMAX <= 4 && PT * NMAX <= 63, "vmcnt range");
-  if (NMAX >= 4 && n >= 4) { wait_vmcnt<(NMAX >= 4 ? 4 * PT : 0)>(); return; }
-  if (NMAX >= 3 && n >= 3) { wait_vmcnt<(NMAX >= 3 ? 3 * PT : 0)>(); return; }
-  if (NMAX >= 2 && n >= 2) { wait_vmcnt<(NMAX >= 2 ? 2 * PT : 0)>(); return; }
-  if (NMAX >= 1 && n >= 1) { wait_vmcnt<PT>(); return; }
-  wait_vmcnt<0>();
-}
-
 // The K loop's pieces as static members of one class template (the pattern
 // of EpiLds): clang's host pass failed substitution of free function templates
 // taking the kernel's local operand-stage types for every kernel instantiation

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Attention fwd / bwd timing on the Transformer-base shape (B=64, H=8,
-L=128, hd=64), HIP-graph replay of 20 calls (set TDG_ATTN_BWD_SPLIT=1 for
-the three-kernel backward)."""
+"""Attention fwd / bwd timing, HIP-graph replay of 20 calls. Default shape:
+Transformer-base (B=64, H=8, L=128, hd=64); ATTN_B / ATTN_H / ATTN_L set
+another (the big seq-512 config: ATTN_B=16 ATTN_H=16 ATTN_L=512). Prints
+us per call and PF/s (causal counts the unmasked half)."""
 import os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -23,7 +24,9 @@ def graph_time(fn, n=20):
     return a.elapsed_time(b) / n * 1e3
 
 B = int(os.environ.get("ATTN_B", "64"))
-H, L, hd = 8, 128, 64
+H = int(os.environ.get("ATTN_H", "8"))
+L = int(os.environ.get("ATTN_L", "128"))
+hd = 64
 for causal in (False, True):
     q, k, v, do = (torch.randn(B, L, H, hd, device="cuda").bfloat16() for _ in range(4))
     kv = torch.full((B,), L, dtype=torch.int32, device="cuda")
@@ -31,4 +34,7 @@ for causal in (False, True):
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     tf = graph_time(lambda: kk.attn_fwd(q, k, v, kv, 0.125, causal))
     tb = graph_time(lambda: kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, causal))
-    print(f"B={B} causal={causal} split={os.environ.get('TDG_ATTN_BWD_SPLIT', '0')}: fwd {tf:.2f} us  bwd {tb:.2f} us", flush=True)
+    fl = 4.0 * B * H * L * L * hd * (0.5 if causal else 1.0)
+    print(f"B={B} H={H} L={L} causal={causal} U={os.environ.get('TDG_ATTN_U', 'default')}: "
+          f"fwd {tf:.2f} us ({fl / tf / 1e9:.3f} PF/s)  bwd {tb:.2f} us ({2.5 * fl / tb / 1e9:.3f} PF/s)",
+          flush=True)
