@@ -25,7 +25,6 @@
 #include "tdg_attn.h"
 #include "tdg_gemm.h"
 
-#include <cstdlib>
 
 namespace tdg {
 
@@ -868,9 +867,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     __builtin_amdgcn_global_load_lds((const void*)(vecs + min(q0 + lane, a.Lq - 1)),
                                      (__attribute__((address_space(3))) void*)(slot + voff), 4, 0, 0);
   };
+  // prologue tiles issued unconditionally (clamped rows, never read) so the
+  // DMA count behind the K / V fragment loads is a constant
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nqt) issue(s);
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  wait_vmcnt_known<(NS - 1) * PT>();
 
   for (int it = 0; it < nqt; ++it) {
     wait_tiles<PT, NS - 2>(min(NS - 2, nqt - 1 - it));
@@ -881,38 +882,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * T::BYTES);
     const float* ldsD = ldsL + 64;
     const int q0 = qstart + 64 * it;
-    // S[q][key] and dP[q][key]: rows q = q0 + 16t + 4g + r, col key (lane)
+    // untracked LDS reads with counted waits (a tracked read would get a
+    // vmcnt(0) for the DMA in flight); the next 16-query tile's Q / dO
+    // fragments and lse / delta are requested before this one is used
     short8_t pf[U][2], dsf[U][2];
+    short8_t qfr[2][T::KS], ofr[2][T::KS];
+    f32x4 l4[2], d4[2];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      qfr[0][ks] = T::frag_row_async(ldsQ, 0, ks, lane);
+      ofr[0][ks] = T::frag_row_async(ldsO, 0, ks, lane);
+    }
+    l4[0] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsL + 4 * g));
+    d4[0] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsD + 4 * g));
+    constexpr int RPT = 2 * T::KS + 2;  // LDS reads per 16-query tile
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       f32x4 p[U][2], ds[U][2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * s2 + tt;
+        const int t = 2 * s2 + tt, cb = t & 1, nb = cb ^ 1;
+        if (t < 3) {
+#pragma unroll
+          for (int ks = 0; ks < T::KS; ++ks) {
+            qfr[nb][ks] = T::frag_row_async(ldsQ, 16 * (t + 1), ks, lane);
+            ofr[nb][ks] = T::frag_row_async(ldsO, 16 * (t + 1), ks, lane);
+          }
+          l4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsL + 16 * (t + 1) + 4 * g));
+          d4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsD + 16 * (t + 1) + 4 * g));
+          lgkm_wait<RPT>();
+        } else {
+          lgkm_wait<0>();
+        }
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          tie(qfr[cb][ks]);
+          tie(ofr[cb][ks]);
+        }
+        tie(l4[cb]);
+        tie(d4[cb]);
         f32x4 sv[U], dpv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
-          const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
-          const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
-            dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
+            sv[u] = mfma16(qfr[cb][ks], kf[u][ks], sv[u]);
+            dpv[u] = mfma16(ofr[cb][ks], vf[u][ks], dpv[u]);
           }
         }
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 16 * t + 4 * g);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 16 * t + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = q0 + 16 * t + 4 * g + r;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
+            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
             p[u][tt][r] = pv;
-            ds[u][tt][r] = pv * (dpv[u][r] - d4[r]);
+            ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
           }
         }
       }
@@ -924,17 +952,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
                            ds[u][1][1], ds[u][1][2], ds[u][1][3]);
       }
     }
+    // dV^T += dO^T P, dK^T += Q^T dS: transposed fragments, next requested
+    // before this one is used
+    short4_t olo[2], ohi[2], qlo[2], qhi[2];
+    T::frag_tr_async(ldsO, 0, 0, lane, olo[0], ohi[0]);
+    T::frag_tr_async(ldsQ, 0, 0, lane, qlo[0], qhi[0]);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int i = 0; i < 2 * T::DT; ++i) {
+      const int s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
+      if (i + 1 < 2 * T::DT) {
+        const int s2n = (i + 1) / T::DT, dtn = (i + 1) % T::DT;
+        T::frag_tr_async(ldsO, s2n, dtn, lane, olo[nb], ohi[nb]);
+        T::frag_tr_async(ldsQ, s2n, dtn, lane, qlo[nb], qhi[nb]);
+        lgkm_wait<4>();
+      } else {
+        lgkm_wait<0>();
+      }
+      tie(olo[cb]);
+      tie(ohi[cb]);
+      tie(qlo[cb]);
+      tie(qhi[cb]);
+      const short8_t ot = cat4(olo[cb], ohi[cb]);
+      const short8_t qt = cat4(qlo[cb], qhi[cb]);
 #pragma unroll
-      for (int dt = 0; dt < T::DT; ++dt) {
-        const short8_t ot = T::frag_tr(ldsO, s2, dt, lane);
-        const short8_t qt = T::frag_tr(ldsQ, s2, dt, lane);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          dv[u][dt] = mfma16(ot, pf[u][s2], dv[u][dt]);
-          dk[u][dt] = mfma16(qt, dsf[u][s2], dk[u][dt]);
-        }
+      for (int u = 0; u < U; ++u) {
+        dv[u][dt] = mfma16(ot, pf[u][s2], dv[u][dt]);
+        dk[u][dt] = mfma16(qt, dsf[u][s2], dk[u][dt]);
       }
     }
   }
@@ -982,19 +1025,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int nkt = (klim + 63) / 64;
   const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
-  G gs;
-  gs.init(w, lane);
-  auto issue = [&](int kt) {
-    char* slot = smem + (kt % NS) * SLOT;
-    gs.issue(kb, (int)a.k_sl, a.Lk, HD, 64 * kt, 0, slot, w);
-    gs.issue(vb, (int)a.v_sl, a.Lk, HD, 64 * kt, 0, slot + T::BYTES, w);
-  };
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nkt) issue(s);
-
   short8_t qf[U][T::KS], of[U][T::KS];
   float L[U], D[U];
+  short8_t ov[U][T::KS];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const bool qvalid = qrow[u] < a.Lq;
@@ -1008,17 +1041,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
     const long long bh = ((long long)b * a.H + h) * a.Lq + qr;
     L[u] = a.lse[bh];
-    float d = 0.f;
     const bf16_t* opr = a.o + b * a.o_sb + (long long)qr * a.o_sl + h * a.o_sh;
 #pragma unroll
-    for (int s = 0; s < T::KS; ++s) {
-      const short8_t ov = gfrag<HD>(opr, qvalid, s, lane);
+    for (int s = 0; s < T::KS; ++s) ov[u][s] = gfrag<HD>(opr, qvalid, s, lane);
+  }
+  G gs;
+  gs.init(w, lane);
+  auto issue = [&](int kt) {
+    char* slot = smem + (kt % NS) * SLOT;
+    gs.issue(kb, (int)a.k_sl, a.Lk, HD, 64 * kt, 0, slot, w);
+    gs.issue(vb, (int)a.v_sl, a.Lk, HD, 64 * kt, 0, slot + T::BYTES, w);
+  };
+  // prologue tiles issued unconditionally (clamped rows, never read) so the
+  // DMA count behind the Q / dO / O / lse loads is a constant
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[e]);
-    }
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  wait_vmcnt_known<(NS - 1) * PT>();
+  // delta = rowsum(dO * O) of the lane's query row (the 4 lane groups hold
+  // disjoint head-dim slices), written for the dK/dV kernel, which runs after
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float d = 0.f;
+#pragma unroll
+    for (int s = 0; s < T::KS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[u][s][e]);
     d += __shfl_xor(d, 16, 64);
     d += __shfl_xor(d, 32, 64);
-    if (qvalid && g == 0) a.delta[bh] = d;  // for the dK/dV kernel, which runs after this one
+    if (qrow[u] < a.Lq && g == 0) a.delta[((long long)b * a.H + h) * a.Lq + qrow[u]] = d;
     D[u] = d;
   }
   f32x4 dq[U][T::DT];
@@ -1034,24 +1084,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     const char* ldsK = smem + (kt % NS) * SLOT;
     const char* ldsV = ldsK + T::BYTES;
     const int k0 = 64 * kt;
+    // untracked LDS reads with counted waits, next 16-key tile requested
+    // before this one is used
     short8_t dsf[U][2];
+    short8_t kfr[2][T::KS], vfr[2][T::KS];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      kfr[0][ks] = T::frag_row_async(ldsK, 0, ks, lane);
+      vfr[0][ks] = T::frag_row_async(ldsV, 0, ks, lane);
+    }
+    constexpr int RPT = 2 * T::KS;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       f32x4 ds[U][2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * s2 + tt;
+        const int t = 2 * s2 + tt, cb = t & 1, nb = cb ^ 1;
+        if (t < 3) {
+#pragma unroll
+          for (int ks = 0; ks < T::KS; ++ks) {
+            kfr[nb][ks] = T::frag_row_async(ldsK, 16 * (t + 1), ks, lane);
+            vfr[nb][ks] = T::frag_row_async(ldsV, 16 * (t + 1), ks, lane);
+          }
+          lgkm_wait<RPT>();
+        } else {
+          lgkm_wait<0>();
+        }
+#pragma unroll
+        for (int ks = 0; ks < T::KS; ++ks) {
+          tie(kfr[cb][ks]);
+          tie(vfr[cb][ks]);
+        }
         f32x4 sv[U], dpv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
-          const short8_t kfr = T::frag_row(ldsK, 16 * t, ks, lane);
-          const short8_t vfr = T::frag_row(ldsV, 16 * t, ks, lane);
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            sv[u] = mfma16(kfr, qf[u][ks], sv[u]);
-            dpv[u] = mfma16(vfr, of[u][ks], dpv[u]);
+            sv[u] = mfma16(kfr[cb][ks], qf[u][ks], sv[u]);
+            dpv[u] = mfma16(vfr[cb][ks], of[u][ks], dpv[u]);
           }
         }
 #pragma unroll
@@ -1070,14 +1142,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
                            ds[u][1][1], ds[u][1][2], ds[u][1][3]);
     }
+    short4_t klo[2], khi[2];
+    T::frag_tr_async(ldsK, 0, 0, lane, klo[0], khi[0]);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-      for (int dt = 0; dt < T::DT; ++dt) {
-        const short8_t kt2 = T::frag_tr(ldsK, s2, dt, lane);
-#pragma unroll
-        for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(kt2, dsf[u][s2], dq[u][dt]);
+    for (int i = 0; i < 2 * T::DT; ++i) {
+      const int s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
+      if (i + 1 < 2 * T::DT) {
+        T::frag_tr_async(ldsK, (i + 1) / T::DT, (i + 1) % T::DT, lane, klo[nb], khi[nb]);
+        lgkm_wait<2>();
+      } else {
+        lgkm_wait<0>();
       }
+      tie(klo[cb]);
+      tie(khi[cb]);
+      const short8_t kt2 = cat4(klo[cb], khi[cb]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(kt2, dsf[u][s2], dq[u][dt]);
     }
   }
   wait_vmcnt<0>();
@@ -1349,35 +1429,26 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 using namespace tdg;
 
 namespace {
-// experiment switch: subtiles per wave of the long-sequence kernels
-int attn_u() { return getenv("TDG_ATTN_U") ? atoi(getenv("TDG_ATTN_U")) : 2; }
-
 template <int HD>
 int fwd_hd(const AttnArgs& a, hipStream_t st) {
   // (64 queries per workgroup for Lq > 64 -- twice the workgroups, K / V
   // staged by both halves -- measured 17.2 vs 12.2 us at B 64, H 8, L 128:
   // csrc/lab/attn_lab.cpp, profiles/attn_lab/)
-  static const int var = getenv("TDG_ATTN_FWD") ? atoi(getenv("TDG_ATTN_FWD")) : 1;  // experiment
+  // hd 64, > 128 queries: LDS-DMA pipelined kernel, 8 waves x 16 queries,
+  // 3-slot ring (seq 512: 40.5 us vs 41-45 for 4 slots or 32 queries per
+  // wave, 47 for the register-staged kernel; profiles/r3/attn_seq512_*)
   if constexpr (HD == 64) {
-    if (a.Lq > 128 && var > 0) {
-#define TDG_AFP(NWV, U, NS)                                                                     \
-  {                                                                                             \
-    static bool attr = false;                                                                   \
-    if (!attr) {                                                                                \
-      hipFuncSetAttribute((const void*)attn_fwd_pipe_kernel<NWV, U, NS>,                        \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
-      attr = true;                                                                              \
-    }                                                                                           \
-    hipLaunchKernelGGL((attn_fwd_pipe_kernel<NWV, U, NS>), dim3(cdiv(a.Lq, 16 * NWV * U), a.H, a.B), \
-                       dim3(NWV * 64), NS * 2 * ATile<64>::BYTES, st, a);                       \
-    return 0;                                                                                   \
-  }
-      if (var == 1) TDG_AFP(8, 1, 4)
-      if (var == 2) TDG_AFP(4, 2, 4)
-      if (var == 3) TDG_AFP(8, 2, 4)
-      if (var == 4) TDG_AFP(4, 1, 4)
-      if (var == 5) TDG_AFP(8, 1, 3)
-#undef TDG_AFP
+    if (a.Lq > 128) {
+      constexpr int NWV = 8, U = 1, NS = 3;
+      static bool attr = false;
+      if (!attr) {
+        hipFuncSetAttribute((const void*)attn_fwd_pipe_kernel<NWV, U, NS>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      hipLaunchKernelGGL((attn_fwd_pipe_kernel<NWV, U, NS>), dim3(cdiv(a.Lq, 16 * NWV * U), a.H, a.B),
+                         dim3(NWV * 64), NS * 2 * ATile<64>::BYTES, st, a);
+      return 0;
     }
   }
   if (a.Lq > 64) {
@@ -1409,45 +1480,30 @@ int bwd_hd(const AttnArgs& a, hipStream_t st) {
     return 0;
   }
   // dQ first: it also writes delta = rowsum(dO * O), which dK/dV reads
-  static const int bvar = getenv("TDG_ATTN_BWD") ? atoi(getenv("TDG_ATTN_BWD")) : 1;  // experiment
+  // hd 64: LDS-DMA pipelined kernels, 32 queries / keys per wave (seq 512:
+  // 121 us vs 132-136 with 16 per wave in either, 147 register-staged)
   if constexpr (HD == 64) {
-    if (bvar > 0) {
-#define TDG_ABP(K, U, NS, GRID)                                                                \
-  {                                                                                            \
-    constexpr int lds = NS * (K == 0 ? 2 * ATile<64>::BYTES : 2 * ATile<64>::BYTES + 768);    \
-    static bool attr = false;                                                                  \
-    if (!attr) {                                                                               \
-      hipFuncSetAttribute(K == 0 ? (const void*)attn_bwd_dq_pipe_kernel<U, NS>                 \
-                                 : (const void*)attn_bwd_dkdv_pipe_kernel<U, NS>,              \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
-      attr = true;                                                                             \
-    }                                                                                          \
-    if (K == 0)                                                                                \
-      hipLaunchKernelGGL((attn_bwd_dq_pipe_kernel<U, NS>), GRID, dim3(256), lds, st, a);       \
-    else                                                                                       \
-      hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<U, NS>), GRID, dim3(256), lds, st, a);     \
-  }
-      const int uq = bvar == 2 ? 1 : 2, uk = bvar == 3 ? 1 : 2;
-      if (uq == 2) TDG_ABP(0, 2, 4, dim3(cdiv(a.Lq, 128), a.H, a.B))
-      else TDG_ABP(0, 1, 4, dim3(cdiv(a.Lq, 64), a.H, a.B))
-      if (uk == 2) TDG_ABP(1, 2, 4, dim3(cdiv(a.Lk, 128), a.H, a.B))
-      else TDG_ABP(1, 1, 4, dim3(cdiv(a.Lk, 64), a.H, a.B))
-#undef TDG_ABP
-      return 0;
+    constexpr int U = 2, NS = 4;
+    constexpr int lds_dq = NS * 2 * ATile<64>::BYTES;
+    constexpr int lds_kv = NS * (2 * ATile<64>::BYTES + 768);
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)attn_bwd_dq_pipe_kernel<U, NS>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)attn_bwd_dkdv_pipe_kernel<U, NS>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
     }
+    hipLaunchKernelGGL((attn_bwd_dq_pipe_kernel<U, NS>), dim3(cdiv(a.Lq, 64 * U), a.H, a.B),
+                       dim3(256), lds_dq, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<U, NS>), dim3(cdiv(a.Lk, 64 * U), a.H, a.B),
+                       dim3(256), lds_kv, st, a);
+    return 0;
   }
-  static const int U = attn_u();
-  if (U == 2) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 2>), dim3(cdiv(a.Lq, 128), a.H, a.B), dim3(256),
-                       2 * ATile<HD>::BYTES, st, a);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), dim3(cdiv(a.Lk, 128), a.H, a.B), dim3(256),
-                       2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), dim3(cdiv(a.Lq, QB), a.H, a.B), dim3(256),
-                       2 * ATile<HD>::BYTES, st, a);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
-                       2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
-  }
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), dim3(cdiv(a.Lq, QB), a.H, a.B), dim3(256),
+                     2 * ATile<HD>::BYTES, st, a);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), dim3(cdiv(a.Lk, KB), a.H, a.B), dim3(256),
+                     2 * ATile<HD>::BYTES + 2 * QB * 4, st, a);
   return 0;
 }
 template <int HD>
