@@ -23,6 +23,7 @@ void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld, in
 int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
+int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
@@ -239,6 +240,59 @@ void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   a.causal = causal;
   c10::DeviceGuard g(q.device());
   check_err(tdg_attn_fwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_fwd");
+}
+
+// e4m3 forward: q8/k8/v8 are [B, L, H, 64] float8_e4m3fn views (hd
+// contiguous; K / V rows 16-byte aligned for the LDS-DMA staging), with
+// per-tensor scales (x8 = e4m3(x * s), one-element f32 device tensors)
+void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Tensor& out,
+                  const Tensor& lse, const optional<Tensor>& kv_len, const Tensor& sq,
+                  const Tensor& sk, const Tensor& sv, double scale, bool causal) {
+  for (auto* t : {&q8, &k8, &v8}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat8_e4m3fn, "attn_fwd_fp8: e4m3 q/k/v");
+    TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1 && t->size(3) == 64,
+                "attn_fwd_fp8: [B,L,H,64] with hd contiguous");
+  }
+  for (auto* t : {&k8, &v8})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) == 0 && t->stride(0) % 16 == 0 &&
+                    t->stride(1) % 16 == 0 && t->stride(2) % 16 == 0,
+                "attn_fwd_fp8: K / V rows must be 16-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(q8.data_ptr()) % 8) == 0 && q8.stride(0) % 8 == 0 &&
+                  q8.stride(1) % 8 == 0 && q8.stride(2) % 8 == 0,
+              "attn_fwd_fp8: Q rows must be 8-byte aligned");
+  tdg::AttnArgs a{};
+  a.B = (int)q8.size(0);
+  a.Lq = (int)q8.size(1);
+  a.H = (int)q8.size(2);
+  a.Lk = (int)k8.size(1);
+  TORCH_CHECK(k8.size(0) == a.B && v8.size(0) == a.B && k8.size(2) == a.H && v8.size(2) == a.H &&
+                  v8.size(1) == a.Lk,
+              "attn_fwd_fp8: q/k/v shape mismatch");
+  a.q = (const uint16_t*)q8.data_ptr();
+  a.k = (const uint16_t*)k8.data_ptr();
+  a.v = (const uint16_t*)v8.data_ptr();
+  a.q_sb = q8.stride(0); a.q_sl = q8.stride(1); a.q_sh = (int)q8.stride(2);
+  a.k_sb = k8.stride(0); a.k_sl = k8.stride(1); a.k_sh = (int)k8.stride(2);
+  a.v_sb = v8.stride(0); a.v_sl = v8.stride(1); a.v_sh = (int)v8.stride(2);
+  check_like(out, a, a.Lq, "out");
+  check_f32(lse, "lse");
+  check_contig(lse, "lse");
+  TORCH_CHECK(lse.numel() == (int64_t)a.B * a.H * a.Lq, "lse must be [B,H,Lq]");
+  for (auto* t : {&sq, &sk, &sv}) check_f32(*t, "fp8 scale");
+  a.out = (uint16_t*)out.data_ptr();
+  a.o_sb = out.stride(0); a.o_sl = out.stride(1); a.o_sh = (int)out.stride(2);
+  a.lse = lse.data_ptr<float>();
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.sq8 = sq.data_ptr<float>();
+  a.sk8 = sk.data_ptr<float>();
+  a.sv8 = sv.data_ptr<float>();
+  a.scale = (float)scale;
+  a.causal = causal;
+  c10::DeviceGuard g(q8.device());
+  check_err(tdg_attn_fwd_fp8(&a, 64, stream_of(q8)), "tdg attn_fwd_fp8");
 }
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
@@ -844,6 +898,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_dequant", &fp8_dequant);
   m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd_fp8", &attn_fwd_fp8);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_probs", &attn_probs);
   m.def("ln_fwd", &ln_fwd);

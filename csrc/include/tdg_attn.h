@@ -22,5 +22,10 @@ struct AttnArgs {
   int B, H, Lq, Lk;
   float scale;  // softmax scale (1/sqrt(dk))
   int causal;
+  // e4m3 forward (attn_fwd_fp8): q / k / v point at e4m3 copies x8 =
+  // e4m3(x * s) (strides in elements = bytes), with these per-tensor scales
+  const float* sq8;
+  const float* sk8;
+  const float* sv8;
 };
 }  // namespace tdg

@@ -179,6 +179,23 @@ __device__ __forceinline__ short8_t lds_read_b128_async(const void* p) {
   return r;
 }
 
+// 8-byte LDS reads, likewise untracked: plain and transposing-bytes (gfx950
+// ds_read_b64_tr_b8: lanes 2r, 2r+1 of a 16-lane group pass the two 8-byte
+// halves of row r of an 8-row x 16-byte block; lane i receives column i, one
+// byte per row -- verified on the box, scripts/probes/fp8_attn_layout.hip)
+__device__ __forceinline__ long lds_read_b64_async(const void* p) {
+  long r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+__device__ __forceinline__ long lds_read_tr8_async(const void* p) {
+  long r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
 template <int N>
 __device__ __forceinline__ void lgkm_wait() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15) : "memory");

@@ -191,7 +191,9 @@ __device__ __forceinline__ bool tile_masked(int k0, int kt, int klim, bool causa
 // c*S -- so that c = 0, the zero logit scale of a kv_len = 0 row, never meets
 // an infinity in a product; unmasked tiles keep raw logits and fold c into
 // the exp's FMA)
-template <int NT16, int DT>
+// (KPERM: the e4m3 kernel's key order, accumulator (t, g, r) = key
+// 32 (t >> 1) + 8 g + 4 (t & 1) + r -- see attn_fwd_fp8_kernel)
+template <int NT16, int DT, bool KPERM = false>
 __device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l, f32x4 (&oacc)[DT],
                                             bool masked, int k0, int klim, bool causal, int qrow,
                                             int g, float c) {
@@ -200,7 +202,7 @@ __device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l
     for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * t + 4 * g + r;
+        const int key = KPERM ? k0 + 32 * (t >> 1) + 8 * g + 4 * (t & 1) + r : k0 + 16 * t + 4 * g + r;
         s[t][r] = key < klim && (!causal || key <= qrow) ? s[t][r] * c : -INFINITY;
       }
   }
@@ -520,6 +522,171 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
     if (g == 0)
       a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + log2f(lu) : INFINITY;
   }
+}
+
+// ============================================================================ forward, e4m3
+// BASELINE config 5's fp8 attention: Q, K, V are the e4m3 copies the fp8
+// input projections emit (per-tensor scales sq, sk, sv), S^T = K Q^T and
+// O^T = V^T P^T on v_mfma_f32_16x16x32_fp8_fp8, P quantised as e4m3(P * 448)
+// (P <= 1 against the running max), softmax in f32. hd = 64, > 128 queries;
+// the structure of attn_fwd_pipe_kernel: 8 waves x 16 queries, K / V tiles of
+// 64 keys (64-byte rows, 4 KiB each) in an NS-slot LDS-DMA ring, waves 0-3
+// staging K and 4-7 V (one 1 KiB piece per wave per tile), untracked counted
+// LDS reads. Images: 8-byte chunk c of row r stored at c ^ 2 ((r >> 2) & 3)
+// (the K row reads and the V transposing reads both conflict-free). The PV
+// product needs each lane group's 8 keys consecutive (ds_read_b64_tr_b8 gives
+// 8 consecutive V rows): the K image is filled in a permuted key order so
+// that the S accumulator (t, g, r) is key 32 (t >> 1) + 8 g + 4 (t & 1) + r,
+// which makes the P registers the PV B operand as they stand. The backward
+// stays bf16 (it recomputes P from the bf16 Q, K and this LSE).
+template <int NS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_fp8_kernel(AttnArgs a) {
+  constexpr int NWV = 8, HD = 64, RB = 64, TB = 64 * RB, SLOT = 2 * TB, QBW = 16 * NWV;
+  constexpr int NT16 = 4, DT = 4;
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint8_t* q8 = reinterpret_cast<const uint8_t*>(a.q);
+  const uint8_t* k8 = reinterpret_cast<const uint8_t*>(a.k);
+  const uint8_t* v8 = reinterpret_cast<const uint8_t*>(a.v);
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  const int qrow = q0 + 16 * w + cl;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, q0 + QBW);
+  const int nkt = (klim + 63) / 64;
+
+  // Q fragments (B operand of S^T): lane (g, q) holds Q[q][32 ks + 8 g .. +7]
+  long qf[2];
+  {
+    const uint8_t* qp = q8 + b * a.q_sb + (long long)min(qrow, a.Lq - 1) * a.q_sl + h * a.q_sh;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qf[ks] = qrow < a.Lq ? *reinterpret_cast<const long*>(qp + 32 * ks + 8 * g) : 0;
+  }
+  // staging: wave w < 4 fills K image rows 16w.., w >= 4 V image rows 16(w-4)..
+  const bool isv = w >= 4;
+  const int rho = 16 * (w & 3) + (lane >> 2);
+  // K image row rho = 16 t + 4 g + r holds key 32 t1 + 8 g + 4 t0 + r
+  const int kin = isv ? rho : ((rho & 0x23) | ((rho & 0x0C) << 1) | ((rho & 0x10) >> 2));
+  const int chunk = (lane & 3) ^ ((rho >> 2) & 3);  // 16-byte source chunk of the swizzled row
+  const uint8_t* src0 = (isv ? v8 + b * a.v_sb + h * a.v_sh : k8 + b * a.k_sb + h * a.k_sh) + 16 * chunk;
+  const long long sl = isv ? a.v_sl : a.k_sl;
+  char* dst0 = smem + (isv ? TB : 0) + (w & 3) * 1024;
+  auto issue = [&](int kt) {
+    const int key = min(64 * kt + kin, a.Lk - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(src0 + key * sl),
+                                     (__attribute__((address_space(3))) void*)(dst0 + (kt % NS) * SLOT),
+                                     16, 0, 0);
+  };
+  // prologue tiles issued unconditionally (clamped rows, never read) so the
+  // DMA count behind the Q loads is a constant
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  wait_vmcnt_known<NS - 1>();
+
+  const float inv_qk = 1.f / (a.sq8[0] * a.sk8[0]);
+  const float c = scl * LOG2E * inv_qk;
+  const int wq0 = q0 + 16 * w;
+  f32x4 oacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_tiles<1, NS - 2>(min(NS - 2, nkt - 1 - kt));
+    lds_barrier();
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+    const char* ldsK = smem + (kt % NS) * SLOT;
+    const char* ldsV = ldsK + TB;
+    const int k0 = 64 * kt;
+    // S^T: K rows 16 t + cl, hd bytes 32 ks + 8 g (8-byte chunk 4 ks + g)
+    long kfr[NT16][2];
+#pragma unroll
+    for (int t = 0; t < NT16; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row = 16 * t + cl;
+        const int ch = (4 * ks + g) ^ (((row >> 2) & 3) << 1);
+        kfr[t][ks] = lds_read_b64_async(ldsK + row * RB + 8 * ch);
+      }
+    f32x4 s[NT16];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half == 0) lgkm_wait<NT16>();
+      else lgkm_wait<0>();
+#pragma unroll
+      for (int t = half * 2; t < half * 2 + 2; ++t) {
+        tie(kfr[t][0]);
+        tie(kfr[t][1]);
+        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(kfr[t][ks], qf[ks], s[t], 0, 0, 0);
+      }
+    }
+    const bool msk = tile_masked(k0, 64, klim, causal, wq0);
+    softmax_max<NT16, DT, true>(s, m, l, oacc, msk, k0, klim, causal, qrow, g, c);
+    // V^T fragments: lane pair (2 r8 + hh) of group g passes V row 32 s2 + 8 g + r8,
+    // 8-byte chunk 2 dt + hh; lane i receives hd column 16 dt + i, keys 8 g .. +7
+    long vfr[2][DT];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int row = 32 * s2 + 8 * g + (cl >> 1);
+        const int ch = (2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1);
+        vfr[s2][dt] = lds_read_tr8_async(ldsV + row * RB + 8 * ch);
+      }
+    // P = exp2(c S - m) (f32 row sum), then e4m3(P * 448) in PV operand order
+    const float cs = msk ? 1.f : c;
+    const float nm = m == -INFINITY ? 0.f : -m;
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT16; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = fast_exp2(fmaf(s[t][r], cs, nm));
+        s[t][r] = p * 448.f;
+        rs += p;
+      }
+    l += rs;
+    long pf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      int lo = pack2_e4m3<false>(s[2 * s2][0], s[2 * s2][1], 0);
+      lo = pack2_e4m3<true>(s[2 * s2][2], s[2 * s2][3], lo);
+      int hi = pack2_e4m3<false>(s[2 * s2 + 1][0], s[2 * s2 + 1][1], 0);
+      hi = pack2_e4m3<true>(s[2 * s2 + 1][2], s[2 * s2 + 1][3], hi);
+      pf[s2] = (long)(uint32_t)lo | ((long)hi << 32);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 0) lgkm_wait<DT>();
+      else lgkm_wait<0>();
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        tie(vfr[s2][dt]);
+        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(vfr[s2][dt], pf[s2], oacc[dt], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  float lu = l;
+  lu += __shfl_xor(lu, 16, 64);
+  lu += __shfl_xor(lu, 32, 64);
+  if (qrow >= a.Lq) return;
+  const float inv = lu > 0.f ? 1.f / (lu * 448.f * a.sv8[0]) : 0.f;
+  bf16_t* op = a.out + b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const uint32_t lo = (uint32_t)f2bf(oacc[dt][0] * inv) | ((uint32_t)f2bf(oacc[dt][1] * inv) << 16);
+    const uint32_t hi = (uint32_t)f2bf(oacc[dt][2] * inv) | ((uint32_t)f2bf(oacc[dt][3] * inv) << 16);
+    *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+  }
+  if (g == 0) a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + log2f(lu) : INFINITY;
 }
 
 // ============================================================================ dK, dV
@@ -1529,6 +1696,19 @@ extern "C" int tdg_attn_fwd(const AttnArgs* a, int hd, hipStream_t st) {
 }
 extern "C" int tdg_attn_bwd(const AttnArgs* a, int hd, hipStream_t st) {
   TDG_HD_CASES(bwd_hd, *a, st)
+}
+extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, hipStream_t st) {
+  if (hd != 64) return -1;
+  constexpr int NS = 3;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_fwd_fp8_kernel<NS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_fwd_fp8_kernel<NS>, dim3(cdiv(a->Lq, 128), a->H, a->B), dim3(512),
+                     NS * 2 * 64 * 64, st, *a);
+  return 0;
 }
 extern "C" int tdg_attn_probs(const AttnArgs* a, int hd, float* probs, hipStream_t st) {
   TDG_HD_CASES(probs_hd, *a, probs, st)

@@ -365,6 +365,7 @@ int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, 
     TDG_F8(2, 64, 128, 2, 2, 3)
     TDG_F8(3, 256, 128, 4, 2, 2)
     TDG_F8(4, 128, 128, 2, 4, 3)
+    TDG_F8(8, 256, 128, 4, 2, 3)
     default:
       TDG_F8(5, 64, 128, 2, 2, 2)
   }

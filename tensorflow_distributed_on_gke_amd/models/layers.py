@@ -441,11 +441,19 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ctx.meta = (heads, causal, scale, site, rt)
         x2 = x.reshape(B * L, d)
         if x.is_cuda:
-            qkv = rt.fp8.linear(x2, wqkv, bqkv) if rt.fp8 is not None else None
+            f8 = rt.fp8 is not None and K.attn_fwd_fp8_ok(L, L, hd)
+            r = rt.fp8.linear(x2, wqkv, bqkv, want8=f8) if rt.fp8 is not None else None
+            qkv, qkv8 = (r[0], r[1]) if f8 and r is not None else (r, None)
             if qkv is None:
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
-            o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
+            if qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
+                q85 = qkv8.view(B, L, 3, heads, hd)
+                s8 = rt.fp8.meta.s(r[2])
+                o, aux = K.attn_fwd_fp8(q85[:, :, 0], q85[:, :, 1], q85[:, :, 2], s8, s8, s8, kv_len,
+                                        scale, causal)
+            else:
+                o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
             s = None  # projection fused with the LayerNorm below
         else:
             qkv = x2 @ wqkv.master.t() + bqkv.master
@@ -511,7 +519,12 @@ class CrossKVFn(torch.autograd.Function):
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
         ctx.save_for_backward(e2)
         if enc.is_cuda:
-            kv = rt.fp8.linear(e2.contiguous(), wkv, bkv) if rt.fp8 is not None else None
+            kv = None
+            if rt.fp8 is not None:
+                r = rt.fp8.linear(e2.contiguous(), wkv, bkv, want8=True)
+                if r is not None:  # its e4m3 copy feeds the decoders' e4m3 attention
+                    kv = r[0]
+                    rt.fp8.kv8 = (r[1].view(B, S, -1), r[2])
             if kv is None:
                 kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
         else:
@@ -566,11 +579,20 @@ class CrossAttnBlockFn(torch.autograd.Function):
         if kv5 is None:
             raise ValueError("kv_all must be contiguous")
         if x.is_cuda:
-            q = rt.fp8.linear(x2, wq, bq) if rt.fp8 is not None else None
+            f8 = (rt.fp8 is not None and rt.fp8.kv8 is not None and K.attn_fwd_fp8_ok(T, S, hd))
+            r = rt.fp8.linear(x2, wq, bq, want8=f8) if rt.fp8 is not None else None
+            q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
             if q is None:
                 q = K.linear_fwd(x2, wq.compute, bq.master)
-            o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len, scale,
-                                False)
+            if q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
+                kv8, kvs = rt.fp8.kv8
+                kv85 = kv8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+                skv = rt.fp8.meta.s(kvs)
+                o, aux = K.attn_fwd_fp8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],
+                                        rt.fp8.meta.s(r[2]), skv, skv, kv_len, scale, False)
+            else:
+                o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len,
+                                    scale, False)
             s = None  # projection fused with the LayerNorm below
         else:
             q = x2 @ wq.master.t() + bq.master

@@ -26,7 +26,7 @@ from tensorflow_distributed_on_gke_amd.ops import kernels as K
 
 FP8 = torch.float8_e4m3fn
 E4M3_MAX = 448.0
-_CANDS = (0, 1, 2, 3, 4, 5)
+_CANDS = (0, 1, 2, 3, 4, 5, 8)
 _TUNED: Dict[tuple, int] = {}
 
 
@@ -105,11 +105,11 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
 
 def choose_fp8(M: int, N: int, Kd: int) -> int:
     """fp8 tile config without a timed search (csrc/kernels/fp8.hip table):
-    the largest tile that still gives every CU a tile."""
-    if -(-M // 256) * -(-N // 128) >= K.NUM_CU:
-        return 3  # 256x128, 8 waves
+    128x128 on 4 waves whenever that fills the CUs -- it beat 256x128 / 8
+    waves on every Transformer-big forward shape, 3-14 % (qkv 42.7 vs 47.0 us,
+    xkv6 160.6 vs 186.6; profiles/r3/fp8_gemm_sweep.jsonl)."""
     if -(-M // 128) * -(-N // 128) >= K.NUM_CU:
-        return 4  # 128x128, 8 waves
+        return 0  # 128x128, 4 waves, 2 stages
     return 5
 
 
@@ -178,8 +178,12 @@ class Fp8State:
         self.ffn_slots: Dict[int, Tuple[int, int]] = {}
         # LayerNorms whose output is an fp8 GEMM input: they emit the e4m3 copy
         self.ln_slots: Dict[int, int] = {}
-        # attention input projections: weight -> activation slot
+        # attention input projections: weight -> activation slot, output slot
+        # (their e4m3 outputs feed the e4m3 attention, attention.hip
+        # attn_fwd_fp8_kernel, on the sequences it covers)
         self.proj_slots: Dict[int, int] = {}
+        self.out_slots: Dict[int, int] = {}
+        self.kv8: Optional[Tuple[torch.Tensor, int]] = None  # batched cross K|V, e4m3
         self.stash: Dict[int, torch.Tensor] = {}
         for layer in list(model.enc_layers) + list(model.dec_layers):
             self.weights.add(layer.ff1.w)
@@ -194,6 +198,7 @@ class Fp8State:
             self.weights.add(w)
             xs = self.meta.slot("p:" + w.name)
             self.proj_slots[id(w)] = xs
+            self.out_slots[id(w)] = self.meta.slot("y:" + w.name)
             if feeder_ln is not None:
                 self.ln_slots[id(feeder_ln.gamma)] = xs
 
@@ -206,10 +211,11 @@ class Fp8State:
         proj(model.cross_kv.w, enc[-1].ln2)
         self.weights.calibrate()
 
-    def linear(self, x2: torch.Tensor, w, b) -> Optional[torch.Tensor]:
+    def linear(self, x2: torch.Tensor, w, b, want8: bool = False):
         """y = x2 @ w^T + b with e4m3 operands when `w` is an fp8 attention
         projection (the input's e4m3 copy comes from its LayerNorm, else it is
-        quantised here); None otherwise."""
+        quantised here); None otherwise. want8: also the e4m3 copy of y from
+        the GEMM epilogue -- returns (y, y8, scale slot of y8)."""
         xs = self.proj_slots.get(id(w))
         if xs is None:
             return None
@@ -217,8 +223,9 @@ class Fp8State:
         x8 = self.stash.pop(xs, None)
         if x8 is None:
             x8 = quantize(x2, self.meta, xs)
-        y, _ = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws)
-        return y
+        ys = self.out_slots[id(w)] if want8 else None
+        y, y8 = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws, out8_slot=ys)
+        return (y, y8, ys) if want8 else y
 
     def after_step(self) -> None:
         self.meta.update()

@@ -351,6 +351,23 @@ def attn_fwd(q, k, v, kv_len, scale: float, causal: bool):
     return out, lse
 
 
+def attn_fwd_fp8_ok(Lq: int, Lk: int, hd: int) -> bool:
+    """Shapes the e4m3 attention forward covers (attention.hip
+    attn_fwd_fp8_kernel): hd 64, the long-sequence path."""
+    return hd == 64 and Lq > 128
+
+
+def attn_fwd_fp8(q8, k8, v8, sq, sk, sv, kv_len, scale: float, causal: bool):
+    """Attention forward on e4m3 copies q8 = e4m3(q * sq) etc. (per-tensor
+    scales, one-element device tensors): O (bf16) and the log2-domain LSE, as
+    attn_fwd; the backward (attn_bwd) works from the bf16 q / k / v."""
+    B, Lq, H, hd = q8.shape
+    out = torch.empty(B, Lq, H, hd, dtype=torch.bfloat16, device=q8.device)
+    lse = torch.empty(B, H, Lq, dtype=torch.float32, device=q8.device)
+    C().attn_fwd_fp8(q8, k8, v8, out, lse, kv_len, sq, sk, sv, scale, causal)
+    return out, lse
+
+
 def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bool):
     delta = workspace("attn_delta", lse.numel(), q.device)[: lse.numel()]
     C().attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal)

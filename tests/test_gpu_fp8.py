@@ -89,3 +89,83 @@ def test_layernorm_fused_fp8_copy(D):
     want = (y.float() * 50.0).clamp(-448, 448).to(torch.float8_e4m3fn)
     assert (y8.view(torch.uint8) == want.view(torch.uint8)).float().mean().item() > 0.999
     assert abs(meta.amax_values()[i].item() - y.float().abs().max().item()) < 1e-6 * D
+
+
+def _attn_ref(q, k, v, kv_len, causal, scale):
+    """fp32 attention with the reference's -1e9 mask add (kv_len = 0 rows:
+    uniform over all keys); O and the log2-domain log-sum-exp."""
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    B, H, Lq, Lk = s.shape
+    keys = torch.arange(Lk, device=q.device)
+    mask = (keys.view(1, 1, 1, Lk) >= kv_len.view(B, 1, 1, 1)).float().expand(B, 1, Lq, Lk)
+    if causal:
+        la = (keys.view(1, Lk) > torch.arange(Lq, device=q.device).view(Lq, 1)).float()
+        mask = torch.maximum(mask, la.view(1, 1, Lq, Lk))
+    s = s + mask * -1e9
+    p = torch.softmax(s, -1)
+    lse2 = torch.logsumexp(s, -1) / 0.6931471805599453
+    return torch.einsum("bhqk,bkhd->bqhd", p, v), lse2
+
+
+@pytest.mark.parametrize("causal,Lq,Lk", [(False, 512, 512), (True, 512, 512), (False, 260, 390),
+                                          (False, 200, 70), (True, 300, 300)])
+def test_attention_fwd_fp8(causal, Lq, Lk):
+    """e4m3 attention forward (attention.hip attn_fwd_fp8_kernel) against fp32
+    attention of the dequantised e4m3 inputs: the error left is the e4m3
+    rounding of P. Ragged key lengths and a kv_len = 0 row (non-causal)."""
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    torch.manual_seed(5)
+    B, H, hd = 3, 2, 64
+    q, k, v = (torch.randn(B, L, H, hd, device=DEV).bfloat16() for L in (Lq, Lk, Lk))
+    kv_len = torch.tensor([Lk, 0 if not causal else Lk // 2, max(1, Lk - 5)], dtype=torch.int32, device=DEV)
+    sc = [torch.tensor([448.0 / t.float().abs().max().item()], device=DEV) for t in (q, k, v)]
+    q8, k8, v8 = ((t.float() * s).clamp(-448, 448).to(torch.float8_e4m3fn) for t, s in zip((q, k, v), sc))
+    scale = hd ** -0.5
+    out, lse = kk.attn_fwd_fp8(q8, k8, v8, sc[0], sc[1], sc[2], kv_len, scale, causal)
+    qd, kd, vd = (t8.float() / s for t8, s in zip((q8, k8, v8), sc))
+    ref, lref = _attn_ref(qd, kd, vd, kv_len, causal, scale)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 4e-2, err
+    live = kv_len > 0  # (kv_len = 0 rows: the kernel's LSE is of its own zero-scale logits)
+    lerr = (lse[live] - lref[live]).abs().max().item()
+    assert lerr < 2e-2, lerr
+    # and close to the bf16 kernel on the unquantised inputs
+    ob, _ = kk.attn_fwd(q, k, v, kv_len, scale, causal)
+    assert (out.float() - ob.float()).abs().max().item() < 0.15 * ob.float().abs().max().item()
+
+
+def test_fp8_attention_training_tracks_bf16(monkeypatch):
+    """fp8 mode with e4m3 attention (hd 64, sequences > 128: the input
+    projections emit e4m3 Q|K|V, attn_fwd_fp8 consumes them) trains like
+    bf16 on the copy task."""
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    from tensorflow_distributed_on_gke_amd.train.optim import Adam
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    calls = {"n": 0}
+    real = kk.attn_fwd_fp8
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(kk, "attn_fwd_fp8", counting)
+    cfg = model_config("tiny", heads=2, src_vocab=64, tgt_vocab=64, dropout=0.0)
+    data = SyntheticPairs(batch=8, src_len=160, tgt_len=161, src_vocab=64, tgt_vocab=64, copy_task=True, seed=0)
+    finals = {}
+    for mode in ("bf16", "fp8"):
+        m = Transformer(cfg).build("cuda", seed=1)
+        opt = Adam(m.store, cfg.d_model, lr=1e-3)
+        st = F.Fp8State(m) if mode == "fp8" else None
+        step = TrainStep(m, opt, None, workers=1.0, seed=3, fp8_state=st)
+        losses = []
+        for i in range(120):
+            src, tgt = data.batch(i)
+            losses.append(step(src.cuda(), tgt.cuda())[0].item())
+        finals[mode] = (losses[0], sum(losses[-10:]) / 10)
+    assert calls["n"] > 0, "e4m3 attention did not run"
+    (b0, b1), (f0, f1) = finals["bf16"], finals["fp8"]
+    assert b1 < 0.9 * b0 and f1 < 0.9 * f0, finals  # (long copy task: slower start)
+    assert abs(f1 - b1) < 0.1 * b1 + 0.05, finals
