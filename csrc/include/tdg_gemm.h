@@ -148,7 +148,9 @@ __device__ __forceinline__ void wait_vmcnt_known() {
 // vmcnt wait leaving `n` younger tiles (PT LDS-DMA each) in flight
 template <int PT, int NMAX>
 __device__ __forceinline__ void wait_tiles(int n) {
-  static_assert(NMAX <= 4 && PT * NMAX <= 63, "vmcnt range");
+  static_assert(NMAX <= 6 && PT * NMAX <= 63, "vmcnt range");
+  if (NMAX >= 6 && n >= 6) { wait_vmcnt<(NMAX >= 6 ? 6 * PT : 0)>(); return; }
+  if (NMAX >= 5 && n >= 5) { wait_vmcnt<(NMAX >= 5 ? 5 * PT : 0)>(); return; }
   if (NMAX >= 4 && n >= 4) { wait_vmcnt<(NMAX >= 4 ? 4 * PT : 0)>(); return; }
   if (NMAX >= 3 && n >= 3) { wait_vmcnt<(NMAX >= 3 ? 3 * PT : 0)>(); return; }
   if (NMAX >= 2 && n >= 2) { wait_vmcnt<(NMAX >= 2 ? 2 * PT : 0)>(); return; }

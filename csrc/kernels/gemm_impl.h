@@ -639,7 +639,7 @@ inline int r256_single(R256Args& a, const bf16_t* const* A, const bf16_t* const*
 
 // Pipelined kernel (gemm_pipe.h): single problem, K % 32 == 0, operands
 // addressable with 31-bit byte offsets. Returns false if not applicable.
-template <int BM, int BN, int NS, bool AK, bool BKc, int EPI, bool F32>
+template <int BM, int BN, int WM, int WN, int NS, bool AK, bool BKc, int EPI, bool F32>
 bool launch_pipe(const bf16_t* A, const bf16_t* B, void* C, const float* bias, const bf16_t* aux,
                  int M, int N, int K, int lda, int ldb, int ldc, int ldaux, float alpha, float beta,
                  hipStream_t st) {
@@ -651,12 +651,13 @@ bool launch_pipe(const bf16_t* A, const bf16_t* B, void* C, const float* bias, c
   constexpr int lds = NS * (BM + BN) * PK * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pipe_kernel<BM, BN, NS, AK, BKc, EPI, F32>,
+    (void)hipFuncSetAttribute((const void*)gemm_pipe_kernel<BM, BN, WM, WN, NS, AK, BKc, EPI, F32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, NS, AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds,
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, NS, AK, BKc, EPI, F32>), dim3(tiles),
+                     dim3(WM * WN * 64), lds,
                      st, A, B, C, bias, aux, M, N, K, lda, ldb, ldc, ldaux, alpha, beta,
                      (int)(ab * 2), (int)(bb * 2));
   return true;
@@ -671,15 +672,18 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
     // software-pipelined kernel (one problem, no split-K); else cfg 0
     if (!grp && splits <= 1) {
       bool ok = false;
-      if (tile_cfg == 20)
-        ok = launch_pipe<256, 256, 4, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                         ldaux, alpha, beta, st);
-      else if (tile_cfg == 21)
-        ok = launch_pipe<256, 128, 6, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                         ldaux, alpha, beta, st);
-      else
-        ok = launch_pipe<128, 256, 6, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                                                         ldaux, alpha, beta, st);
+#define TDG_PIPE(ID, BM_, BN_, WM_, WN_, NS_)                                                      \
+  case ID:                                                                                    \
+    ok = launch_pipe<BM_, BN_, WM_, WN_, NS_, AK, BKc, EPI, F32>(A, B, C, bias, aux, M, N, K, lda, \
+                                                                 ldb, ldc, ldaux, alpha, beta, st); \
+    break;
+      switch (tile_cfg) {
+        TDG_PIPE(20, 256, 256, 2, 4, 4)
+        TDG_PIPE(21, 256, 128, 2, 4, 6)
+        TDG_PIPE(22, 128, 256, 2, 4, 6)
+        default: break;
+      }
+#undef TDG_PIPE
       if (ok) return;
     }
     tile_cfg = 0;

@@ -20,8 +20,11 @@
 //     (the k-step's last MFMA row waits only for its own fragment);
 //   * the DMA goes through buffer_load ... lds with per-lane byte offsets
 //     computed once and a scalar per-K-tile offset (no per-issue VALU).
-// 8 waves as 2 (M) x 4 (N); tiles 256x256 (wave tile 128x64), 256x128
-// (128x32), 128x256 (64x64). Same operand layouts (K- or MN-contiguous,
+// WM x WN waves: 2 x 4 for tiles 256x256 (wave tile 128x64), 256x128
+// (128x32), 128x256 (64x64). Measured and not kept
+// (profiles/gemm/r3s2_pipe_wave_layouts.txt): 128x128 with 2 x 4 waves, and
+// 2 x 2 waves (one per SIMD, fewer LDS fragment bytes per FLOP) at 128x128 /
+// 256x128 -- all slower than the lock-step 128x128 kernels at N = 512. Same operand layouts (K- or MN-contiguous,
 // XOR-swizzled images, conflict-free fragment reads) and the same epilogue
 // (EpiLds) as the other kernels. K % 32 == 0; one problem per launch.
 #pragma once
@@ -119,10 +122,10 @@ __device__ __forceinline__ short8_t pfrag(const char* lds, int base, int lane) {
 // of EpiLds): clang's host pass failed substitution of free function templates
 // taking the kernel's local operand-stage types for every kernel instantiation
 // but the first, silently dropping those kernels' host handles.
-template <int BM, int BN, int NS, bool A_KC, bool B_KC>
+template <int BM, int BN, int WM, int WN, int NS, bool A_KC, bool B_KC>
 struct Pipe {
-  static constexpr int NW = 8;
-  static constexpr int TM = BM / 32, TN = BN / 64;  // 16x16 fragments per wave (2 x 4 waves)
+  static constexpr int NW = WM * WN;
+  static constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);  // 16x16 fragments per wave
   static constexpr int A_BYTES = BM * PK * 2, SB = A_BYTES + BN * PK * 2;
   using SA = PStage<A_KC, BM, NW>;
   using SBt = PStage<B_KC, BN, NW>;
@@ -185,20 +188,20 @@ struct Pipe {
   }
 };
 
-template <int BM, int BN, int NS, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(512) void gemm_pipe_kernel(
+template <int BM, int BN, int WM, int WN, int NS, bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_pipe_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
     const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
     int ldb, int ldc, int ldaux, float alpha, float beta, int a_bytes, int b_bytes) {
-  using P = Pipe<BM, BN, NS, A_KC, B_KC>;
+  using P = Pipe<BM, BN, WM, WN, NS, A_KC, B_KC>;
   constexpr int NW = P::NW, TM = P::TM, TN = P::TN, A_BYTES = P::A_BYTES, SB = P::SB, PT = P::PT;
-  constexpr int WTM = BM / 2, WTN = BN / 4;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   static_assert(NS >= 3, "ring: refilled, being read, landed");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   int tm, tn;
