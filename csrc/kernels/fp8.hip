@@ -104,6 +104,92 @@ using tdg::pack2_e4m3;
 
 enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2 };
 
+// Epilogue of both fp8 kernels: dequant, bias, relu -> per-wave bf16 LDS
+// image -> 16-byte stores (+ the optional e4m3 copy and its amax). Called
+// after a barrier that ends every wave's reads of the pipeline stages.
+template <int BM, int BN, int WM, int WN, int EPI>
+struct F8Epi {
+  static constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int SROW = WTN * 2 + 16;
+  static constexpr int CPR = WTN / 8;
+  static constexpr int LDS = NW * WTM * SROW + 64;  // images + amax scratch
+  static __device__ __forceinline__ void run(char* smem, const f32x4 (&acc)[TM][TN],
+                                             bf16_t* __restrict__ C, const float* __restrict__ bias,
+                                             const float* __restrict__ sa,
+                                             const float* __restrict__ sb, uint8_t* __restrict__ C8,
+                                             const float* __restrict__ sc8,
+                                             unsigned* __restrict__ amax_out, int M, int N, int ldc,
+                                             int ldc8, int m0, int n0, int wid, int lane, int tid) {
+    const int wm = wid / WN, wn = wid % WN;
+    const float alpha = 1.f / (sa[0] * sb[0]);
+    const float s8 = C8 ? sc8[0] : 0.f;
+    char* wimg = smem + wid * (WTM * SROW);
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + 16 * j + cl;
+      float bn = 0.f;
+      if constexpr (EPI != F8_EPI_NONE) bn = bias[n < N ? n : N - 1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = alpha * acc[i][j][r] + bn;
+          if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+          *reinterpret_cast<bf16_t*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * 2) = f2bf(v);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float amax = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < (WTM * CPR) / 64; ++tt) {
+      const int id = lane + 64 * tt;
+      const int row = id / CPR, ch = id % CPR;
+      const int m = m0 + wm * WTM + row;
+      const int n = n0 + wn * WTN + ch * 8;
+      if (m >= M || n >= N) continue;
+      const short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
+      if (n + 8 <= N) {
+        *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
+      }
+      if (C8) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f[e] = bf2f((bf16_t)v[e]);
+          amax = fmaxf(amax, fabsf(f[e]));
+        }
+        int lo = f8::pack2_e4m3<false>(f[0] * s8, f[1] * s8, 0);
+        lo = f8::pack2_e4m3<true>(f[2] * s8, f[3] * s8, lo);
+        int hi = f8::pack2_e4m3<false>(f[4] * s8, f[5] * s8, 0);
+        hi = f8::pack2_e4m3<true>(f[6] * s8, f[7] * s8, hi);
+        if (n + 8 <= N) {
+          *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
+        } else {
+          const uint8_t* b8 = reinterpret_cast<const uint8_t*>(&lo);
+          const uint8_t* c8 = reinterpret_cast<const uint8_t*>(&hi);
+          for (int e = 0; e < 8 && n + e < N; ++e) C8[(size_t)m * ldc8 + n + e] = e < 4 ? b8[e] : c8[e - 4];
+        }
+      }
+    }
+    if (C8 && amax_out) {  // one atomic per workgroup, spread over AMAX_SPREAD words
+      amax = wave_max(amax);
+      float* red = reinterpret_cast<float*>(smem + NW * WTM * SROW);
+      if (lane == 0) red[wid] = amax;
+      __syncthreads();
+      if (tid == 0) {
+        float m = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) m = fmaxf(m, red[w]);
+        f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)), m);
+      }
+    }
+  }
+};
+
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
@@ -191,76 +277,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
     }
   }
 
-  // ---------------- epilogue: dequant, bias, relu -> bf16 LDS image -> 16-byte stores
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int SROW = WTN * 2 + 16;
-  constexpr int CPR = WTN / 8;
-  const float alpha = 1.f / (sa[0] * sb[0]);
-  const float s8 = C8 ? sc8[0] : 0.f;
   f8::lds_barrier();
-  char* wimg = smem + wid * (WTM * SROW);
-  const int g = lane >> 4, cl = lane & 15;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + 16 * j + cl;
-    float bn = 0.f;
-    if constexpr (EPI != F8_EPI_NONE) bn = bias[n < N ? n : N - 1];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = alpha * acc[i][j][r] + bn;
-        if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-        *reinterpret_cast<bf16_t*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * 2) = f2bf(v);
-      }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  float amax = 0.f;
-#pragma unroll
-  for (int tt = 0; tt < (WTM * CPR) / 64; ++tt) {
-    const int id = lane + 64 * tt;
-    const int row = id / CPR, ch = id % CPR;
-    const int m = m0 + wm * WTM + row;
-    const int n = n0 + wn * WTN + ch * 8;
-    if (m >= M || n >= N) continue;
-    const short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
-    if (n + 8 <= N) {
-      *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
-    } else {
-      for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
-    }
-    if (C8) {
-      float f[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        f[e] = bf2f((bf16_t)v[e]);
-        amax = fmaxf(amax, fabsf(f[e]));
-      }
-      int lo = f8::pack2_e4m3<false>(f[0] * s8, f[1] * s8, 0);
-      lo = f8::pack2_e4m3<true>(f[2] * s8, f[3] * s8, lo);
-      int hi = f8::pack2_e4m3<false>(f[4] * s8, f[5] * s8, 0);
-      hi = f8::pack2_e4m3<true>(f[6] * s8, f[7] * s8, hi);
-      if (n + 8 <= N) {
-        *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
-      } else {
-        const uint8_t* b8 = reinterpret_cast<const uint8_t*>(&lo);
-        const uint8_t* c8 = reinterpret_cast<const uint8_t*>(&hi);
-        for (int e = 0; e < 8 && n + e < N; ++e) C8[(size_t)m * ldc8 + n + e] = e < 4 ? b8[e] : c8[e - 4];
-      }
-    }
-  }
-  if (C8 && amax_out) {  // one atomic per workgroup, spread over AMAX_SPREAD words
-    amax = wave_max(amax);
-    float* red = reinterpret_cast<float*>(smem + NW * WTM * SROW);
-    if (lane == 0) red[wid] = amax;
-    __syncthreads();
-    if (tid == 0) {
-      float m = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) m = fmaxf(m, red[w]);
-      f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)), m);
-    }
-  }
+  F8Epi<BM, BN, WM, WN, EPI>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8,
+                                  m0, n0, wid, lane, tid);
 }
 
 // y8 = e4m3(x * scale[0]); amax_out = max|x| (both optional sides)

@@ -7,6 +7,9 @@
 // the older kernels (barrier -> reads -> wait -> MFMAs) it drops by ~25 %,
 // with both by ~70 % -- at an unchanged clock, also from L2-resident operands:
 // the phases of a K tile serialise. Here nothing waits in bulk:
+//   * fragment reads are untracked inline asm with counted lgkmcnt waits
+//     (PFrag): the compiler would otherwise drain the LDS-DMA ring before
+//     every read;
 //   * K tiles are 32 deep (one MFMA k-step) in an NS-slot LDS ring, NS-2 .. NS-1
 //     tiles in flight, one barrier per K tile and no LDS drain at it (the
 //     slot refilled in iteration kt is tile kt-1's, whose reads every wave has
@@ -16,8 +19,7 @@
 //     into the same registers (the B fragments of kt+1 are double-buffered)
 //     and, spread over the rows, its share of tile kt+NS-1's LDS-DMA pieces,
 //     so LDS reads, DMA issue and address arithmetic all run in the MFMA
-//     shadow; the compiler-visible LDS reads get exact counted lgkmcnt waits
-//     (the k-step's last MFMA row waits only for its own fragment);
+//     shadow (each MFMA row waits only for its own fragment);
 //   * the DMA goes through buffer_load ... lds with per-lane byte offsets
 //     computed once and a scalar per-K-tile offset (no per-issue VALU).
 // WM x WN waves: 2 x 4 for tiles 256x256 (wave tile 128x64), 256x128
@@ -100,23 +102,42 @@ struct PStage {
 };
 
 // MFMA operand fragment (16 rows / columns at `base`) of a PK-deep image:
-// lane l holds X(base + (l & 15), 8 (l >> 4) + j), j < 8. Compiler-tracked
-// reads (counted lgkmcnt waits, hazards handled).
+// lane l holds X(base + (l & 15), 8 (l >> 4) + j), j < 8. UNTRACKED reads
+// (inline asm, tdg_common.h): the compiler's waitcnt pass treats a plain LDS
+// read as possibly aliasing every LDS-DMA in flight and puts an
+// `s_waitcnt vmcnt(0)` in front of it, which drains the ring at every
+// fragment read (the first version of this kernel did exactly that). The
+// caller waits with a counted lgkmcnt and ties the registers before use.
 template <bool KC, int R>
-__device__ __forceinline__ short8_t pfrag(const char* lds, int base, int lane) {
-  typedef __attribute__((address_space(3))) short4_t lds4;
-  if constexpr (KC) {
-    const int row = base + (lane & 15);
-    return *reinterpret_cast<const short8_t*>(lds + plds_off<true, R>(row, (lane >> 4) * 16));
-  } else {
-    const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
-    const int krow = 8 * g + q;
-    const int byte = (base + 4 * p) * 2;
-    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(lds + plds_off<false, R>(krow, byte)));
-    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(lds + plds_off<false, R>(krow + 4, byte)));
-    return cat4(lo, hi);
+struct PFrag {
+  static constexpr int NI = KC ? 1 : 2;  // LDS instructions per fragment
+  short8_t v;       // KC
+  short4_t lo, hi;  // MC (two transposing 8-byte reads)
+  __device__ __forceinline__ void read(const char* lds, int base, int lane) {
+    if constexpr (KC) {
+      const int row = base + (lane & 15);
+      v = lds_read_b128_async(lds + plds_off<true, R>(row, (lane >> 4) * 16));
+    } else {
+      const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+      const int krow = 8 * g + q;
+      const int byte = (base + 4 * p) * 2;
+      lo = lds_read_tr_async(lds + plds_off<false, R>(krow, byte));
+      hi = lds_read_tr_async(lds + plds_off<false, R>(krow + 4, byte));
+    }
   }
-}
+  __device__ __forceinline__ void tie_() {
+    if constexpr (KC) {
+      tie(v);
+    } else {
+      tie(lo);
+      tie(hi);
+    }
+  }
+  __device__ __forceinline__ short8_t get() const {
+    if constexpr (KC) return v;
+    else return cat4(lo, hi);
+  }
+};
 
 // The K loop's pieces as static members of one class template (the pattern
 // of EpiLds): clang's host pass failed substitution of free function templates
@@ -152,8 +173,26 @@ struct Pipe {
   // kt+NS-1's DMA pieces behind the MFMA rows. FB: this tile's B fragments,
   // FN: receives the next tile's (named buffers: the caller unrolls by two so
   // every array index stays a compile-time constant).
-  static __device__ __forceinline__ void ktile(int kt, int nk, short8_t (&FB)[TN],
-                                               short8_t (&FN)[TN], short8_t (&fa)[TM],
+  using FA = PFrag<A_KC, BM>;
+  using FBt = PFrag<B_KC, BN>;
+  // LDS instructions a wave has issued after its read of A fragment i of a
+  // tile, by the time row i of that tile's MFMAs is reached: A fragments
+  // i+1.. of the same tile, the next tile's B fragments, A fragments ..i-1 of
+  // the next tile -- the same for every i
+  static constexpr int LGKM = (TM - 1) * FA::NI + TN * FBt::NI;
+  // The counter is 4 bits: with more than 15 LDS instructions in flight it
+  // no longer counts them (measured: wrong fragments, not a stall). Layouts
+  // with LGKM > 15 (MN-contiguous A at 256 rows) throttle every read to keep
+  // at most 15 in flight -- then fa[i], older than LGKM >= 16 reads, has
+  // landed by row i and the row wait is a no-op.
+  static constexpr bool THROTTLE = LGKM > 15;
+  template <typename F>
+  static __device__ __forceinline__ void throttle() {
+    if constexpr (THROTTLE) lgkm_wait<15 - F::NI>();
+  }
+
+  static __device__ __forceinline__ void ktile(int kt, int nk, FBt (&FB)[TN],
+                                               FBt (&FN)[TN], FA (&fa)[TM],
                                                f32x4 (&acc)[TM][TN], const SA& sa, const SBt& sb,
                                                char* smem, int lane, int wid, int abase,
                                                int bbase) {
@@ -171,14 +210,25 @@ struct Pipe {
     // tile from a stale slot, never used -- so the compiler's lgkmcnt
     // bookkeeping stays exact: no branch around an LDS read)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) FN[j] = pfrag<B_KC, BN>(nx + A_BYTES, bbase + 16 * j, lane);
+    for (int j = 0; j < TN; ++j) {
+      throttle<FBt>();
+      FN[j].read(nx + A_BYTES, bbase + 16 * j, lane);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      lgkm_wait<LGKM>();  // fa[i] of this tile (and this tile's B fragments)
+      fa[i].tie_();
+      if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) FB[j].tie_();
+      }
+      const short8_t a = fa[i].get();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(FB[j], fa[i], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(FB[j].get(), a, acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
-      fa[i] = pfrag<A_KC, BM>(nx, abase + 16 * i, lane);
+      throttle<FA>();
+      fa[i].read(nx, abase + 16 * i, lane);
       // this wave's DMA pieces of tile rt, spread over the MFMA rows
 #pragma unroll
       for (int q = 0; q < PT; ++q)
@@ -232,11 +282,18 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pipe_kernel(
     if (s < nk) P::stage(sa, sb, smem, s, wid);
   wait_tiles<PT, NS - 2>(min(NS - 1, nk) - 1);
   __builtin_amdgcn_s_barrier();
-  short8_t fa[TM], fb[TN], fbn[TN];
+  typename P::FA fa[TM];
+  typename P::FBt fb[TN], fbn[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) fb[j] = pfrag<B_KC, BN>(smem + A_BYTES, bbase + 16 * j, lane);
+  for (int j = 0; j < TN; ++j) {
+    lgkm_wait<15 - P::FBt::NI>();  // (prologue: at most 15 LDS reads in flight)
+    fb[j].read(smem + A_BYTES, bbase + 16 * j, lane);
+  }
 #pragma unroll
-  for (int i = 0; i < TM; ++i) fa[i] = pfrag<A_KC, BM>(smem, abase + 16 * i, lane);
+  for (int i = 0; i < TM; ++i) {
+    lgkm_wait<15 - P::FA::NI>();
+    fa[i].read(smem, abase + 16 * i, lane);
+  }
 
   // kt = 0 refills nothing (tile NS-1's slot was never used): issue it now
   if (NS - 1 < nk) P::stage(sa, sb, smem, NS - 1, wid);
@@ -248,6 +305,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pipe_kernel(
   if (kt < nk) P::ktile(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
 
   // ---------------- epilogue: per-wave LDS image over the pipeline stages
+  // (the last tile's next-fragment reads, from a stale slot, are drained here)
+  lgkm_wait<0>();
   wait_vmcnt<0>();
   lds_barrier();
   {

@@ -104,12 +104,16 @@ def test_gemm_wgrad_f32(M, N, K, splits):
     _close(out, 2 * ref, 2e-3, "gemm wgrad beta=1")
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 256, 1024), (300, 520, 128), (7010, 512, 256)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 1024), (300, 520, 128), (7010, 512, 256), (256, 264, 32)])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_gemm256_nn_tn(M, N, K, beta):
-    """256x256 tiles (cfg 12) with MN-contiguous operands: dgrad NN (bf16,
-    beta) and wgrad TN (f32, beta); NT with the bias + ReLU epilogue."""
-    cfg = 12
+@pytest.mark.parametrize("cfg", [12, 20, 21, 22])
+def test_gemm256_nn_tn(M, N, K, beta, cfg):
+    """256x256 tiles (cfg 12) and the software-pipelined kernel (cfg 20-22:
+    256x256 / 256x128 / 128x256, untracked fragment reads with counted waits)
+    with MN-contiguous operands: dgrad NN (bf16, beta) and wgrad TN (f32,
+    beta); NT with the bias + ReLU epilogue."""
+    if cfg == 12 and K % 64:
+        pytest.skip("256x256 lock-step tiles need K % 64 == 0 (falls back to cfg 0)")
     from tensorflow_distributed_on_gke_amd.ops._ext import C
     ld = (M + 7) // 8 * 8
     # NN: out[M,N] = dy[M,K] @ w[K,N]
