@@ -59,6 +59,8 @@ int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, 
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
+int tdg_fp8_quant_multi(const void* const* x, void* const* y, const long long* n, const int* slot,
+                        int nseg, const float* scale, unsigned* amax, hipStream_t st);
 int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale, unsigned* amax,
                   hipStream_t st);
 int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2, hipStream_t st);
@@ -714,6 +716,36 @@ void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
                           amax_ptr(amax), stream_of(x)), "tdg fp8_quant");
 }
 
+void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& ys,
+                     const std::vector<int64_t>& slots, const Tensor& scale, const Tensor& amax) {
+  const int n = (int)xs.size();
+  TORCH_CHECK(n >= 1 && n <= 64 && (int)ys.size() == n && (int)slots.size() == n,
+              "fp8_quant_multi: 1..64 tensors, one output and slot each");
+  check_f32(scale, "scale");
+  TORCH_CHECK(amax.numel() == 64 * scale.numel(), "fp8_quant_multi: amax is [slots, 64]");
+  std::vector<const void*> xp(n);
+  std::vector<void*> yp(n);
+  std::vector<long long> ne(n);
+  std::vector<int> sl(n);
+  for (int i = 0; i < n; ++i) {
+    check_bf16(xs[i], "x");
+    check_contig(xs[i], "x");
+    check_f8(ys[i], "y8");
+    TORCH_CHECK(ys[i].numel() >= xs[i].numel() && ys[i].is_contiguous(), "fp8_quant_multi: y8");
+    TORCH_CHECK(xs[i].device() == scale.device() && ys[i].device() == scale.device(),
+                "fp8_quant_multi: one device");
+    TORCH_CHECK(slots[i] >= 0 && slots[i] < scale.numel(), "fp8_quant_multi: slot range");
+    xp[i] = xs[i].data_ptr();
+    yp[i] = ys[i].data_ptr();
+    ne[i] = xs[i].numel();
+    sl[i] = (int)slots[i];
+  }
+  c10::DeviceGuard g(scale.device());
+  check_err(tdg_fp8_quant_multi(xp.data(), yp.data(), ne.data(), sl.data(), n,
+                                scale.data_ptr<float>(), amax_ptr(amax), stream_of(scale)),
+            "tdg fp8_quant_multi");
+}
+
 void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow2) {
   check_f32(scale, "scale");
   TORCH_CHECK(amax.numel() == 64 * scale.numel(), "fp8_scale_update: amax is [n, 64]");
@@ -894,6 +926,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum_grouped", &colsum_grouped);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("fp8_quant", &fp8_quant);
+  m.def("fp8_quant_multi", &fp8_quant_multi);
   m.def("fp8_scale_update", &fp8_scale_update);
   m.def("fp8_dequant", &fp8_dequant);
   m.def("colsum", &colsum);

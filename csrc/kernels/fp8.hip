@@ -323,6 +323,63 @@ __global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict
                     fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
+// Many tensors in one launch (the weight refresh after every optimizer step:
+// 43 weight matrices of Transformer-big, 43 launches of ~8 us before): block
+// ranges per segment from a host prefix sum, each segment its own scale and
+// amax slot.
+constexpr int QMAX = 64;
+struct QuantSegs {
+  const bf16_t* x[QMAX];
+  uint8_t* y[QMAX];
+  long long n[QMAX];
+  int slot[QMAX];
+  int blk0[QMAX + 1];
+};
+
+__global__ __launch_bounds__(256) void fp8_quant_multi_kernel(const QuantSegs segs, int nseg,
+                                                              const float* __restrict__ scale,
+                                                              unsigned* __restrict__ amax_out) {
+  int sg = 0;
+  for (int i = 1; i < nseg; ++i)
+    if ((int)blockIdx.x >= segs.blk0[i]) sg = i;
+  const bf16_t* __restrict__ x = segs.x[sg];
+  uint8_t* __restrict__ y8 = segs.y[sg];
+  const long long n = segs.n[sg];
+  const int b = blockIdx.x - segs.blk0[sg], nb = segs.blk0[sg + 1] - segs.blk0[sg];
+  const float s = scale[segs.slot[sg]];
+  float amax = 0.f;
+  for (long long i = ((long long)b * blockDim.x + threadIdx.x) * 8; i < n;
+       i += (long long)nb * blockDim.x * 8) {
+    if (i + 8 <= n) {
+      const short8_t v = *reinterpret_cast<const short8_t*>(x + i);
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = bf2f((bf16_t)v[e]);
+        amax = fmaxf(amax, fabsf(f[e]));
+      }
+      int lo = f8::pack2_e4m3<false>(f[0] * s, f[1] * s, 0);
+      lo = f8::pack2_e4m3<true>(f[2] * s, f[3] * s, lo);
+      int hi = f8::pack2_e4m3<false>(f[4] * s, f[5] * s, 0);
+      hi = f8::pack2_e4m3<true>(f[6] * s, f[7] * s, hi);
+      *reinterpret_cast<int2*>(y8 + i) = make_int2(lo, hi);
+    } else {
+      for (long long e = i; e < n; ++e) {
+        const float f = bf2f(x[e]);
+        amax = fmaxf(amax, fabsf(f));
+        y8[e] = (uint8_t)(f8::pack2_e4m3<false>(f * s, 0.f, 0) & 0xff);
+      }
+    }
+  }
+  __shared__ float red[4];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  if (threadIdx.x == 0 && amax_out)
+    f8::atomic_amax(amax_out + (long long)segs.slot[sg] * AMAX_SPREAD + (b & (AMAX_SPREAD - 1)),
+                    fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
 // Delayed scaling: scale[i] = 448 / (amax[i] * 2^margin) from last step's
 // amax (kept when nothing was recorded), then amax[i] = 0.
 __global__ void fp8_scale_update_kernel(float* __restrict__ scale, unsigned* __restrict__ amax,
@@ -410,6 +467,30 @@ extern "C" int tdg_fp8_quant(const void* x, void* y8, long long n, const float* 
   const int blocks = (int)std::min<long long>(1024, (n / 8 + 255) / 256 + 1);
   hipLaunchKernelGGL(fp8_quant_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x,
                      (uint8_t*)y8, n, scale, amax);
+  return 0;
+}
+
+// segments: x[i] (bf16, n[i] elements) -> y[i] with scale[slot[i]], amax into
+// amax[slot[i]] (AMAX_SPREAD words each); blocks split by size
+extern "C" int tdg_fp8_quant_multi(const void* const* x, void* const* y, const long long* n,
+                                   const int* slot, int nseg, const float* scale, unsigned* amax,
+                                   hipStream_t st) {
+  if (nseg <= 0 || nseg > QMAX) return -2;
+  QuantSegs q{};
+  long long total = 0;
+  for (int i = 0; i < nseg; ++i) total += n[i];
+  int blk = 0;
+  for (int i = 0; i < nseg; ++i) {
+    q.x[i] = (const bf16_t*)x[i];
+    q.y[i] = (uint8_t*)y[i];
+    q.n[i] = n[i];
+    q.slot[i] = slot[i];
+    q.blk0[i] = blk;
+    // ~4096 blocks over all segments, at least one each
+    blk += (int)std::max<long long>(1, (n[i] * 4096 + total - 1) / std::max<long long>(total, 1));
+  }
+  q.blk0[nseg] = blk;
+  hipLaunchKernelGGL(fp8_quant_multi_kernel, dim3(blk), dim3(256), 0, st, q, nseg, scale, amax);
   return 0;
 }
 

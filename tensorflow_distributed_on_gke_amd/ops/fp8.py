@@ -151,8 +151,12 @@ class Fp8Weights:
         return self.by_param[id(param)]
 
     def refresh(self) -> None:
-        for p, w8, slot in self.items:
-            C().fp8_quant(p.compute, w8, self.meta.s(slot), self.meta.a(slot))
+        """All weight copies in one launch per 64 weights (fp8_quant_multi),
+        each with its own scale and amax slot."""
+        for c0 in range(0, len(self.items), 64):
+            chunk = self.items[c0:c0 + 64]
+            C().fp8_quant_multi([p.compute for p, _, _ in chunk], [w8 for _, w8, _ in chunk],
+                                [slot for _, _, slot in chunk], self.meta.scale, self.meta.amax)
 
     def calibrate(self) -> None:
         """Initial weight scales from their actual amax."""

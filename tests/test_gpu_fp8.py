@@ -169,3 +169,24 @@ def test_fp8_attention_training_tracks_bf16(monkeypatch):
     (b0, b1), (f0, f1) = finals["bf16"], finals["fp8"]
     assert b1 < 0.9 * b0 and f1 < 0.9 * f0, finals  # (long copy task: slower start)
     assert abs(f1 - b1) < 0.1 * b1 + 0.05, finals
+
+
+def test_quant_multi_matches_single():
+    """The weight refresh's one-launch quantisation of many tensors is bitwise
+    the per-tensor quantisation, with each tensor's amax in its own slot."""
+    torch.manual_seed(3)
+    meta = F.Fp8Meta(DEV)
+    shapes = [(1024, 1024), (7, 13), (4096, 1024), (3, 8), (1000, 512)]
+    xs = [(torch.randn(*s, device=DEV) * (i + 1)).bfloat16() for i, s in enumerate(shapes)]
+    slots = [meta.slot(f"w{i}") for i in range(len(xs))]
+    for i, s in enumerate(slots):
+        meta.scale[s] = 448.0 / (i + 1) / 5.0
+    want = [F.quantize(x, meta, s, record=False) for x, s in zip(xs, slots)]
+    got = [torch.empty_like(w) for w in want]
+    from tensorflow_distributed_on_gke_amd.ops._ext import C
+    C().fp8_quant_multi(xs, got, slots, meta.scale, meta.amax)
+    for g, w in zip(got, want):
+        assert torch.equal(g.view(torch.uint8), w.view(torch.uint8))
+    am = meta.amax_values()
+    for x, s in zip(xs, slots):
+        assert am[s].item() == x.float().abs().max().item()
