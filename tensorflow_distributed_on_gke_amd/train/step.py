@@ -212,9 +212,9 @@ class TrainStep:
         return True
 
     def choose_dp_mode(self, src: torch.Tensor, tgt: torch.Tensor, steps: int = 8,
-                       rounds: int = 2, margin: float = 0.03) -> Dict[str, object]:
+                       rounds: int = 3, margin: float = 0.03) -> Dict[str, object]:
         """Data parallel: capture the segmented graph, then time it against the
-        eager step on this batch (interleaved rounds, best per mode, MAX over
+        eager step on this batch (interleaved rounds, median per mode, MAX over
         ranks so every rank takes the same decision) and keep the faster. The
         segmented graph wins when the host is the bottleneck (eight ranks
         sharing a node's CPUs: the eager step's enqueue costs about its GPU
@@ -243,13 +243,16 @@ class TrainStep:
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / steps
 
-        best = {"seg": float("inf"), "0": float("inf")}
+        runs = {"seg": [], "0": []}
         for _ in range(rounds):
             self.segments = seg
-            best["seg"] = min(best["seg"], timed(lambda: self(src, tgt)))
+            runs["seg"].append(timed(lambda: self(src, tgt)))
             self.segments = None
-            best["0"] = min(best["0"], timed(lambda: self.eager(src, tgt)))
-        t = torch.tensor([best["seg"], best["0"]], dtype=torch.float64, device=dev)
+            runs["0"].append(timed(lambda: self.eager(src, tgt)))
+        # median per mode: one noisy round (box clock, host contention) does
+        # not decide the mode for the whole run
+        med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
+        t = torch.tensor([med["seg"], med["0"]], dtype=torch.float64, device=dev)
         self.ddp.check_quiescent("choose_dp_mode")
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ddp.group)
         seg_s, eager_s = float(t[0]), float(t[1])
