@@ -181,14 +181,16 @@ struct Pipe {
   // the next tile -- the same for every i
   static constexpr int LGKM = (TM - 1) * FA::NI + TN * FBt::NI;
   // The counter is 4 bits: with more than 15 LDS instructions in flight it
-  // no longer counts them (measured: wrong fragments, not a stall). Layouts
-  // with LGKM > 15 (MN-contiguous A at 256 rows) throttle every read to keep
-  // at most 15 in flight -- then fa[i], older than LGKM >= 16 reads, has
-  // landed by row i and the row wait is a no-op.
-  static constexpr bool THROTTLE = LGKM > 15;
+  // no longer counts them -- a later counted wait passes early, the compiler
+  // reuses the destination registers, and the late data lands on top of
+  // whatever they hold by then (measured: wrong fragments, and an illegal
+  // address once an address register was hit). So every read first waits
+  // for at most 15 - NI in flight (free in the steady state whenever
+  // LGKM <= 15 - NI); with LGKM > 15 (MN-contiguous A at 256 rows) fa[i],
+  // older than LGKM >= 16 reads, has landed by row i anyway.
   template <typename F>
   static __device__ __forceinline__ void throttle() {
-    if constexpr (THROTTLE) lgkm_wait<15 - F::NI>();
+    lgkm_wait<15 - F::NI>();
   }
 
   static __device__ __forceinline__ void ktile(int kt, int nk, FBt (&FB)[TN],
