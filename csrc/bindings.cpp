@@ -361,8 +361,8 @@ void check_f8(const Tensor& t, const char* n) {
 }
 unsigned* amax_ptr(const optional<Tensor>& t) {
   if (!t.has_value()) return nullptr;
-  TORCH_CHECK(t->is_cuda() && t->element_size() == 4 && t->numel() >= 64,
-              "amax must be a 64-word GPU tensor (one fp8 slot)");
+  TORCH_CHECK(t->is_cuda() && t->element_size() == 4 && t->numel() >= 2048,
+              "amax must be a 2048-word GPU tensor (one fp8 slot: 64 words, 32 apart)");
   return reinterpret_cast<unsigned*>(t->data_ptr());
 }
 
@@ -722,7 +722,7 @@ void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& y
   TORCH_CHECK(n >= 1 && n <= 64 && (int)ys.size() == n && (int)slots.size() == n,
               "fp8_quant_multi: 1..64 tensors, one output and slot each");
   check_f32(scale, "scale");
-  TORCH_CHECK(amax.numel() == 64 * scale.numel(), "fp8_quant_multi: amax is [slots, 64]");
+  TORCH_CHECK(amax.numel() == 2048 * scale.numel(), "fp8_quant_multi: amax is [slots, 2048]");
   std::vector<const void*> xp(n);
   std::vector<void*> yp(n);
   std::vector<long long> ne(n);
@@ -748,7 +748,7 @@ void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& y
 
 void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow2) {
   check_f32(scale, "scale");
-  TORCH_CHECK(amax.numel() == 64 * scale.numel(), "fp8_scale_update: amax is [n, 64]");
+  TORCH_CHECK(amax.numel() == 2048 * scale.numel(), "fp8_scale_update: amax is [n, 2048]");
   c10::DeviceGuard g(scale.device());
   check_err(tdg_fp8_scale_update(scale.data_ptr<float>(), amax_ptr(amax), (int)scale.numel(),
                                  (float)margin_pow2, stream_of(scale)), "tdg fp8_scale_update");

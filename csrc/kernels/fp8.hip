@@ -184,7 +184,7 @@ struct F8Epi {
         float m = 0.f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) m = fmaxf(m, red[w]);
-        f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)), m);
+        f8::atomic_amax(amax_word(amax_out, blockIdx.x), m);
       }
     }
   }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
   __syncthreads();
   if (threadIdx.x == 0 && amax_out)
-    f8::atomic_amax(amax_out + (blockIdx.x & (AMAX_SPREAD - 1)),
+    f8::atomic_amax(amax_word(amax_out, blockIdx.x),
                     fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
@@ -376,24 +376,26 @@ __global__ __launch_bounds__(256) void fp8_quant_multi_kernel(const QuantSegs se
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
   __syncthreads();
   if (threadIdx.x == 0 && amax_out)
-    f8::atomic_amax(amax_out + (long long)segs.slot[sg] * AMAX_SPREAD + (b & (AMAX_SPREAD - 1)),
+    f8::atomic_amax(amax_word(amax_out + (long long)segs.slot[sg] * AMAX_WORDS, b),
                     fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 // Delayed scaling: scale[i] = 448 / (amax[i] * 2^margin) from last step's
 // amax (kept when nothing was recorded), then amax[i] = 0.
-__global__ void fp8_scale_update_kernel(float* __restrict__ scale, unsigned* __restrict__ amax,
-                                        int n, float margin_pow2) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per slot, lane j reads (and clears) word j of the slot's spread.
+__global__ __launch_bounds__(256) void fp8_scale_update_kernel(float* __restrict__ scale,
+                                                               unsigned* __restrict__ amax, int n,
+                                                               float margin_pow2) {
+  static_assert(AMAX_SPREAD == 64, "one lane per spread word");
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= n) return;
-  unsigned m = 0u;
+  unsigned* w = amax + (long long)i * AMAX_WORDS + lane * AMAX_STRIDE;
+  unsigned m = *w;
+  *w = 0u;
 #pragma unroll
-  for (int j = 0; j < AMAX_SPREAD; ++j) {
-    m = max(m, amax[i * AMAX_SPREAD + j]);
-    amax[i * AMAX_SPREAD + j] = 0u;
-  }
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
   const float a = __uint_as_float(m);
-  if (a > 0.f && isfinite(a)) scale[i] = E4M3_MAX / (a * margin_pow2);
+  if (lane == 0 && a > 0.f && isfinite(a)) scale[i] = E4M3_MAX / (a * margin_pow2);
 }
 
 // e4m3 -> f32 (tests / debugging)
@@ -496,8 +498,8 @@ extern "C" int tdg_fp8_quant_multi(const void* const* x, void* const* y, const l
 
 extern "C" int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2,
                                     hipStream_t st) {
-  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, scale, amax,
-                     n, margin_pow2);
+  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(cdiv(n, 4)), dim3(256), 0, st, scale, amax, n,
+                     margin_pow2);
   return 0;
 }
 

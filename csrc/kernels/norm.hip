@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     if (lane == 0) red8[threadIdx.x >> 6] = am;
     __syncthreads();
     if (threadIdx.x == 0 && amax8)
-      atomic_amax(amax8 + (blockIdx.x & (AMAX_SPREAD - 1)),
+      atomic_amax(amax_word(amax8, blockIdx.x),
                   fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
   }
 }

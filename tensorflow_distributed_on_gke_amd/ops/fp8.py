@@ -26,6 +26,7 @@ from tensorflow_distributed_on_gke_amd.ops import kernels as K
 
 FP8 = torch.float8_e4m3fn
 E4M3_MAX = 448.0
+AMAX_WORDS = 64 * 32  # per slot (csrc/include/tdg_common.h AMAX_WORDS)
 _CANDS = (0, 1, 2, 3, 4, 5, 8)
 _TUNED: Dict[tuple, int] = {}
 
@@ -34,8 +35,9 @@ class Fp8Meta:
     def __init__(self, device, capacity: int = 256, margin: int = 0):
         self.device = torch.device(device)
         self.scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
-        # [slot, 64]: producers spread their atomics over 64 words (AMAX_SPREAD)
-        self.amax = torch.zeros(capacity, 64, dtype=torch.int32, device=self.device)
+        # [slot, 2048]: producers spread their atomics over 64 words, one per
+        # 128-byte line (tdg_common.h AMAX_SPREAD / AMAX_STRIDE; the rest stay 0)
+        self.amax = torch.zeros(capacity, AMAX_WORDS, dtype=torch.int32, device=self.device)
         self.margin = margin
         self.names: List[str] = []
 
