@@ -1620,7 +1620,17 @@ int fwd_hd(const AttnArgs& a, hipStream_t st) {
   }
   if (a.Lq > 64) {
     dim3 grid(cdiv(a.Lq, 128), a.H, a.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 8, 128, 1>), grid, dim3(512), 4 * ATile<HD>::BYTES, st, a);
+    // 4 waves x 2 query subtiles (each K / V fragment read from LDS feeds two
+    // MFMAs; 225 VGPRs, two 4-wave workgroups per CU): 9.6 vs 10.3 us (causal
+    // 10.3 vs 11.7) for 8 waves x 1 subtile, whose 142 VGPRs fit only one
+    // 8-wave workgroup per CU -- the 512 (batch, head) items ran in two
+    // rounds (profiles/r3s2/attn_short_fwd_variants.txt); headline step
+    // 5.04-5.06 vs 5.07-5.08 ms A/B (profiles/r3s2/attn_short_fwd_ab.txt)
+    // (hd 128: 8 waves x 1 subtile, two subtiles per wave would spill)
+    if constexpr (HD <= 64)
+      hipLaunchKernelGGL((attn_fwd_kernel<HD, 4, 128, 2>), grid, dim3(256), 4 * ATile<HD>::BYTES, st, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<HD, 8, 128, 1>), grid, dim3(512), 4 * ATile<HD>::BYTES, st, a);
   } else {
     dim3 grid(cdiv(a.Lq, 64), a.H, a.B);
     hipLaunchKernelGGL((attn_fwd_kernel<HD, 4, 64, 1>), grid, dim3(256), 2 * ATile<HD>::BYTES, st, a);
