@@ -1354,11 +1354,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 // wave w owns queries 16w..16w+15): dQ^T = K^T dS^T.
 // Versus the three-kernel path (delta, dK/dV, dQ): every tile is read from
 // HBM once and there is one launch instead of three.
-template <int HD>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 4 : 2))) void attn_bwd_fused_kernel(AttnArgs a) {
+// U: 16-key (phase 1) / 16-query (phase 2) subtiles per wave, 8 / U waves.
+// U = 2 reads every Q / dO / K fragment from LDS once for two MFMAs (the
+// U = 1 loops issue one LDS read per MFMA).
+template <int HD, int U>
+__global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 ? (HD <= 64 ? 4 : 2) : 2))) void attn_bwd_fused_kernel(AttnArgs a) {
   using T = ATile<HD>;
   using TS = ATile<128>;  // dS image: 128 key rows x 128 queries (bf16)
   constexpr int R = 128;
+  constexpr int NT = 512 / U;  // threads
   constexpr int TB = R * T::RB;  // bytes of one 128-row tile image
   constexpr int SB = R * TS::RB;  // dS image bytes (32 KiB)
   constexpr int ALIAS = 2 * TB >= SB;  // dS fits over Q + dO
@@ -1386,27 +1390,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
   const bf16_t* ob = a.dout + b * a.do_sb + h * a.do_sh;
   const bf16_t* kbp = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* obo = a.o + b * a.o_sb + h * a.o_sh;
-  const int key = 16 * w + cl;
-  short8_t kf[T::KS], vf[T::KS];
-  {
-    const int krow = min(key, a.Lk - 1);
+  int key[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) key[u] = 16 * (U * w + u) + cl;
+  short8_t kf[U][T::KS], vf[U][T::KS];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int krow = min(key[u], a.Lk - 1);
     const bf16_t* kp = kbp + (long long)krow * a.k_sl;
     const bf16_t* vp = a.v + b * a.v_sb + (long long)krow * a.v_sl + h * a.v_sh;
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) {
-      kf[ks] = gfrag<HD>(kp, key < a.Lk, ks, lane);
-      vf[ks] = gfrag<HD>(vp, key < a.Lk, ks, lane);
+      kf[u][ks] = gfrag<HD>(kp, key[u] < a.Lk, ks, lane);
+      vf[u][ks] = gfrag<HD>(vp, key[u] < a.Lk, ks, lane);
     }
   }
   {
     constexpr int CPR = HD / 8;  // 16-byte chunks per row
     constexpr int TOTAL = R * CPR;
-    constexpr int NI = (TOTAL + 511) / 512;
+    constexpr int NI = (TOTAL + NT - 1) / NT;
     short8_t vq[NI], vo[NI], vk[NI], vx[NI];
     const short8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int id = tid + i * 512;
+      const int id = tid + i * NT;
       const int row = id / CPR, cc = id % CPR;
       vq[i] = vo[i] = vk[i] = vx[i] = z;
       if (id < TOTAL && row < a.Lq) {
@@ -1420,7 +1427,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
     const float lse_v = (tid < R && tid < a.Lq) ? a.lse[((long long)b * a.H + h) * a.Lq + tid] : INFINITY;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int id = tid + i * 512;
+      const int id = tid + i * NT;
       const int row = id / CPR, cc = id % CPR;
       if (id < TOTAL) {
         *reinterpret_cast<short8_t*>(ldsQ + T::off(row, cc * 16)) = vq[i];
@@ -1441,103 +1448,141 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HD <= 64 ? 
   __syncthreads();
   TDG_STAMP(1);
 
-  // ---- phase 1: this wave's 16 keys against all queries
-  const bool kvalid = key < klim;
-  const bool active = 16 * w < klim;  // wave-uniform
-  f32x4 dk[T::DT], dv[T::DT];
+  // ---- phase 1: this wave's U x 16 keys against all queries
+  f32x4 dk[U][T::DT], dv[U][T::DT];
 #pragma unroll
-  for (int i = 0; i < T::DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dk[u][i] = dv[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   // P and dS of [q = 16t + 4g + r][key], packed to bf16 pairs as produced
-  uint32_t pk[8][2], dk2[8][2];
+  uint32_t pk[U][8][2], dk2[U][8][2];
+  const bool active = 16 * U * w < klim;  // wave-uniform
   if (active) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dpv = {0.f, 0.f, 0.f, 0.f};
-      const bool live = 16 * t < a.Lq && (!causal || 16 * t + 15 >= 16 * w);  // uniform
+      f32x4 sv[U], dpv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool live = 16 * t < a.Lq && (!causal || 16 * t + 15 >= 16 * U * w);  // uniform
       if (live) {
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
-          sv = mfma16(T::frag_row(ldsQ, 16 * t, ks, lane), kf[ks], sv);
-          dpv = mfma16(T::frag_row(ldsO, 16 * t, ks, lane), vf[ks], dpv);
+          const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
+          const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
+            dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
+          }
         }
       }
       // lse / delta of queries 16t + 4g .. +3: one 16-byte LDS read each
       const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 16 * t + 4 * g);
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 16 * t + 4 * g);
-      float pv[4], dv4[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = 16 * t + 4 * g + r;
-        const bool ok = live && kvalid && q < a.Lq && (!causal || key <= q);
-        pv[r] = ok ? fast_exp2(sv[r] * c - l4[r]) : 0.f;
-        dv4[r] = pv[r] * (dpv[r] - d4[r]);
+      for (int u = 0; u < U; ++u) {
+        float pv[4], dv4[4];
+        const bool kvalid = key[u] < klim;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * t + 4 * g + r;
+          const bool ok = live && kvalid && q < a.Lq && (!causal || key[u] <= q);
+          pv[r] = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
+          dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
+        }
+        pk[u][t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
+        pk[u][t][1] = (uint32_t)f2bf(pv[2]) | ((uint32_t)f2bf(pv[3]) << 16);
+        dk2[u][t][0] = (uint32_t)f2bf(dv4[0]) | ((uint32_t)f2bf(dv4[1]) << 16);
+        dk2[u][t][1] = (uint32_t)f2bf(dv4[2]) | ((uint32_t)f2bf(dv4[3]) << 16);
       }
-      pk[t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
-      pk[t][1] = (uint32_t)f2bf(pv[2]) | ((uint32_t)f2bf(pv[3]) << 16);
-      dk2[t][0] = (uint32_t)f2bf(dv4[0]) | ((uint32_t)f2bf(dv4[1]) << 16);
-      dk2[t][1] = (uint32_t)f2bf(dv4[2]) | ((uint32_t)f2bf(dv4[3]) << 16);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       if (32 * s2 >= a.Lq) break;
-      const short8_t pf = __builtin_bit_cast(
-          short8_t, make_uint4(pk[2 * s2][0], pk[2 * s2][1], pk[2 * s2 + 1][0], pk[2 * s2 + 1][1]));
-      const short8_t dsf = __builtin_bit_cast(
-          short8_t, make_uint4(dk2[2 * s2][0], dk2[2 * s2][1], dk2[2 * s2 + 1][0], dk2[2 * s2 + 1][1]));
+      short8_t pf[U], dsf[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pf[u] = __builtin_bit_cast(short8_t, make_uint4(pk[u][2 * s2][0], pk[u][2 * s2][1],
+                                                        pk[u][2 * s2 + 1][0], pk[u][2 * s2 + 1][1]));
+        dsf[u] = __builtin_bit_cast(short8_t, make_uint4(dk2[u][2 * s2][0], dk2[u][2 * s2][1],
+                                                         dk2[u][2 * s2 + 1][0], dk2[u][2 * s2 + 1][1]));
+      }
 #pragma unroll
       for (int dt = 0; dt < T::DT; ++dt) {
-        dv[dt] = mfma16(T::frag_tr(ldsO, s2, dt, lane), pf, dv[dt]);
-        dk[dt] = mfma16(T::frag_tr(ldsQ, s2, dt, lane), dsf, dk[dt]);
+        const short8_t otr = T::frag_tr(ldsO, s2, dt, lane);
+        const short8_t qtr = T::frag_tr(ldsQ, s2, dt, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          dv[u][dt] = mfma16(otr, pf[u], dv[u][dt]);
+          dk[u][dt] = mfma16(qtr, dsf[u], dk[u][dt]);
+        }
       }
     }
   } else {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) dk2[t][0] = dk2[t][1] = 0u;
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) dk2[u][t][0] = dk2[u][t][1] = 0u;
   }
   TDG_STAMP(2);
   __syncthreads();  // everyone done with Q / dO (the dS image aliases them)
   // dS^T image: row = key, bytes (16t + 4g) * 2 .. +8 = queries 16t+4g .. +3
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
-    *reinterpret_cast<uint2*>(ldsS + TS::off(key, (16 * t + 4 * g) * 2)) = make_uint2(dk2[t][0], dk2[t][1]);
-  // dK, dV out (key rows on lanes)
-  if (key < a.Lk) {
-    bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key * a.dk_sl + h * a.dk_sh;
-    bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key * a.dv_sl + h * a.dv_sh;
-    const float sc = a.scale;
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      uint32_t lo = (uint32_t)f2bf(dk[dt][0] * sc) | ((uint32_t)f2bf(dk[dt][1] * sc) << 16);
-      uint32_t hi = (uint32_t)f2bf(dk[dt][2] * sc) | ((uint32_t)f2bf(dk[dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-      lo = (uint32_t)f2bf(dv[dt][0]) | ((uint32_t)f2bf(dv[dt][1]) << 16);
-      hi = (uint32_t)f2bf(dv[dt][2]) | ((uint32_t)f2bf(dv[dt][3]) << 16);
-      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    for (int t = 0; t < 8; ++t)
+      *reinterpret_cast<uint2*>(ldsS + TS::off(key[u], (16 * t + 4 * g) * 2)) = make_uint2(dk2[u][t][0], dk2[u][t][1]);
+  // dK, dV out (key rows on lanes)
+  const float sc = a.scale;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (key[u] < a.Lk) {
+      bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
+      bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) {
+        uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
+        uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
+        *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+        lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
+        hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
+        *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+      }
     }
   }
   __syncthreads();
 
-  // ---- phase 2: dQ for queries 16w .. 16w+15 (query on lanes)
-  const int qrow = 16 * w + cl;
-  if (16 * w >= a.Lq) return;
-  f32x4 dq[T::DT];
+  // ---- phase 2: dQ for queries 16 (U w + u) .. +15 (query on lanes)
+  if (16 * U * w >= a.Lq) return;
+  f32x4 dq[U][T::DT];
 #pragma unroll
-  for (int i = 0; i < T::DT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < T::DT; ++i) dq[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s2 = 0; s2 < 4; ++s2) {
     if (32 * s2 >= klim) break;
-    const short8_t dsf = TS::frag_tr(ldsS, s2, w, lane);
+    short8_t dsf[U];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) dq[dt] = mfma16(T::frag_tr(ldsK, s2, dt, lane), dsf, dq[dt]);
+    for (int u = 0; u < U; ++u) dsf[u] = TS::frag_tr(ldsS, s2, U * w + u, lane);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      const short8_t ktr = T::frag_tr(ldsK, s2, dt, lane);
+#pragma unroll
+      for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(ktr, dsf[u], dq[u][dt]);
+    }
   }
-  if (qrow >= a.Lq) return;
-  bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow * a.dq_sl + h * a.dq_sh;
-  const float sc = a.scale;
 #pragma unroll
-  for (int dt = 0; dt < T::DT; ++dt) {
-    const uint32_t lo = (uint32_t)f2bf(dq[dt][0] * sc) | ((uint32_t)f2bf(dq[dt][1] * sc) << 16);
-    const uint32_t hi = (uint32_t)f2bf(dq[dt][2] * sc) | ((uint32_t)f2bf(dq[dt][3] * sc) << 16);
-    *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+  for (int u = 0; u < U; ++u) {
+    const int qrow = 16 * (U * w + u) + cl;
+    if (qrow >= a.Lq) continue;
+    bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow * a.dq_sl + h * a.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) {
+      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
+      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
+      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
   }
 #ifdef TDG_STAMPS
   TDG_STAMP(3);
@@ -1647,13 +1692,17 @@ template <int HD>
 int bwd_hd(const AttnArgs& a, hipStream_t st) {
   if (a.Lq <= 128 && a.Lk <= 128) {
     constexpr int lds = fused_bwd_lds<HD>();
+    // U = 1: 8 waves, 16 keys / queries each. U = 2 (4 waves, every fragment
+    // read feeding two MFMAs, 231 VGPRs) measured slower: 22.7 vs 21.7 us per
+    // call, step 5.15 vs 5.13 ms (profiles/r3s2/attn_bwd_u2.txt)
+    constexpr int U = 1;
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<HD>,
+      hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<HD, U>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL(attn_bwd_fused_kernel<HD>, dim3(a.B * a.H), dim3(512), lds, st, a);
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, U>), dim3(a.B * a.H), dim3(512 / U), lds, st, a);
     return 0;
   }
   // dQ first: it also writes delta = rowsum(dO * O), which dK/dV reads
