@@ -58,12 +58,14 @@ int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, 
                     float beta, float* const* bias_out, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
-                 int lda, int ldb, int ldc, int ldc8, int epi, int cfg, hipStream_t st);
+                 int lda, int ldb, int ldc, int ldc8, int epi, int cfg, int afmt, int cfmt,
+                 const void* aux, int ldaux, float beta, hipStream_t st);
 int tdg_fp8_quant_multi(const void* const* x, void* const* y, const long long* n, const int* slot,
                         int nseg, const float* scale, unsigned* amax, hipStream_t st);
 int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale, unsigned* amax,
-                  hipStream_t st);
-int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2, hipStream_t st);
+                  int fmt, hipStream_t st);
+int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2, float fmax,
+                         hipStream_t st);
 int tdg_fp8_dequant(const void* x8, float* y, long long n, float inv_scale, hipStream_t st);
 int tdg_xent(void* logits, int M, int V, int ldl, const void* labels, int lab64, const float* ntok,
              float workers, float smoothing, float* row_loss, float* row_correct, int write_grad,
@@ -679,7 +681,8 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<
               const Tensor& sa, const Tensor& sb, const optional<Tensor>& C8,
               const optional<Tensor>& sc8, const optional<Tensor>& amax, int64_t M, int64_t N,
               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldc8, int64_t epi,
-              int64_t cfg) {
+              int64_t cfg, int64_t afmt, int64_t cfmt, const optional<Tensor>& aux, int64_t ldaux,
+              double beta) {
   check_f8(A, "A8");
   check_f8(B, "B8");
   check_bf16(C, "C");
@@ -689,7 +692,11 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<
   TORCH_CHECK(A.numel() >= (M - 1) * lda + K && B.numel() >= (N - 1) * ldb + K, "gemm_fp8: A/B extent");
   TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc % 8 == 0, "gemm_fp8: C extent / ldc");
   if (bias.has_value()) check_f32(*bias, "bias");
-  TORCH_CHECK(epi == 0 || bias.has_value(), "gemm_fp8: epilogue needs bias");
+  TORCH_CHECK(epi == 0 || epi == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
+  TORCH_CHECK(epi != 3 || (aux.has_value() && aux->numel() >= (M - 1) * ldaux + N),
+              "gemm_fp8: the ReLU-backward epilogue needs aux [M, >= N]");
+  if (aux.has_value()) check_bf16(*aux, "aux");
+  TORCH_CHECK((afmt == 0 || afmt == 1) && (cfmt == 0 || cfmt == 1), "gemm_fp8: formats are 0 / 1");
   if (C8.has_value()) {
     check_f8(*C8, "C8");
     TORCH_CHECK(sc8.has_value() && C8->numel() >= (M - 1) * ldc8 + N && ldc8 % 8 == 0, "gemm_fp8: C8");
@@ -700,12 +707,13 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<
                               sb.data_ptr<float>(), C8 ? C8->data_ptr() : nullptr,
                               sc8 ? sc8->data_ptr<float>() : nullptr, amax_ptr(amax), (int)M,
                               (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)ldc8, (int)epi,
-                              (int)cfg, stream_of(A));
+                              (int)cfg, (int)afmt, (int)cfmt, aux ? aux->data_ptr() : nullptr,
+                              (int)ldaux, (float)beta, stream_of(A));
   check_err(rc, "tdg gemm_fp8");
 }
 
 void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
-               const optional<Tensor>& amax) {
+               const optional<Tensor>& amax, int64_t fmt) {
   check_bf16(x, "x");
   check_contig(x, "x");
   check_f8(y8, "y8");
@@ -713,7 +721,7 @@ void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
   check_f32(scale, "scale");
   c10::DeviceGuard g(x.device());
   check_err(tdg_fp8_quant(x.data_ptr(), y8.data_ptr(), x.numel(), scale.data_ptr<float>(),
-                          amax_ptr(amax), stream_of(x)), "tdg fp8_quant");
+                          amax_ptr(amax), (int)fmt, stream_of(x)), "tdg fp8_quant");
 }
 
 void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& ys,
@@ -746,12 +754,12 @@ void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& y
             "tdg fp8_quant_multi");
 }
 
-void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow2) {
+void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow2, double fmax) {
   check_f32(scale, "scale");
   TORCH_CHECK(amax.numel() == 2048 * scale.numel(), "fp8_scale_update: amax is [n, 2048]");
   c10::DeviceGuard g(scale.device());
   check_err(tdg_fp8_scale_update(scale.data_ptr<float>(), amax_ptr(amax), (int)scale.numel(),
-                                 (float)margin_pow2, stream_of(scale)), "tdg fp8_scale_update");
+                                 (float)margin_pow2, (float)fmax, stream_of(scale)), "tdg fp8_scale_update");
 }
 
 void fp8_dequant(const Tensor& x8, const Tensor& y, double inv_scale) {

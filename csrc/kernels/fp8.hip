@@ -100,14 +100,38 @@ __device__ __forceinline__ void lds_barrier() {
 using tdg::atomic_amax;
 using tdg::pack2_e4m3;
 
+// OCP e5m2 (gfx950 bf8): the gradient format of the fp8 backward
+constexpr float E5M2_MAX = 57344.f;
+template <bool HI>
+__device__ __forceinline__ int pack2_e5m2(float a, float b, int old) {
+  a = fminf(fmaxf(a, -E5M2_MAX), E5M2_MAX);
+  b = fminf(fmaxf(b, -E5M2_MAX), E5M2_MAX);
+  return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
+}
+// FMT 0: e4m3, 1: e5m2
+template <int FMT, bool HI>
+__device__ __forceinline__ int pack2_f8(float a, float b, int old) {
+  if constexpr (FMT == 0) return pack2_e4m3<HI>(a, b, old);
+  else return pack2_e5m2<HI>(a, b, old);
+}
+
 }  // namespace f8
 
-enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2 };
+enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2, F8_EPI_DRELU = 3 };
 
-// Epilogue of both fp8 kernels: dequant, bias, relu -> per-wave bf16 LDS
-// image -> 16-byte stores (+ the optional e4m3 copy and its amax). Called
-// after a barrier that ends every wave's reads of the pipeline stages.
-template <int BM, int BN, int WM, int WN, int EPI>
+// Backward-GEMM extras: the ReLU mask operand (F8_EPI_DRELU: out = 0 where
+// aux <= 0) and C = alpha A B^T + beta C.
+struct F8Extra {
+  const bf16_t* aux;
+  int ldaux;
+  float beta;
+};
+
+// Epilogue: dequant, bias, relu -> per-wave bf16 LDS image -> 16-byte
+// stores (ReLU-backward mask and beta applied per 8-column chunk) + the
+// optional fp8 copy (format CF) and its amax. Called after a barrier that
+// ends every wave's reads of the pipeline stages.
+template <int BM, int BN, int WM, int WN, int EPI, int CF = 0>
 struct F8Epi {
   static constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -120,17 +144,38 @@ struct F8Epi {
                                              const float* __restrict__ sb, uint8_t* __restrict__ C8,
                                              const float* __restrict__ sc8,
                                              unsigned* __restrict__ amax_out, int M, int N, int ldc,
-                                             int ldc8, int m0, int n0, int wid, int lane, int tid) {
+                                             int ldc8, int m0, int n0, int wid, int lane, int tid,
+                                             const F8Extra& ex) {
     const int wm = wid / WN, wn = wid % WN;
     const float alpha = 1.f / (sa[0] * sb[0]);
     const float s8 = C8 ? sc8[0] : 0.f;
     char* wimg = smem + wid * (WTM * SROW);
     const int g = lane >> 4, cl = lane & 15;
+    // the ReLU mask / old C of every chunk this lane stores, loaded before
+    // the image is written (one memory latency per tile, not per chunk)
+    constexpr int ITER = (WTM * CPR) / 64;
+    constexpr bool PRE = EPI == F8_EPI_DRELU;
+    short8_t pre_aux[PRE ? ITER : 1], pre_c[PRE ? ITER : 1];
+    const bool vec_ok = (ldc & 7) == 0 && (EPI != F8_EPI_DRELU || (ex.ldaux & 7) == 0);
+    if constexpr (PRE) {
+#pragma unroll
+      for (int tt = 0; tt < ITER; ++tt) {
+        const int id = lane + 64 * tt;
+        const int row = id / CPR, ch = id % CPR;
+        const int m = m0 + wm * WTM + row;
+        const int n = n0 + wn * WTN + ch * 8;
+        pre_aux[tt] = pre_c[tt] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        if (vec_ok && m < M && n + 8 <= N) {
+          pre_aux[tt] = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
+          if (ex.beta != 0.f) pre_c[tt] = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WTN + 16 * j + cl;
       float bn = 0.f;
-      if constexpr (EPI != F8_EPI_NONE) bn = bias[n < N ? n : N - 1];
+      if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -149,7 +194,33 @@ struct F8Epi {
       const int m = m0 + wm * WTM + row;
       const int n = n0 + wn * WTN + ch * 8;
       if (m >= M || n >= N) continue;
-      const short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
+      short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
+      if (EPI == F8_EPI_DRELU || ex.beta != 0.f) {
+        // 16-byte mask / old-C loads for whole aligned chunks (8 scalar
+        // 2-byte loads per chunk made the ReLU-backward GEMM 2.4x slower)
+        const bool vec = n + 8 <= N && vec_ok;
+        short8_t mk = v, old = v;
+        if (vec) {
+          if constexpr (PRE) {
+            mk = pre_aux[tt];
+            old = pre_c[tt];
+          } else if (ex.beta != 0.f) {
+            old = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (!vec && n + e >= N) break;
+          float f = bf2f((bf16_t)v[e]);
+          if constexpr (EPI == F8_EPI_DRELU) {
+            const float a = vec ? bf2f((bf16_t)mk[e]) : bf2f(ex.aux[(size_t)m * ex.ldaux + n + e]);
+            if (!(a > 0.f)) f = 0.f;
+          }
+          if (ex.beta != 0.f)
+            f += ex.beta * (vec ? bf2f((bf16_t)old[e]) : bf2f(C[(size_t)m * ldc + n + e]));
+          v[e] = (short)f2bf(f);
+        }
+      }
       if (n + 8 <= N) {
         *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
       } else {
@@ -162,10 +233,10 @@ struct F8Epi {
           f[e] = bf2f((bf16_t)v[e]);
           amax = fmaxf(amax, fabsf(f[e]));
         }
-        int lo = f8::pack2_e4m3<false>(f[0] * s8, f[1] * s8, 0);
-        lo = f8::pack2_e4m3<true>(f[2] * s8, f[3] * s8, lo);
-        int hi = f8::pack2_e4m3<false>(f[4] * s8, f[5] * s8, 0);
-        hi = f8::pack2_e4m3<true>(f[6] * s8, f[7] * s8, hi);
+        int lo = f8::pack2_f8<CF, false>(f[0] * s8, f[1] * s8, 0);
+        lo = f8::pack2_f8<CF, true>(f[2] * s8, f[3] * s8, lo);
+        int hi = f8::pack2_f8<CF, false>(f[4] * s8, f[5] * s8, 0);
+        hi = f8::pack2_f8<CF, true>(f[6] * s8, f[7] * s8, hi);
         if (n + 8 <= N) {
           *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
         } else {
@@ -190,12 +261,14 @@ struct F8Epi {
   }
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
+// AF: format of A (0 e4m3, 1 e5m2: the gradient operand of a dgrad), B is
+// e4m3; CF: format of the optional C8 copy.
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int AF = 0, int CF = 0>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
     uint8_t* __restrict__ C8, const float* __restrict__ sc8, unsigned* __restrict__ amax_out,
-    int M, int N, int K, int lda, int ldb, int ldc, int ldc8) {
+    int M, int N, int K, int lda, int ldb, int ldc, int ldc8, F8Extra ex) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int A_BYTES = BM * BK8, B_BYTES = BN * BK8, SB = A_BYTES + B_BYTES;
@@ -257,8 +330,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0,
-                                                                     0, 127, 0, 127);
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], AF,
+                                                                     0, 0, 127, 0, 127);
     __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < nk) {
       if (kt + STAGES - 1 < nk) f8::wait_vmcnt<(STAGES - 2) * PT>();
@@ -278,11 +351,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   }
 
   f8::lds_barrier();
-  F8Epi<BM, BN, WM, WN, EPI>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8,
-                                  m0, n0, wid, lane, tid);
+  F8Epi<BM, BN, WM, WN, EPI, CF>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc,
+                                      ldc8, m0, n0, wid, lane, tid, ex);
 }
 
 // y8 = e4m3(x * scale[0]); amax_out = max|x| (both optional sides)
+template <int FMT>
 __global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict__ x,
                                                         uint8_t* __restrict__ y8, long long n,
                                                         const float* __restrict__ scale,
@@ -299,16 +373,16 @@ __global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict
         f[e] = bf2f((bf16_t)v[e]);
         amax = fmaxf(amax, fabsf(f[e]));
       }
-      int lo = f8::pack2_e4m3<false>(f[0] * s, f[1] * s, 0);
-      lo = f8::pack2_e4m3<true>(f[2] * s, f[3] * s, lo);
-      int hi = f8::pack2_e4m3<false>(f[4] * s, f[5] * s, 0);
-      hi = f8::pack2_e4m3<true>(f[6] * s, f[7] * s, hi);
+      int lo = f8::pack2_f8<FMT, false>(f[0] * s, f[1] * s, 0);
+      lo = f8::pack2_f8<FMT, true>(f[2] * s, f[3] * s, lo);
+      int hi = f8::pack2_f8<FMT, false>(f[4] * s, f[5] * s, 0);
+      hi = f8::pack2_f8<FMT, true>(f[6] * s, f[7] * s, hi);
       *reinterpret_cast<int2*>(y8 + i) = make_int2(lo, hi);
     } else {
       for (long long e = i; e < n; ++e) {
         const float f = bf2f(x[e]);
         amax = fmaxf(amax, fabsf(f));
-        const int w = f8::pack2_e4m3<false>(f * s, 0.f, 0);
+        const int w = f8::pack2_f8<FMT, false>(f * s, 0.f, 0);
         y8[e] = (uint8_t)(w & 0xff);
       }
     }
@@ -385,7 +459,7 @@ __global__ __launch_bounds__(256) void fp8_quant_multi_kernel(const QuantSegs se
 // One wave per slot, lane j reads (and clears) word j of the slot's spread.
 __global__ __launch_bounds__(256) void fp8_scale_update_kernel(float* __restrict__ scale,
                                                                unsigned* __restrict__ amax, int n,
-                                                               float margin_pow2) {
+                                                               float margin_pow2, float fmax) {
   static_assert(AMAX_SPREAD == 64, "one lane per spread word");
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= n) return;
@@ -395,7 +469,7 @@ __global__ __launch_bounds__(256) void fp8_scale_update_kernel(float* __restrict
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
   const float a = __uint_as_float(m);
-  if (lane == 0 && a > 0.f && isfinite(a)) scale[i] = E4M3_MAX / (a * margin_pow2);
+  if (lane == 0 && a > 0.f && isfinite(a)) scale[i] = fmax / (a * margin_pow2);
 }
 
 // e4m3 -> f32 (tests / debugging)
@@ -411,32 +485,32 @@ __global__ void fp8_dequant_kernel(const uint8_t* __restrict__ x8, float* __rest
 using namespace tdg;
 
 namespace {
-template <int BM, int BN, int WM, int WN, int ST, int EPI>
+template <int BM, int BN, int WM, int WN, int ST, int EPI, int AF = 0, int CF = 0>
 int launch_f8(const void* A, const void* B, void* C, const float* bias, const float* sa,
               const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
-              int lda, int ldb, int ldc, int ldc8, hipStream_t st) {
+              int lda, int ldb, int ldc, int ldc8, const F8Extra& ex, hipStream_t st) {
   constexpr int img = WM * WN * (BM / WM) * ((BN / WN) * 2 + 16) + 64;  // + amax scratch
   constexpr int lds = std::max(ST * (BM + BN) * BK8, img);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI>,
+    hipFuncSetAttribute((const void*)gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI>), dim3(tiles), dim3(WM * WN * 64),
-                     lds, st, (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C, bias, sa, sb,
-                     (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8);
+  hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF>), dim3(tiles),
+                     dim3(WM * WN * 64), lds, st, (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C,
+                     bias, sa, sb, (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
   return 0;
 }
 
 template <int EPI>
 int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, const float* sa,
              const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
-             int lda, int ldb, int ldc, int ldc8, hipStream_t st) {
+             int lda, int ldb, int ldc, int ldc8, const F8Extra& ex, hipStream_t st) {
 #define TDG_F8(ID, BM_, BN_, WM_, WN_, ST_) \
   case ID:                                 \
-    return launch_f8<BM_, BN_, WM_, WN_, ST_, EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
+    return launch_f8<BM_, BN_, WM_, WN_, ST_, EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
   switch (cfg) {
     TDG_F8(0, 128, 128, 2, 2, 2)
     TDG_F8(1, 128, 64, 2, 2, 3)
@@ -451,24 +525,42 @@ int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, 
 }
 }  // namespace
 
+// afmt / cfmt: formats of A and of the C8 copy (0 e4m3, 1 e5m2). The e5m2-A
+// backward GEMMs (ReLU-backward dgrad with an e5m2 copy of its output; the
+// plain dgrad accumulating into C) run on the 128x128 tile only.
 extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias,
                             const float* sa, const float* sb, void* C8, const float* sc8,
                             unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
-                            int ldc8, int epi, int cfg, hipStream_t st) {
+                            int ldc8, int epi, int cfg, int afmt, int cfmt, const void* aux,
+                            int ldaux, float beta, hipStream_t st) {
   if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
-  switch (epi) {
-    case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
-    case F8_EPI_BIAS: return tiles_f8<F8_EPI_BIAS>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
-    case F8_EPI_BIAS_RELU: return tiles_f8<F8_EPI_BIAS_RELU>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, st);
-    default: return -1;
+  const F8Extra ex{(const bf16_t*)aux, ldaux, beta};
+  if (afmt == 0 && cfmt == 0) {
+    switch (epi) {
+      case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      case F8_EPI_BIAS: return tiles_f8<F8_EPI_BIAS>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      case F8_EPI_BIAS_RELU: return tiles_f8<F8_EPI_BIAS_RELU>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      default: return -1;
+    }
   }
+  if (afmt == 1 && cfmt == 1) {
+    if (epi == F8_EPI_DRELU)
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    if (epi == F8_EPI_NONE)
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_NONE, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+  }
+  return -1;
 }
 
 extern "C" int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale,
-                             unsigned* amax, hipStream_t st) {
+                             unsigned* amax, int fmt, hipStream_t st) {
   const int blocks = (int)std::min<long long>(1024, (n / 8 + 255) / 256 + 1);
-  hipLaunchKernelGGL(fp8_quant_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x,
-                     (uint8_t*)y8, n, scale, amax);
+  if (fmt == 1)
+    hipLaunchKernelGGL(fp8_quant_kernel<1>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x,
+                       (uint8_t*)y8, n, scale, amax);
+  else
+    hipLaunchKernelGGL(fp8_quant_kernel<0>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x,
+                       (uint8_t*)y8, n, scale, amax);
   return 0;
 }
 
@@ -497,9 +589,9 @@ extern "C" int tdg_fp8_quant_multi(const void* const* x, void* const* y, const l
 }
 
 extern "C" int tdg_fp8_scale_update(float* scale, unsigned* amax, int n, float margin_pow2,
-                                    hipStream_t st) {
+                                    float fmax, hipStream_t st) {
   hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(cdiv(n, 4)), dim3(256), 0, st, scale, amax, n,
-                     margin_pow2);
+                     margin_pow2, fmax);
   return 0;
 }
 

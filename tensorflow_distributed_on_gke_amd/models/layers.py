@@ -699,6 +699,24 @@ class FFNBlockFn(torch.autograd.Function):
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
             _wgrad(rt, ds2, h, d, w2)
+            bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if rt.fp8 is not None else None
+            if bw is not None:
+                # fp8 backward: e5m2 gradients x e4m3 transposed weights on the
+                # block-scaled MFMA; the ReLU-backward dgrad also emits the e5m2
+                # copy of its output for the next dgrad, which accumulates the
+                # residual gradient already in dh (weight gradients stay bf16)
+                st = rt.fp8
+                gs, gh = bw
+                M = B * L
+                ds8 = fp8.quantize(ds2, st.gmeta, gs)
+                w2t8, s2t = st.weights.get(w2, transposed=True)
+                w1t8, s1t = st.weights.get(w1, transposed=True)
+                dpre = torch.empty(M, ff, dtype=ds2.dtype, device=ds2.device)
+                dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, dpre, relu_aux=h,
+                                           out8_slot=gh)
+                _wgrad(rt, dpre, x2, ff, w1, b1)
+                fp8.gemm_bf8_dgrad(dpre8, st.gmeta, gh, w1t8, st.meta, s1t, dh.view(M, d), beta=1.0)
+                return (dh.view(B, L, d),) + (None,) * 8
             if w2.compute_t is not None:  # NT layout against W2^T (ParamStore.add_transposed)
                 dpre = K.linear_dgrad_t(ds2, w2.compute_t, relu_aux=h)
             else:

@@ -11,8 +11,13 @@ scale the next forward will dequantise with.
 
 Forward: activation -> e4m3 (fp8_quant, or fused into the producing GEMM's
 epilogue), e4m3 x e4m3 GEMM on the block-scaled MFMA (csrc/kernels/fp8.hip),
-bf16 out. Backward and the optimizer stay bf16 / fp32 (the bf16 activations
-the fp8 GEMMs were fed are what the backward saves).
+bf16 out. Backward (`Fp8State(backward=True)`): the two FFN dgrads run as
+e5m2-gradient x e4m3-transposed-weight GEMMs (the ReLU-backward one emits the
+e5m2 copy of its output for the other, which accumulates the residual
+gradient); gradient scales live in a second, e5m2 `Fp8Meta`. Weight
+gradients, the attention backward and the optimizer stay bf16 / fp32.
+Measured on Transformer-big seq 512: 14.77-14.83 vs 14.85-14.99 ms/step with
+the FFN backward in bf16 (profiles/r3s2/fp8_backward_ab.txt).
 """
 from __future__ import annotations
 
@@ -25,15 +30,22 @@ from tensorflow_distributed_on_gke_amd.ops._ext import C
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
 
 FP8 = torch.float8_e4m3fn
+BF8 = torch.float8_e5m2  # gradient format of the fp8 backward
 E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
 AMAX_WORDS = 64 * 32  # per slot (csrc/include/tdg_common.h AMAX_WORDS)
 _CANDS = (0, 1, 2, 3, 4, 5, 8)
 _TUNED: Dict[tuple, int] = {}
 
 
 class Fp8Meta:
-    def __init__(self, device, capacity: int = 256, margin: int = 0):
+    """fmt 0: e4m3 slots (activations, weights); fmt 1: e5m2 (gradients)."""
+
+    def __init__(self, device, capacity: int = 256, margin: int = 0, fmt: int = 0):
         self.device = torch.device(device)
+        self.fmt = fmt
+        self.dtype = BF8 if fmt else FP8
+        self.fmax = E5M2_MAX if fmt else E4M3_MAX
         self.scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
         # [slot, 2048]: producers spread their atomics over 64 words, one per
         # 128-byte line (tdg_common.h AMAX_SPREAD / AMAX_STRIDE; the rest stay 0)
@@ -56,7 +68,7 @@ class Fp8Meta:
     def update(self) -> None:
         n = len(self.names)
         if n:
-            C().fp8_scale_update(self.scale[:n], self.amax[:n], float(2 ** self.margin))
+            C().fp8_scale_update(self.scale[:n], self.amax[:n], float(2 ** self.margin), self.fmax)
 
     def amax_values(self) -> torch.Tensor:
         return self.amax[: len(self.names)].view(torch.float32).amax(dim=1)
@@ -65,8 +77,8 @@ class Fp8Meta:
 def quantize(x: torch.Tensor, meta: Fp8Meta, i: int, out: Optional[torch.Tensor] = None,
              record: bool = True) -> torch.Tensor:
     if out is None:
-        out = torch.empty(x.shape, dtype=FP8, device=x.device)
-    C().fp8_quant(x.contiguous(), out, meta.s(i), meta.a(i) if record else None)
+        out = torch.empty(x.shape, dtype=meta.dtype, device=x.device)
+    C().fp8_quant(x.contiguous(), out, meta.s(i), meta.a(i) if record else None, meta.fmt)
     return out
 
 
@@ -90,7 +102,7 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
         C().gemm_fp8(a8, b8, y, bias, meta.s(ia), meta.s(ib), y8,
                      meta.s(out8_slot) if y8 is not None else None,
                      meta.a(out8_slot) if y8 is not None else None,
-                     M, N, Kd, a8.stride(0), b8.stride(0), N, N, epi, c)
+                     M, N, Kd, a8.stride(0), b8.stride(0), N, N, epi, c, 0, 0, None, 0, 0.0)
 
     if cfg is None:
         key = (M, N, Kd, epi, y8 is not None)
@@ -103,6 +115,24 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
             _TUNED[key] = cfg
     run(cfg)
     return y, y8
+
+
+def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8t, wmeta: Fp8Meta, iw: int,
+                   out: torch.Tensor, relu_aux: Optional[torch.Tensor] = None, beta: float = 0.0,
+                   out8_slot: Optional[int] = None) -> Optional[torch.Tensor]:
+    """Backward GEMM on the block-scaled MFMA: out[M,N] (=|+= beta) dequant(
+    g8[M,K] (e5m2 gradient) @ w8t[N,K]^T (e4m3 transposed weight)), bf16;
+    relu_aux: zero where relu_aux <= 0 (ReLU backward); out8_slot: also the
+    e5m2 copy of out in gmeta's slot (returned, amax recorded)."""
+    M, Kd = g8.shape
+    N = w8t.shape[0]
+    o8 = torch.empty(M, N, dtype=BF8, device=g8.device) if out8_slot is not None else None
+    C().gemm_fp8(g8, w8t, out, None, gmeta.s(ig), wmeta.s(iw), o8,
+                 gmeta.s(out8_slot) if o8 is not None else None,
+                 gmeta.a(out8_slot) if o8 is not None else None,
+                 M, N, Kd, g8.stride(0), w8t.stride(0), out.stride(0), N, 3 if relu_aux is not None else 0,
+                 0, 1, 1, relu_aux, relu_aux.stride(0) if relu_aux is not None else 0, beta)
+    return o8
 
 
 def choose_fp8(M: int, N: int, Kd: int) -> int:
@@ -142,23 +172,30 @@ class Fp8Weights:
         self.items: List[Tuple[object, torch.Tensor, int]] = []
         self.by_param: Dict[int, Tuple[torch.Tensor, int]] = {}
 
-    def add(self, param) -> Tuple[torch.Tensor, int]:
-        w8 = torch.empty(param.shape, dtype=FP8, device=self.meta.device)
-        slot = self.meta.slot("w:" + param.name)
-        self.items.append((param, w8, slot))
-        self.by_param[id(param)] = (w8, slot)
+    def add(self, param, transposed: bool = False) -> Tuple[torch.Tensor, int]:
+        """transposed: an e4m3 copy of param.compute_t (the [in, out] layout a
+        dgrad reads K-contiguous; ParamStore.add_transposed keeps it)."""
+        shape = (param.shape[1], param.shape[0]) if transposed else param.shape
+        w8 = torch.empty(shape, dtype=FP8, device=self.meta.device)
+        slot = self.meta.slot(("wt:" if transposed else "w:") + param.name)
+        self.items.append((param, w8, slot, transposed))
+        self.by_param[(id(param), transposed)] = (w8, slot)
         return w8, slot
 
-    def get(self, param) -> Tuple[torch.Tensor, int]:
-        return self.by_param[id(param)]
+    def get(self, param, transposed: bool = False) -> Tuple[torch.Tensor, int]:
+        return self.by_param[(id(param), transposed)]
+
+    def has(self, param, transposed: bool = False) -> bool:
+        return (id(param), transposed) in self.by_param
 
     def refresh(self) -> None:
         """All weight copies in one launch per 64 weights (fp8_quant_multi),
         each with its own scale and amax slot."""
         for c0 in range(0, len(self.items), 64):
             chunk = self.items[c0:c0 + 64]
-            C().fp8_quant_multi([p.compute for p, _, _ in chunk], [w8 for _, w8, _ in chunk],
-                                [slot for _, _, slot in chunk], self.meta.scale, self.meta.amax)
+            C().fp8_quant_multi([p.compute_t if t else p.compute for p, _, _, t in chunk],
+                                [w8 for _, w8, _, _ in chunk], [slot for _, _, slot, _ in chunk],
+                                self.meta.scale, self.meta.amax)
 
     def calibrate(self) -> None:
         """Initial weight scales from their actual amax."""
@@ -178,9 +215,17 @@ class Fp8State:
     own kernel. The attention output projections stay bf16: their input, the
     attention output, would need a separate quantisation pass."""
 
-    def __init__(self, model, margin: int = 0):
+    def __init__(self, model, margin: int = 0, backward: bool = True):
+
         self.meta = Fp8Meta(model.device, margin=margin)
         self.weights = Fp8Weights(self.meta)
+        # e5m2 gradients of the FFN backward (`backward`): ds (LayerNorm
+        # backward output) and the ReLU-backward dgrad's output, per layer
+        self.gmeta = Fp8Meta(model.device, margin=margin, fmt=1)
+        # first-step scale of the gradient slots (delayed scaling takes over
+        # after one step): 2^16 keeps |g| in [2^-32, 0.875] representable
+        self.gmeta.scale.fill_(65536.0)
+        self.ffn_bwd_slots: Dict[int, Tuple[int, int]] = {}
         self.ffn_slots: Dict[int, Tuple[int, int]] = {}
         # LayerNorms whose output is an fp8 GEMM input: they emit the e4m3 copy
         self.ln_slots: Dict[int, int] = {}
@@ -199,6 +244,13 @@ class Fp8State:
             self.ffn_slots[id(layer.ff1.w)] = (xs, hs)
             feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
             self.ln_slots[id(feeder.gamma)] = xs
+            if backward:
+                model.store.add_transposed(layer.ff1.w)
+                model.store.add_transposed(layer.ff2.w)
+                self.weights.add(layer.ff1.w, transposed=True)
+                self.weights.add(layer.ff2.w, transposed=True)
+                self.ffn_bwd_slots[id(layer.ff1.w)] = (self.gmeta.slot(f"gs:{id(layer)}"),
+                                                       self.gmeta.slot(f"gh:{id(layer)}"))
 
         def proj(w, feeder_ln) -> None:
             self.weights.add(w)
@@ -235,4 +287,5 @@ class Fp8State:
 
     def after_step(self) -> None:
         self.meta.update()
+        self.gmeta.update()
         self.weights.refresh()

@@ -123,13 +123,13 @@ class TrainStep:
         ts = [self.model.store.flat, self.opt.m, self.opt.v, self.opt.step, self.rt.ctr,
               self.accum, self.last]
         if self.fp8 is not None:
-            ts += [self.fp8.meta.scale]
+            ts += [self.fp8.meta.scale, self.fp8.gmeta.scale]
         return ts
 
     def snapshot(self):
         st = [t.clone() for t in self._state()]
         if self.fp8 is not None:
-            st.append(self.fp8.meta.amax.clone())
+            st += [self.fp8.meta.amax.clone(), self.fp8.gmeta.amax.clone()]
         return st
 
     def restore(self, st) -> None:
@@ -141,7 +141,8 @@ class TrainStep:
         self.model.store.refresh_compute()
         if self.fp8 is not None:
             self.fp8.weights.refresh()  # e4m3 copies with the restored scales
-            self.fp8.meta.amax.copy_(st[-1])
+            self.fp8.meta.amax.copy_(st[-2])
+            self.fp8.gmeta.amax.copy_(st[-1])
 
     def eager(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         self.model.loss_and_backward(src, tgt, self.rt, self.workers, accum=self.accum,

@@ -1,6 +1,8 @@
-"""FP8 (OCP e4m3) path: quantisation vs torch's float8_e4m3fn, the block-scaled
-MFMA GEMM vs an fp32 reference of the dequantised operands, the fused fp8
-epilogue output, delayed scaling, and an fp8 training run vs bf16."""
+"""FP8 (OCP e4m3 / e5m2) path: quantisation vs torch's float8 types, the
+block-scaled MFMA GEMM (forward, and the e5m2-gradient backward GEMMs with the
+ReLU-backward mask and beta accumulation) vs an fp32 reference of the
+dequantised operands, the fused fp8 epilogue output, delayed scaling, and an
+fp8 training run (forward + FFN backward in fp8) vs bf16."""
 import pytest
 import torch
 
@@ -49,6 +51,48 @@ def test_gemm_fp8(M, N, K, epi):
         want8 = (y.float() * 4.0).clamp(-448, 448).to(torch.float8_e4m3fn)
         assert (y8.view(torch.uint8) == want8.view(torch.uint8)).float().mean().item() > 0.999
     assert abs(meta.amax_values()[io].item() - y.float().abs().max().item()) <= 1e-3 * y.float().abs().max().item()
+
+
+def test_quantize_matches_torch_e5m2():
+    meta = F.Fp8Meta(DEV, fmt=1)
+    i = meta.slot("g")
+    meta.scale[i] = 4096.0
+    x = (torch.randn(1000, 96, device=DEV) * 1e-3).bfloat16()
+    x[0, 0] = 30.0  # saturates at 57344 after scaling
+    x8 = F.quantize(x, meta, i)
+    assert x8.dtype == torch.float8_e5m2
+    ref = (x.float() * 4096.0).clamp(-57344, 57344).to(torch.float8_e5m2)
+    assert (x8.view(torch.uint8) == ref.view(torch.uint8)).float().mean().item() > 0.999
+    meta.update()
+    assert abs(meta.scale[i].item() - 57344.0 / 30.0) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128)])
+@pytest.mark.parametrize("relu,beta", [(True, 0.0), (False, 1.0)])
+def test_gemm_bf8_dgrad(M, N, K, relu, beta):
+    """out (=|+= beta) dequant(g8 e5m2 @ w8t e4m3^T), ReLU-backward mask, and
+    the e5m2 copy of the output, against an fp32 reference."""
+    torch.manual_seed(1)
+    wm, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
+    iw, ig, io = wm.slot("w"), gm.slot("g"), gm.slot("o")
+    wm.scale[iw], gm.scale[ig], gm.scale[io] = 900.0, 2.0 ** 20, 2.0 ** 10
+    g = (torch.randn(M, K, device=DEV) * 1e-3).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    aux = torch.randn(M, N, device=DEV).bfloat16() if relu else None
+    out = torch.randn(M, N, device=DEV).bfloat16()
+    g8, w8 = F.quantize(g, gm, ig), F.quantize(w, wm, iw)
+    ref = (g8.float() / 2.0 ** 20) @ (w8.float() / 900.0).t()
+    if relu:
+        ref = ref * (aux.float() > 0)
+    ref = ref + beta * out.float()
+    o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux=aux, beta=beta,
+                          out8_slot=io if relu else None)
+    err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+    assert err < 1e-2, err
+    if relu:
+        want = (out.float() * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
+        assert (o8.view(torch.uint8) == want.view(torch.uint8)).float().mean().item() > 0.999
+        assert abs(gm.amax_values()[io].item() - out.float().abs().max().item()) <= 1e-3 * out.float().abs().max().item()
 
 
 def test_fp8_training_tracks_bf16():
