@@ -54,7 +54,8 @@ def main() -> None:
     ap.add_argument("--defer-wgrad", type=int, default=-1,
                     help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: FFN + attention-input forward GEMMs in e4m3 with delayed scaling "
+                    help="fp8: FFN + attention-input forward GEMMs and the attention forward in "
+                         "e4m3, FFN dgrads e5m2 x e4m3, delayed scaling "
                          "(BASELINE config 5)")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     ap.add_argument("--force-dp", type=int, default=0,
@@ -148,7 +149,8 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": ("fp32 (CPU reference ops)" if dev.type != "cuda" else "bf16") if args.dtype == "bf16" else
-                     "fp8 (e4m3 forward GEMMs of the FFNs and attention input projections, bf16 elsewhere)",
+                     "fp8 (e4m3 forward GEMMs of the FFNs and attention input projections, e4m3 "
+                     "attention forward, e5m2 x e4m3 FFN dgrads; bf16 elsewhere)",
             "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
                 "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "
