@@ -32,7 +32,7 @@ int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float
                const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, int accumulate, int skip_reduce,
-               hipStream_t st);
+               int rpb, hipStream_t st);
 int tdg_reduce_partials_multi(const float* const* parts, float* const* outs, const int* nparts,
                               int G, int N, float beta, hipStream_t st);
 int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe, void* out, int M,
@@ -428,7 +428,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
             const Tensor& gamma, const Tensor& dh, const optional<Tensor>& ds,
             const optional<Tensor>& dres, const Tensor& dgamma, const Tensor& dbeta,
             const optional<Tensor>& dbias, const Tensor& ws, double p, int64_t seed,
-            const optional<Tensor>& ctr, int64_t site, bool accumulate, bool skip_reduce) {
+            const optional<Tensor>& ctr, int64_t site, bool accumulate, bool skip_reduce,
+            int64_t rpb) {
   check_bf16(dy, "dy");
   check_contig(dy, "dy");
   const int64_t D = dy.size(-1), M = dy.numel() / D;
@@ -453,7 +454,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
     TORCH_CHECK(dbias->numel() == D && ds.has_value(), "ln_bwd: dbias needs ds");
   }
   check_f32(ws, "ws");
-  TORCH_CHECK(ws.numel() >= 3 * ((M + 7) / 8) * D, "ln_bwd: workspace too small");
+  TORCH_CHECK(rpb == 16 || rpb == 32 || rpb == 64, "ln_bwd: rows per block 16 / 32 / 64");
+  TORCH_CHECK(ws.numel() >= 3 * ((M + rpb - 1) / rpb) * D, "ln_bwd: workspace too small");
   c10::DeviceGuard g(dy.device());
   const int rc = tdg_ln_bwd(
       dy.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
@@ -461,7 +463,7 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
       dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(),
       dbeta.data_ptr<float>(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
       ws.data_ptr<float>(), (int)M, (int)D, (float)p, (uint64_t)seed, ctr_ptr(ctr),
-      (uint64_t)site, accumulate, skip_reduce, stream_of(dy));
+      (uint64_t)site, accumulate, skip_reduce, (int)rpb, stream_of(dy));
   check_err(rc, "tdg ln_bwd");
 }
 

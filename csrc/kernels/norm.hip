@@ -95,7 +95,7 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
     const long long* ctr, uint64_t site, int iters) {
   constexpr int VEC = D / 64;
-  __shared__ float red[3][NWV][D];
+  __shared__ float red[NWV][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float ag[VEC], ab[VEC], as[VEC];
 #pragma unroll
@@ -163,25 +163,22 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     dh.store_row(dh_out + rbase, lane, wdh);
   }
   }  // row groups
+  // cross-wave fold, one quantity at a time (NWV x D floats of LDS: 8 waves
+  // x D = 1024 stay at 32 KB)
+  float* const parts[3] = {part_g, part_b, part_s};
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    const int col = RowMap<VEC>::col(lane, i);
-    red[0][w][col] = ag[i];
-    red[1][w][col] = ab[i];
-    red[2][w][col] = as[i];
-  }
-  __syncthreads();
-  for (int col = threadIdx.x; col < D; col += NWV * 64) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int q = 0; q < 3; ++q) {
+    if (q == 2 && !part_s) break;
 #pragma unroll
-    for (int k = 0; k < NWV; ++k) {
-      a0 += red[0][k][col];
-      a1 += red[1][k][col];
-      a2 += red[2][k][col];
+    for (int i = 0; i < VEC; ++i) red[w][RowMap<VEC>::col(lane, i)] = q == 0 ? ag[i] : q == 1 ? ab[i] : as[i];
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += NWV * 64) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < NWV; ++k) a += red[k][col];
+      parts[q][(size_t)blockIdx.x * D + col] = a;
     }
-    part_g[(size_t)blockIdx.x * D + col] = a0;
-    part_b[(size_t)blockIdx.x * D + col] = a1;
-    if (part_s) part_s[(size_t)blockIdx.x * D + col] = a2;
+    __syncthreads();
   }
 }
 
@@ -206,19 +203,25 @@ template <int D>
 void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
-              int accumulate, int skip_reduce, hipStream_t st) {
+              int accumulate, int skip_reduce, int rpb, hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
-  // 16 rows per block whatever the variant (kernels.py ln_bwd_nparts)
-  // (2 or 1 rows per wave on 8 or 16 waves per block measured within +-10 %)
-  constexpr int RPW = D >= 1024 ? 2 : 4, NWV = 4, rpb = 16;
+  // rpb rows per block (kernels.py ln_bwd_nparts): 16 on 4 waves, 32 / 64 on
+  // 8 waves (fewer partial rows for the fold); RPW rows per wave per pass
+  constexpr int RPW = D >= 1024 ? 2 : 4;
   const int nb = cdiv(M, rpb);
   float* pg = ws;
   float* pb = ws + (size_t)nb * D;
   float* ps = dbias ? ws + 2 * (size_t)nb * D : nullptr;
-  hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, NWV>), dim3(nb), dim3(NWV * 64), 0, st,
-                     (const bf16_t*)dy, (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh,
-                     (bf16_t*)ds, (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
-                     rpb / (RPW * NWV));
+  if (rpb <= 16)
+    hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
+                       (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
+                       max(1, rpb / (RPW * 4)));
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 8>), dim3(nb), dim3(512), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
+                       (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
+                       max(1, rpb / (RPW * 8)));
   if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
@@ -244,15 +247,16 @@ extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, cons
 #undef TDG_LN_F
 }
 
-// ws must hold 3 * ceil(M/8) * D floats.
+// ws must hold 3 * ceil(M / rpb) * D floats.
 extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                           const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,
                           uint64_t seed, const long long* ctr, uint64_t site, int accumulate,
-                          int skip_reduce, hipStream_t st) {
+                          int skip_reduce, int rpb, hipStream_t st) {
+  if (rpb != 16 && rpb != 32 && rpb != 64) return -2;
 #define TDG_LN_B(DD)                                                                              \
   ln_bwd_d<DD>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, \
-               ctr, site, accumulate, skip_reduce, st);                                           \
+               ctr, site, accumulate, skip_reduce, rpb, st);                                      \
   return 0;
   switch (D) {
     case 128: TDG_LN_B(128)
@@ -298,6 +302,49 @@ __global__ __launch_bounds__(256) void reduce_partials_multi_kernel(MultiReduce 
     out[col] = (beta != 0.f ? beta * out[col] : 0.f) + t;
   }
 }
+// N % 4 == 0: 16-byte loads, a 64-column (256-byte) strip per block, 16 row
+// groups; every partial row is read in whole 128-byte lines
+__global__ __launch_bounds__(256) void reduce_partials_multi4_kernel(MultiReduce mr, int N,
+                                                                     float beta) {
+  __shared__ float4 red[16][17];
+  const float* part = mr.part[blockIdx.y];
+  float* out = mr.out[blockIdx.y];
+  const int P = mr.nparts[blockIdx.y];
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + c * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < N) {
+#pragma unroll 8
+    for (int q = g; q < P; q += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)q * N + col);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      t.x += red[k][c].x;
+      t.y += red[k][c].y;
+      t.z += red[k][c].z;
+      t.w += red[k][c].w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + col);
+    if (beta != 0.f) {
+      const float4 b = *o;
+      t.x += beta * b.x;
+      t.y += beta * b.y;
+      t.z += beta * b.z;
+      t.w += beta * b.w;
+    }
+    *o = t;
+  }
+}
 }  // namespace tdg
 
 extern "C" int tdg_reduce_partials_multi(const float* const* parts, float* const* outs,
@@ -310,7 +357,15 @@ extern "C" int tdg_reduce_partials_multi(const float* const* parts, float* const
     mr.out[i] = outs[i];
     mr.nparts[i] = nparts[i];
   }
-  hipLaunchKernelGGL(reduce_partials_multi_kernel, dim3(cdiv(N, 16), G), dim3(256), 0, st, mr, N,
-                     beta);
+  bool al = N % 4 == 0;  // float4 path: every base pointer 16-byte aligned
+  for (int i = 0; i < G; ++i)
+    al = al && (reinterpret_cast<uintptr_t>(parts[i]) % 16 == 0) &&
+         (reinterpret_cast<uintptr_t>(outs[i]) % 16 == 0);
+  if (al)
+    hipLaunchKernelGGL(reduce_partials_multi4_kernel, dim3(cdiv(N, 64), G), dim3(256), 0, st, mr,
+                       N, beta);
+  else
+    hipLaunchKernelGGL(reduce_partials_multi_kernel, dim3(cdiv(N, 16), G), dim3(256), 0, st, mr, N,
+                       beta);
   return 0;
 }

@@ -396,9 +396,22 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
     return y, h, mean, rstd
 
 
+# LayerNorm-backward rows per workgroup (norm.hip ln_bwd_d): 16 on 4 waves,
+# 32 / 64 on 8 waves -- fewer dgamma / dbeta partial rows for the fold.
+# Measured (profiles/r3s2/ln_rpb.txt): 32 for D <= 512 (base step 5.00-5.02 vs
+# 5.02-5.05 ms, LN backward 308 vs 321 us + fold 10.6 vs 20.4 us), 16 for
+# D = 1024 (big 13.14-13.19 vs 13.20-13.22 ms); 64 loses 3.5 % (two serial
+# row passes). TDG_LN_BWD_RPB overrides.
+LN_BWD_RPB = int(os.environ.get("TDG_LN_BWD_RPB", "0"))
+
+
+def ln_bwd_rpb(D: int) -> int:
+    return LN_BWD_RPB or (32 if D <= 512 else 16)
+
+
 def ln_bwd_nparts(M: int, D: int) -> int:
-    """Partial-sum rows ln_bwd writes (norm.hip ln_bwd_d: 16 rows per block)."""
-    return math.ceil(M / 16)
+    """Partial-sum rows ln_bwd writes (one per workgroup)."""
+    return math.ceil(M / ln_bwd_rpb(D))
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
@@ -412,11 +425,11 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
     need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
     ds = torch.empty_like(dy) if need_ds else None
     if defer is None:
-        ws = workspace("ln_bwd", 3 * math.ceil(M / 8) * D, dy.device)
+        ws = workspace("ln_bwd", 3 * ln_bwd_nparts(M, D) * D, dy.device)
     else:  # partials must survive until the fold: one workspace per site
-        ws = workspace(f"ln_bwd_part_{site}", 3 * math.ceil(M / 8) * D, dy.device)
+        ws = workspace(f"ln_bwd_part_{site}", 3 * ln_bwd_nparts(M, D) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
-               accumulate, defer is not None)
+               accumulate, defer is not None, ln_bwd_rpb(D))
     if defer is not None:
         nb = ln_bwd_nparts(M, D)
         outs = [dgamma, dbeta] + ([dbias] if dbias is not None else [])

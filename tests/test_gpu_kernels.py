@@ -332,7 +332,9 @@ def test_attention_probs():
 # --------------------------------------------------------------------------- layernorm
 @pytest.mark.parametrize("D", [128, 512, 1024])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_add_ln_fwd_bwd(D, p):
+@pytest.mark.parametrize("rpb", [16, 32, 64])
+def test_add_ln_fwd_bwd(D, p, rpb, monkeypatch):
+    monkeypatch.setattr(kk, "LN_BWD_RPB", rpb)  # rows per backward workgroup
     M = 300
     seed, site = 1234, 7
     ctr = torch.tensor([5], dtype=torch.int64)
@@ -372,6 +374,25 @@ def test_add_ln_fwd_bwd(D, p):
     kk.reduce_partials_multi(defer)
     for got, want in ((dg2, dg), (db2, db), (dbias2, dbias)):
         torch.testing.assert_close(got, want + 2.0, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,off", [(512, 0), (512, 1), (100, 0), (36, 0)])
+def test_reduce_partials_multi(N, off):
+    """Deferred column folds: float4 strips (N % 4 == 0, 16-byte aligned) and
+    the scalar kernel (misaligned output view, N % 4 != 0 not used by LN but
+    N = 36 is a partial strip), plain and accumulating."""
+    g = torch.Generator().manual_seed(N + off)
+    items, want = [], []
+    for i, P in enumerate((7, 130, 513)):
+        part = torch.randn(P * N, generator=g).to(DEV)
+        buf = torch.randn(N + off, generator=g).to(DEV)
+        out = buf[off:]
+        beta = 1.0 if i == 1 else 0.0
+        want.append(part.view(P, N).double().sum(0).float() + (out.clone() if beta else 0))
+        items.append((part, out, P, N, beta))
+    kk.reduce_partials_multi(items)
+    for (_, out, _, _, _), w in zip(items, want):
+        torch.testing.assert_close(out, w, rtol=1e-5, atol=1e-4)
 
 
 # --------------------------------------------------------------------------- embedding
