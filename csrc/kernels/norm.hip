@@ -18,6 +18,43 @@
 
 namespace tdg {
 
+// e4m3 copy of one LayerNorm output row (delayed per-tensor scale s8) for an
+// fp8 GEMM; the row's |y| max folded into am.
+template <int D>
+__device__ __forceinline__ void ln_row_y8(const RowVec<D / 64>& o, float s8, uint8_t* __restrict__ y8,
+                                          size_t rbase, int lane, float& am) {
+  constexpr int VEC = D / 64;
+  int w[(VEC + 3) / 4];
+#pragma unroll
+  for (int i = 0; i < (VEC + 3) / 4; ++i) w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < VEC; i += 2) {
+    const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
+    am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
+    if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
+    else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+  }
+  uint8_t* dst = y8 + rbase + lane * RowMap<VEC>::W;
+  if constexpr (VEC == 2) {
+    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
+  } else if constexpr (VEC == 4) {
+    *reinterpret_cast<int*>(dst) = w[0];
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC / 8; ++i)
+      *reinterpret_cast<int2*>(dst + 512 * i) = make_int2(w[2 * i], w[2 * i + 1]);
+  }
+}
+
+// block-wide |y| max of the e4m3 copy -> one atomic per block (spread slots)
+__device__ __forceinline__ void ln_amax_flush(float am, float* red8, unsigned* amax8) {
+  am = wave_max(am);
+  if ((threadIdx.x & 63) == 0) red8[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0 && amax8)
+    atomic_amax(amax_word(amax8, blockIdx.x), fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
+}
+
 // RPW rows per wave (4 waves per block): the loads of all of a wave's rows
 // are issued before the first row is reduced, so a row's stores overlap the
 // next rows' loads still in flight.
@@ -48,38 +85,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     RowVec<VEC> o;
     ln_row_fwd<D>(h[k], t[k], s != nullptr, rbase, row, lane, gamma, beta, y, hsave, mean_out,
                   rstd_out, p, thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t));
-    if (y8) {  // fused e4m3 copy of y for an fp8 GEMM (delayed per-tensor scale)
-      const float s8 = s8p[0];
-      int w[(VEC + 3) / 4];
-#pragma unroll
-      for (int i = 0; i < (VEC + 3) / 4; ++i) w[i] = 0;
-#pragma unroll
-      for (int i = 0; i < VEC; i += 2) {
-        const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
-        am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
-        if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
-        else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
-      }
-      uint8_t* dst = y8 + rbase + lane * RowMap<VEC>::W;
-      if constexpr (VEC == 2) {
-        *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
-      } else if constexpr (VEC == 4) {
-        *reinterpret_cast<int*>(dst) = w[0];
-      } else {
-#pragma unroll
-        for (int i = 0; i < VEC / 8; ++i)
-          *reinterpret_cast<int2*>(dst + 512 * i) = make_int2(w[2 * i], w[2 * i + 1]);
-      }
-    }
+    if (y8) ln_row_y8<D>(o, s8p[0], y8, rbase, lane, am);
   }
-  if (y8) {
-    am = wave_max(am);
-    if (lane == 0) red8[threadIdx.x >> 6] = am;
-    __syncthreads();
-    if (threadIdx.x == 0 && amax8)
-      atomic_amax(amax_word(amax8, blockIdx.x),
-                  fmaxf(fmaxf(red8[0], red8[1]), fmaxf(red8[2], red8[3])));
-  }
+  if (y8) ln_amax_flush(am, red8, amax8);
 }
 
 // RPW rows per wave, 4 waves (4*RPW rows) per 256-thread block; all loads of
@@ -194,7 +202,9 @@ void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* bet
               unsigned* amax8, hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
   // one row per wave measured best with dropout (2 rows: 8.1 vs 8.2 us
-  // without, 11.1 vs 9.3 us with, D = 1024 x 8192 rows)
+  // without, 11.1 vs 9.3 us with, D = 1024 x 8192 rows); a grid-strided
+  // variant (fewer waves, each loading its next row while it reduces and
+  // stores the current one) lost 2-9 us per call (profiles/r3s2/ln_fwd_strided.txt)
   hipLaunchKernelGGL((ln_fwd_kernel<D, 1>), dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)s, gamma, beta, (bf16_t*)y, (bf16_t*)hsave, mean, rstd, M, p,
                      thresh, seed, ctr, site, eps, (uint8_t*)y8, s8, amax8);
