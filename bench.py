@@ -99,7 +99,7 @@ def main() -> None:
     dp_select = None
     if use_graph and ddp is not None and ddp.active:
         # segmented graph or eager step, whichever measures faster on this node
-        # (every rank takes the same decision; TDG_DP_AUTOSELECT=0: graph)
+        # (every rank takes the same decision; train.step.DP_AUTOSELECT = False: graph)
         dp_select = step.choose_dp_mode(*batches[0])
         use_graph = int(step.captured)
     elif use_graph:

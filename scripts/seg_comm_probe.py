@@ -17,7 +17,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29613", RANK="0", WORLD_SIZE="1",
-                 LOCAL_RANK="0", TDG_DP_AUTOSELECT="0").items():
+                 LOCAL_RANK="0").items():
     os.environ.setdefault(k, v)
 
 import torch  # noqa: E402

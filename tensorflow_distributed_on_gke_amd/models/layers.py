@@ -117,7 +117,7 @@ class WgradQueue:
     long-K GEMM per layer (split-K slabs + a reduce kernel, 64x64 tiles to
     fill the chip) all of them run as ONE ragged launch of 256x256 whole-K
     tiles (ops.kernels.wgrad_ragged: 5 shapes, 62 problems, ~730 tiles for
-    Transformer-base; bias gradients fused), or, with TDG_WGRAD_RAGGED=0, one
+    Transformer-base; bias gradients fused), or, with RAGGED_WGRAD = False, one
     grouped launch per shape (ops.kernels.wgrad_grouped) plus column sums.
     The data-parallel grad_ready notifications follow in backward order."""
 
