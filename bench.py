@@ -5,7 +5,9 @@ synthetic (source, target) pairs of length 128, bf16 compute, synchronous data
 parallelism over RCCL on N MI355X GPUs (one process per GPU).
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    (N > 1: starts its own N ranks, one per GPU, when no launcher set
+    WORLD_SIZE; under python -m torch.distributed.run --nproc-per-node N it
+    is one of the N ranks. A world that is not N exits non-zero.)
 
 A timed step is the full training step: forward, masked cross-entropy,
 backward, bucketed gradient all-reduce, Adam update. Weak scaling: the local
@@ -37,6 +39,33 @@ METRIC = "tokens/sec (whole node), Transformer-base en-pt at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
 
 
+def self_launch(n: int) -> int:
+    """Spawn `n` ranks of this script (one per GPU) and return their exit code.
+
+    Runs BEFORE anything touches the GPU in this parent: children are plain
+    subprocesses (never exec), each binds GPU LOCAL_RANK; the first child to
+    fail takes the others down (cluster/launch.py). Counting devices does not
+    initialise HIP. With fewer GPUs than ranks the request is refused (exit 2)
+    unless TDG_DIST_BACKEND=gloo asks for a one-GPU rehearsal; on a host with
+    no GPU the ranks run the CPU reference ops over gloo.
+    """
+    import socket
+
+    from tensorflow_distributed_on_gke_amd.cluster import launch, rendezvous
+
+    ngpu = torch.cuda.device_count()
+    if 0 < ngpu < n and os.environ.get("TDG_DIST_BACKEND") != "gloo":
+        print(f"bench.py: --gpus {n} requested but only {ngpu} GPU(s) are visible; refusing to "
+              f"measure fewer ranks (set TDG_DIST_BACKEND=gloo for a shared-GPU rehearsal)",
+              file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    spec = rendezvous.ClusterSpec(0, 1, ["127.0.0.1"], "127.0.0.1", port)
+    return launch.launch([os.path.abspath(__file__)] + sys.argv[1:], n, spec)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,10 +91,18 @@ def main() -> None:
                     help="1: run the RCCL data-parallel path even with one rank (testing)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` with no launcher: start the N ranks here
+        sys.exit(self_launch(args.gpus))
+
     info = tdist.init_distributed(force=bool(args.force_dp))
     world = info.world
-    if world != args.gpus and info.rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        # never print a one-GPU number under an N-GPU request
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+              file=sys.stderr, flush=True)
+        tdist.shutdown()
+        sys.exit(3)
     dev = info.device
     cfg = model_config(args.preset, max_src_len=max(1000, args.seq_len), max_tgt_len=max(1000, args.seq_len))
     model = Transformer(cfg).build(dev, seed=args.seed)

@@ -35,3 +35,30 @@ def test_bench_two_ranks_json_contract():
     # whole-job tokens/s: global batch x (src + tgt) tokens per step / step time
     expect = 8 * (16 + 16) / (d["ms_per_step"] / 1000.0)
     assert abs(d["value"] - expect) / expect < 0.01
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its own two ranks
+    (here over gloo on CPU) and prints one dp2 line."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--preset", "tiny", "--local-batch", "4", "--seq-len", "16"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 8
+
+
+def test_bench_rejects_world_mismatch():
+    """A launcher world that differs from --gpus is an error, not a warning."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--preset", "tiny", "--local-batch", "2", "--seq-len", "8"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
