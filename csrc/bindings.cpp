@@ -361,6 +361,14 @@ void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
 void check_f8(const Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.element_size() == 1, n, " must be a 1-byte (fp8 e4m3) GPU tensor");
 }
+// fmt 0: e4m3 (float8_e4m3fn), 1: e5m2 (float8_e5m2); raw uint8 buffers are
+// accepted as untyped storage, a float8 dtype of the other format is not
+void check_f8_fmt(const Tensor& t, int64_t fmt, const char* n) {
+  check_f8(t, n);
+  const auto st = t.scalar_type();
+  TORCH_CHECK(st == at::kByte || st == (fmt ? at::kFloat8_e5m2 : at::kFloat8_e4m3fn), n,
+              " has dtype ", st, " but the format argument says ", fmt ? "e5m2" : "e4m3");
+}
 unsigned* amax_ptr(const optional<Tensor>& t) {
   if (!t.has_value()) return nullptr;
   TORCH_CHECK(t->is_cuda() && t->element_size() == 4 && t->numel() >= 2048,
@@ -405,7 +413,7 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
       TORCH_CHECK((*t)->numel() == M, "ln: mean/rstd shape");
     }
   if (y8.has_value()) {
-    check_f8(*y8, "y8");
+    check_f8_fmt(*y8, 0, "y8");
     TORCH_CHECK(y8->numel() == x.numel() && y8->is_contiguous() && s8.has_value(), "ln: y8");
     check_f32(*s8, "s8");
   }
@@ -685,8 +693,8 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<
               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldc8, int64_t epi,
               int64_t cfg, int64_t afmt, int64_t cfmt, const optional<Tensor>& aux, int64_t ldaux,
               double beta) {
-  check_f8(A, "A8");
-  check_f8(B, "B8");
+  check_f8_fmt(A, afmt, "A8");
+  check_f8_fmt(B, 0, "B8");
   check_bf16(C, "C");
   check_f32(sa, "sa");
   check_f32(sb, "sb");
@@ -694,13 +702,16 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<
   TORCH_CHECK(A.numel() >= (M - 1) * lda + K && B.numel() >= (N - 1) * ldb + K, "gemm_fp8: A/B extent");
   TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc % 8 == 0, "gemm_fp8: C extent / ldc");
   if (bias.has_value()) check_f32(*bias, "bias");
-  TORCH_CHECK(epi == 0 || epi == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
-  TORCH_CHECK(epi != 3 || (aux.has_value() && aux->numel() >= (M - 1) * ldaux + N),
+  const int64_t epi_id = epi & 15;  // (flag 16: C = dequant(C8))
+  TORCH_CHECK((epi & ~int64_t(31)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
+  TORCH_CHECK(!(epi & 16) || C8.has_value(), "gemm_fp8: C = dequant(C8) needs C8");
+  TORCH_CHECK(epi_id == 0 || epi_id == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
+  TORCH_CHECK(epi_id != 3 || (aux.has_value() && aux->numel() >= (M - 1) * ldaux + N),
               "gemm_fp8: the ReLU-backward epilogue needs aux [M, >= N]");
   if (aux.has_value()) check_bf16(*aux, "aux");
   TORCH_CHECK((afmt == 0 || afmt == 1) && (cfmt == 0 || cfmt == 1), "gemm_fp8: formats are 0 / 1");
   if (C8.has_value()) {
-    check_f8(*C8, "C8");
+    check_f8_fmt(*C8, cfmt, "C8");
     TORCH_CHECK(sc8.has_value() && C8->numel() >= (M - 1) * ldc8 + N && ldc8 % 8 == 0, "gemm_fp8: C8");
   }
   c10::DeviceGuard g(A.device());
@@ -718,7 +729,8 @@ void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
                const optional<Tensor>& amax, int64_t fmt) {
   check_bf16(x, "x");
   check_contig(x, "x");
-  check_f8(y8, "y8");
+  check_f8_fmt(y8, fmt, "y8");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fp8_quant: format is 0 / 1");
   TORCH_CHECK(y8.numel() >= x.numel() && y8.is_contiguous(), "fp8_quant: y8");
   check_f32(scale, "scale");
   c10::DeviceGuard g(x.device());
@@ -740,7 +752,7 @@ void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& y
   for (int i = 0; i < n; ++i) {
     check_bf16(xs[i], "x");
     check_contig(xs[i], "x");
-    check_f8(ys[i], "y8");
+    check_f8_fmt(ys[i], 0, "y8");
     TORCH_CHECK(ys[i].numel() >= xs[i].numel() && ys[i].is_contiguous(), "fp8_quant_multi: y8");
     TORCH_CHECK(xs[i].device() == scale.device() && ys[i].device() == scale.device(),
                 "fp8_quant_multi: one device");
@@ -765,7 +777,7 @@ void fp8_scale_update(const Tensor& scale, const Tensor& amax, double margin_pow
 }
 
 void fp8_dequant(const Tensor& x8, const Tensor& y, double inv_scale) {
-  check_f8(x8, "x8");
+  check_f8_fmt(x8, 0, "x8");
   check_f32(y, "y");
   TORCH_CHECK(y.numel() == x8.numel(), "fp8_dequant: sizes");
   c10::DeviceGuard g(x8.device());

@@ -108,6 +108,25 @@ __device__ __forceinline__ int pack2_e5m2(float a, float b, int old) {
   b = fminf(fmaxf(b, -E5M2_MAX), E5M2_MAX);
   return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
 }
+// byte `sel` (0..3) of a packed word, decoded (FMT 0: e4m3, 1: e5m2)
+template <int FMT>
+__device__ __forceinline__ float unpack_f8(int w, int sel) {
+  if constexpr (FMT == 0) {
+    switch (sel) {
+      case 0: return __builtin_amdgcn_cvt_f32_fp8(w, 0);
+      case 1: return __builtin_amdgcn_cvt_f32_fp8(w, 1);
+      case 2: return __builtin_amdgcn_cvt_f32_fp8(w, 2);
+      default: return __builtin_amdgcn_cvt_f32_fp8(w, 3);
+    }
+  } else {
+    switch (sel) {
+      case 0: return __builtin_amdgcn_cvt_f32_bf8(w, 0);
+      case 1: return __builtin_amdgcn_cvt_f32_bf8(w, 1);
+      case 2: return __builtin_amdgcn_cvt_f32_bf8(w, 2);
+      default: return __builtin_amdgcn_cvt_f32_bf8(w, 3);
+    }
+  }
+}
 // FMT 0: e4m3, 1: e5m2
 template <int FMT, bool HI>
 __device__ __forceinline__ int pack2_f8(float a, float b, int old) {
@@ -118,6 +137,8 @@ __device__ __forceinline__ int pack2_f8(float a, float b, int old) {
 }  // namespace f8
 
 enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2, F8_EPI_DRELU = 3 };
+// flag on top of the epilogue id: C = dequant(C8) (needs C8)
+constexpr int F8_EPI_CDEQ = 16;
 
 // Backward-GEMM extras: the ReLU mask operand (F8_EPI_DRELU: out = 0 where
 // aux <= 0) and C = alpha A B^T + beta C.
@@ -125,6 +146,7 @@ struct F8Extra {
   const bf16_t* aux;
   int ldaux;
   float beta;
+  int cdeq;  // C = dequant(C8) instead of the unrounded value (epi flag F8_EPI_CDEQ)
 };
 
 // Epilogue: dequant, bias, relu -> per-wave bf16 LDS image -> 16-byte
@@ -221,11 +243,7 @@ struct F8Epi {
           v[e] = (short)f2bf(f);
         }
       }
-      if (n + 8 <= N) {
-        *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
-      } else {
-        for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
-      }
+      int lo = 0, hi = 0;
       if (C8) {
         float f[8];
 #pragma unroll
@@ -233,10 +251,28 @@ struct F8Epi {
           f[e] = bf2f((bf16_t)v[e]);
           amax = fmaxf(amax, fabsf(f[e]));
         }
-        int lo = f8::pack2_f8<CF, false>(f[0] * s8, f[1] * s8, 0);
+        lo = f8::pack2_f8<CF, false>(f[0] * s8, f[1] * s8, 0);
         lo = f8::pack2_f8<CF, true>(f[2] * s8, f[3] * s8, lo);
-        int hi = f8::pack2_f8<CF, false>(f[4] * s8, f[5] * s8, 0);
+        hi = f8::pack2_f8<CF, false>(f[4] * s8, f[5] * s8, 0);
         hi = f8::pack2_f8<CF, true>(f[6] * s8, f[7] * s8, hi);
+        if (ex.cdeq) {
+          // C = dequant(C8): the bf16 output carries exactly the values the
+          // fp8 consumer sees (power-of-two scales: exact in bf16), so a
+          // backward that reads C differentiates the forward that ran
+          const float inv = 1.f / s8;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = (short)f2bf(f8::unpack_f8<CF>(lo, e) * inv);
+            v[e + 4] = (short)f2bf(f8::unpack_f8<CF>(hi, e) * inv);
+          }
+        }
+      }
+      if (n + 8 <= N) {
+        *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
+      }
+      if (C8) {
         if (n + 8 <= N) {
           *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
         } else {
@@ -469,7 +505,13 @@ __global__ __launch_bounds__(256) void fp8_scale_update_kernel(float* __restrict
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
   const float a = __uint_as_float(m);
-  if (lane == 0 && a > 0.f && isfinite(a)) scale[i] = fmax / (a * margin_pow2);
+  // power-of-two scales: dequantisation (x8 / scale) is exact in bf16 / f32,
+  // so an fp8 operand and its bf16 dequantised copy carry the same values
+  if (lane == 0 && a > 0.f && isfinite(a)) {
+    int e;
+    frexpf(fmax / (a * margin_pow2), &e);  // ratio = f * 2^e, f in [0.5, 1)
+    scale[i] = ldexpf(1.f, e - 1);         // largest 2^k <= ratio
+  }
 }
 
 // e4m3 -> f32 (tests / debugging)
@@ -534,7 +576,10 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
                             int ldc8, int epi, int cfg, int afmt, int cfmt, const void* aux,
                             int ldaux, float beta, hipStream_t st) {
   if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
-  const F8Extra ex{(const bf16_t*)aux, ldaux, beta};
+  const int cdeq = (epi & F8_EPI_CDEQ) != 0;
+  epi &= ~F8_EPI_CDEQ;
+  if (cdeq && !C8) return -2;
+  const F8Extra ex{(const bf16_t*)aux, ldaux, beta, cdeq};
   if (afmt == 0 && cfmt == 0) {
     switch (epi) {
       case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);

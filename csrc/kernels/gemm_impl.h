@@ -668,7 +668,7 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st,
                   const GemmGroup* grp = nullptr, int G = 1) {
-  if (tile_cfg >= 20 && tile_cfg <= 22) {
+  if (tile_cfg >= 20 && tile_cfg <= 24) {
     // software-pipelined kernel (one problem, no split-K); else cfg 0
     if (!grp && splits <= 1) {
       bool ok = false;
@@ -681,6 +681,9 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
         TDG_PIPE(20, 256, 256, 2, 4, 4)
         TDG_PIPE(21, 256, 128, 2, 4, 6)
         TDG_PIPE(22, 128, 256, 2, 4, 6)
+        // one wave per SIMD, 128x128 per wave (accumulators beyond 256 VGPRs)
+        TDG_PIPE(23, 256, 256, 2, 2, 4)
+        TDG_PIPE(24, 256, 256, 2, 2, 5)
         default: break;
       }
 #undef TDG_PIPE

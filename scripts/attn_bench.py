@@ -35,6 +35,6 @@ for causal in (False, True):
     tf = graph_time(lambda: kk.attn_fwd(q, k, v, kv, 0.125, causal))
     tb = graph_time(lambda: kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, causal))
     fl = 4.0 * B * H * L * L * hd * (0.5 if causal else 1.0)
-    print(f"B={B} H={H} L={L} causal={causal} U={os.environ.get('TDG_ATTN_U', 'default')}: "
+    print(f"B={B} H={H} L={L} causal={causal}: "
           f"fwd {tf:.2f} us ({fl / tf / 1e9:.3f} PF/s)  bwd {tb:.2f} us ({2.5 * fl / tb / 1e9:.3f} PF/s)",
           flush=True)

@@ -586,6 +586,9 @@ class CrossAttnBlockFn(torch.autograd.Function):
                 q = K.linear_fwd(x2, wq.compute, bq.master)
             if q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
                 kv8, kvs = rt.fp8.kv8
+                if kv8.shape != kv_all.shape:
+                    raise RuntimeError(f"fp8 cross K|V {tuple(kv8.shape)} is not this forward's "
+                                       f"{tuple(kv_all.shape)}")
                 kv85 = kv8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
                 skv = rt.fp8.meta.s(kvs)
                 o, aux = K.attn_fwd_fp8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],

@@ -251,8 +251,12 @@ class Transformer:
         kvh = KVGrad()
         kv_all = CrossKVFn.apply(enc, self.cross_kv.w, self.cross_kv.b, kvh, rt)
         x = EmbedFn.apply(self.store.anchor, tgt_in.contiguous(), self.dec_emb, self.pe_tgt, self.dec_site, rt)
-        for layer in self.dec_layers:
-            x = layer(x, kv_all, kvh, src_len, tgt_len, rt)
+        try:
+            for layer in self.dec_layers:
+                x = layer(x, kv_all, kvh, src_len, tgt_len, rt)
+        finally:
+            if rt.fp8 is not None:
+                rt.fp8.kv8 = None  # this forward's e4m3 K|V: never seen by the next one
         return x
 
     def features(self, src, tgt_in, rt: RunCtx, lengths=None):

@@ -87,15 +87,20 @@ def dequantize(x8: torch.Tensor, scale: float) -> torch.Tensor:
 
 
 def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
-             out8_slot: Optional[int] = None, cfg: Optional[int] = None
+             out8_slot: Optional[int] = None, cfg: Optional[int] = None, c_deq: bool = False
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """y[M,N] = dequant(a8[M,K] @ b8[N,K]^T) + bias (relu), bf16, on the
     block-scaled e4m3 MFMA (csrc/kernels/fp8.hip); with out8_slot also
-    y8 = e4m3(y * scale[out8_slot]) (amax recorded)."""
+    y8 = e4m3(y * scale[out8_slot]) (amax recorded). c_deq (needs out8_slot):
+    y = y8 / scale instead, the exact values the e4m3 consumer of y8 sees
+    (scales are powers of two), so a backward reading y is consistent with
+    a forward that ran on y8."""
     M, Kd = a8.shape
     N = b8.shape[0]
     y8 = torch.empty(M, N, dtype=FP8, device=a8.device) if out8_slot is not None else None
-    epi = 2 if relu else (1 if bias is not None else 0)
+    if c_deq and y8 is None:
+        raise ValueError("gemm_fp8: c_deq needs out8_slot")
+    epi = (2 if relu else (1 if bias is not None else 0)) | (16 if c_deq else 0)
     y = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device)
 
     def run(c):
@@ -234,7 +239,9 @@ class Fp8State:
         # attn_fwd_fp8_kernel, on the sequences it covers)
         self.proj_slots: Dict[int, int] = {}
         self.out_slots: Dict[int, int] = {}
-        self.kv8: Optional[Tuple[torch.Tensor, int]] = None  # batched cross K|V, e4m3
+        # batched cross K|V (e4m3) of the CURRENT forward, with its scale slot:
+        # set by CrossKVFn, cleared by Transformer.forward after the decoder
+        self.kv8: Optional[Tuple[torch.Tensor, int]] = None
         self.stash: Dict[int, torch.Tensor] = {}
         for layer in list(model.enc_layers) + list(model.dec_layers):
             self.weights.add(layer.ff1.w)
@@ -282,7 +289,10 @@ class Fp8State:
         if x8 is None:
             x8 = quantize(x2, self.meta, xs)
         ys = self.out_slots[id(w)] if want8 else None
-        y, y8 = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws, out8_slot=ys)
+        # want8: y is the dequantised y8 (the attention backward reads y and
+        # must see the operands the e4m3 attention forward used)
+        y, y8 = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws, out8_slot=ys,
+                         c_deq=want8)
         return (y, y8, ys) if want8 else y
 
     def after_step(self) -> None:

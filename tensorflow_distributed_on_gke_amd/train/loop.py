@@ -223,6 +223,14 @@ class Trainer:
         s, info = self.settings, self.info
         if s.kill_point not in ("step", "backward"):
             raise ValueError(f"kill_point must be step or backward, got {s.kill_point!r}")
+        # the grad-ready hook below runs on the host during an EAGER backward
+        # only: a captured step (single HIP graph or the segmented data-parallel
+        # graph) replays without it, so with a backward fault armed every rank
+        # steps eagerly (fit() skips the capture) -- the fault would otherwise
+        # silently never fire
+        self._backward_fault_armed = s.kill_at_step >= 0 and s.kill_point == "backward"
+        if self._backward_fault_armed and info.chief:
+            self.log("fault injection at a backward point: HIP-graph capture disabled for this run")
         if s.kill_at_step < 0 or s.kill_point != "backward" or info.rank != (s.kill_rank % info.world):
             return
         seen = [0]
@@ -263,7 +271,8 @@ class Trainer:
             for batch in range(steps):
                 src, tgt = self._to_dev(self.train_data.next())
                 epoch_tokens += (src.shape[1] + tgt.shape[1] - 1) * src.shape[0] * info.world
-                if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured:
+                if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured \
+                        and not self._backward_fault_armed:
                     # capture() restores the state its warm-up steps changed,
                     # so this batch is still trained exactly once (below)
                     if self.ddp is not None and self.ddp.active:

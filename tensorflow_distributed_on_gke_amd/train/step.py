@@ -91,7 +91,11 @@ class TrainStep:
         if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
             opt.zero_grad = False  # every GPU gradient writer overwrites
         mode = DP_OVERLAP_OPT
-        if ddp is not None and ddp.active and fp8_state is None and mode != "0":
+        # (fp8: the scale update and the e4m3 weight re-quantisation run after
+        # ddp.finish(), when every bucket's Adam is done, so the per-bucket
+        # Adam stays on; the mid-backward variant would update weights the
+        # fp8 copies of which the encoder backward still reads)
+        if ddp is not None and ddp.active and mode != "0" and not (fp8_state is not None and mode != "tail"):
             ddp.attach_optimizer(opt, release=mode != "tail")
         # metric accumulators [sum loss, sum acc, n steps, n tokens] (device)
         self.accum = torch.zeros(4, dtype=torch.float32, device=dev)

@@ -146,6 +146,78 @@ def test_gpu_dp_rehearsal_matches_single_process(tmp_path, world, opt_mode, loss
     assert torch.allclose(r0["loss"], torch.stack(losses), rtol=1e-3, atol=1e-4)
 
 
+def _fp8_worker(rank, world, port, out, graph):
+    """Config 5's data-parallel step (fp8 forward + FFN backward, per-bucket
+    Adam at the tail, bf16 gradient all-reduce) with `world` ranks on cuda:0."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
+                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD="0")
+    from tensorflow_distributed_on_gke_amd.train import step as step_mod
+    step_mod.WAVE_TILES = 37
+    step_mod.DP_OVERLAP_OPT = "tail"
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.ops import fp8 as F
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
+    from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
+    from tensorflow_distributed_on_gke_amd.train.optim import Adam
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    kk.AUTOTUNE = False
+    info = tdist.init_distributed("cuda")
+    # hd 64 and sequences > 128: the e4m3 attention forward runs too
+    cfg = model_config("tiny", d_model=128, heads=2, d_ff=512, src_vocab=1000, tgt_vocab=1000,
+                       dropout=0.1)
+    m = Transformer(cfg).build(info.device, seed=1 + rank)
+    opt = Adam(m.store, m.cfg.d_model, lr=1e-3)
+    ddp = DataParallel(m.store, bucket_mb=0.25, comm_dtype=torch.bfloat16)
+    ddp.broadcast_params(0)
+    st = F.Fp8State(m)  # after the broadcast: weight scales from the common weights
+    st.weights.calibrate()
+    step = TrainStep(m, opt, ddp, workers=world, seed=5, fp8_state=st, loss_mode="global_mean")
+    assert ddp.opt is not None, "per-bucket Adam must be attached under fp8"
+    g = torch.Generator().manual_seed(7 + rank)
+
+    def batch():
+        src = torch.randint(4, 1000, (4, 160), generator=g)
+        tgt = torch.randint(4, 1000, (4, 161), generator=g)
+        return src.to(info.device), tgt.to(info.device)
+
+    if graph:
+        assert step.capture(*batch())
+        assert step.segments is not None
+    losses = []
+    for i in range(4):
+        losses.append(float(step(*batch())[0]))
+        ddp.verify_replicas()
+    torch.cuda.synchronize()
+    wslots = [i for i, n in enumerate(st.meta.names) if n.startswith(("w:", "wt:"))]
+    torch.save({"flat": m.store.flat.cpu(), "wscale": st.meta.scale[wslots].cpu(),
+                "w8": [w8.view(torch.uint8).cpu() for _, w8, _, _ in st.weights.items],
+                "loss": losses}, f"{out}.{rank}")
+    ddp.close()
+    tdist.barrier()
+    tdist.shutdown()
+
+
+@pytest.mark.parametrize("world,graph", [(2, "seg"), (4, "seg"), (2, "")])
+def test_gpu_dp_fp8_replicas_identical(tmp_path, world, graph):
+    """fp8 + data parallel (BASELINE config 5 is DP = 8): replicas stay
+    bitwise equal, every rank derives the same weight scales and e4m3 weight
+    copies, and the losses are finite."""
+    out = str(tmp_path / "res")
+    mp.start_processes(_fp8_worker, args=(world, _port(), out, graph), nprocs=world, join=True,
+                       start_method="spawn")
+    rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["flat"], r["flat"])
+        assert torch.equal(rs[0]["wscale"], r["wscale"])
+        for a, b in zip(rs[0]["w8"], r["w8"]):
+            assert torch.equal(a, b)
+    for r in rs:
+        assert all(l == l and 0 < l < 20 for l in r["loss"]), r["loss"]
+
+
 def test_gpu_rank_dying_mid_backward_with_comm_thread(tmp_path):
     """Failure detection on the GPU path: two ranks on one GPU (gloo), host
     comm thread forced on, eager steps; rank 1 exits inside a backward while

@@ -3,6 +3,8 @@ block-scaled MFMA GEMM (forward, and the e5m2-gradient backward GEMMs with the
 ReLU-backward mask and beta accumulation) vs an fp32 reference of the
 dequantised operands, the fused fp8 epilogue output, delayed scaling, and an
 fp8 training run (forward + FFN backward in fp8) vs bf16."""
+import math
+
 import pytest
 import torch
 
@@ -24,7 +26,9 @@ def test_quantize_matches_torch_e4m3():
     assert (x8.view(torch.uint8) == ref.view(torch.uint8)).float().mean().item() > 0.999
     assert abs(meta.amax_values()[i].item() - x.float().abs().max().item()) < 1e-6
     meta.update()
-    assert abs(meta.scale[i].item() - 448.0 / x.float().abs().max().item()) < 1e-3
+    # power-of-two delayed scale: the largest 2^k <= 448 / amax
+    r = 448.0 / x.float().abs().max().item()
+    assert meta.scale[i].item() == 2.0 ** math.floor(math.log2(r))
     assert meta.amax_values()[i].item() == 0.0
 
 
@@ -64,7 +68,7 @@ def test_quantize_matches_torch_e5m2():
     ref = (x.float() * 4096.0).clamp(-57344, 57344).to(torch.float8_e5m2)
     assert (x8.view(torch.uint8) == ref.view(torch.uint8)).float().mean().item() > 0.999
     meta.update()
-    assert abs(meta.scale[i].item() - 57344.0 / 30.0) < 1e-2
+    assert meta.scale[i].item() == 2.0 ** math.floor(math.log2(57344.0 / 30.0))
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128)])
@@ -234,3 +238,63 @@ def test_quant_multi_matches_single():
     am = meta.amax_values()
     for x, s in zip(xs, slots):
         assert am[s].item() == x.float().abs().max().item()
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_gemm_fp8_c_deq(relu):
+    """c_deq: the bf16 output is exactly dequant(y8) (power-of-two scale), and
+    y8 is unchanged by the flag."""
+    torch.manual_seed(2)
+    meta = F.Fp8Meta(DEV)
+    ia, ib, io = meta.slot("a"), meta.slot("b"), meta.slot("o")
+    meta.scale[ia], meta.scale[ib], meta.scale[io] = 64.0, 1024.0, 8.0
+    a = torch.randn(1000, 256, device=DEV).bfloat16()
+    b = (torch.randn(384, 256, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(384, device=DEV)
+    a8, b8 = F.quantize(a, meta, ia), F.quantize(b, meta, ib)
+    y0, y80 = F.gemm_fp8(a8, b8, bias, meta, ia, ib, relu=relu, out8_slot=io, cfg=0)
+    y, y8 = F.gemm_fp8(a8, b8, bias, meta, ia, ib, relu=relu, out8_slot=io, cfg=0, c_deq=True)
+    assert torch.equal(y8.view(torch.uint8), y80.view(torch.uint8))
+    assert torch.equal(y.float(), y8.float() / 8.0)
+    # and within e4m3 rounding of the plain output
+    assert (y.float() - y0.float()).abs().max().item() <= 0.07 * y0.float().abs().max().item()
+
+
+@pytest.mark.parametrize("causal,Lq,Lk", [(False, 384, 384), (True, 512, 512), (False, 260, 390)])
+def test_fp8_attention_gradients_consistent(causal, Lq, Lk):
+    """fp8 mode's attention: forward on e4m3 Q/K/V (attn_fwd_fp8), backward
+    (attn_bwd) on the bf16 copies the c_deq projection epilogue writes, i.e.
+    the dequantised e4m3 values. The gradients must be those of fp32
+    attention on the dequantised inputs -- the backward's recomputed P must
+    match the P of the forward that produced O and the LSE."""
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    torch.manual_seed(7)
+    B, H, hd = 2, 3, 64
+    meta = F.Fp8Meta(DEV)
+    slots = [meta.slot(n) for n in "qkv"]
+    raw = [torch.randn(B, L, H, hd, device=DEV).bfloat16() * 2 for L in (Lq, Lk, Lk)]
+    for t, i in zip(raw, slots):  # delayed scaling: amax -> power-of-two scale
+        F.quantize(t, meta, i)
+    meta.update()
+    x8 = [F.quantize(t, meta, i, record=False).view(t.shape) for t, i in zip(raw, slots)]
+    sc = [meta.scale[i].item() for i in slots]
+    deq = [(t8.float() / s) for t8, s in zip(x8, sc)]
+    q, k, v = (d.bfloat16() for d in deq)
+    for d, bq in zip(deq, (q, k, v)):
+        assert torch.equal(d, bq.float())  # exact: power-of-two scales
+    kv_len = torch.tensor([Lk, max(1, Lk - 37)], dtype=torch.int32, device=DEV)
+    scale = hd ** -0.5
+    o, lse = kk.attn_fwd_fp8(x8[0], x8[1], x8[2], meta.s(slots[0]), meta.s(slots[1]),
+                             meta.s(slots[2]), kv_len, scale, causal)
+    do = torch.randn(B, Lq, H, hd, device=DEV).bfloat16()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv_len, scale, causal)
+    qr, kr, vr = (d.clone().requires_grad_(True) for d in deq)
+    ref, _ = _attn_ref(qr, kr, vr, kv_len, causal, scale)
+    ref.backward(do.float())
+    for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        err = (got.float() - want).abs().max().item() / (want.abs().max().item() + 1e-12)
+        # bf16 kernels on exact operands: the forward's e4m3 P and bf16 O are
+        # the only roundings left (a P inconsistent with the forward's LSE
+        # shows as errors of order 1)
+        assert err < 5e-2, (name, err)
