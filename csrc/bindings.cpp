@@ -55,11 +55,15 @@ int tdg_gemm_grouped(const void* const* A, const void* const* B, void* const* C,
                      float alpha, float beta, int tile_cfg, hipStream_t st);
 int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                     const int* shapes, int K, int a_kc, int b_kc, int out_f32, float alpha,
-                    float beta, float* const* bias_out, hipStream_t st);
+                    float beta, float* const* bias_out, int impl, hipStream_t st);
+int tdg_wgrad_fp8(const void* const* A, const void* const* B, float* const* C,
+                  const float* const* sa, const float* const* sb, int P, const int* shapes, int T,
+                  float beta, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, int afmt, int cfmt,
-                 const void* aux, int ldaux, float beta, hipStream_t st);
+                 const void* aux, int ldaux, float beta, const void* aux8, float* colsum_out,
+                 float colsum_beta, float* ws, hipStream_t st);
 int tdg_fp8_quant_multi(const void* const* x, void* const* y, const long long* n, const int* slot,
                         int nseg, const float* scale, unsigned* amax, hipStream_t st);
 int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale, unsigned* amax,
@@ -608,7 +612,7 @@ void gemm_grouped(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
 void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
                  const std::vector<Tensor>& Cs, const std::vector<int64_t>& shapes, int64_t K,
                  bool a_kc, bool b_kc, double alpha, double beta,
-                 const std::vector<c10::optional<Tensor>>& bias_out) {
+                 const std::vector<c10::optional<Tensor>>& bias_out, int64_t impl) {
   const size_t P = As.size();
   TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && shapes.size() == 7 * P,
               "gemm_ragged: 1..64 problems, 7 shape values each (M, N, lda, ldb, ldc, t_first, "
@@ -658,7 +662,7 @@ void gemm_ragged(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
   c10::DeviceGuard g(As[0].device());
   const int rc = tdg_gemm_ragged(a.data(), b.data(), c.data(), (int)P, sh.data(), (int)K, a_kc,
                                  b_kc, f32, (float)alpha, (float)beta,
-                                 any_bias ? bo.data() : nullptr, stream_of(As[0]));
+                                 any_bias ? bo.data() : nullptr, (int)impl, stream_of(As[0]));
   check_err(rc, "tdg gemm_ragged");
 }
 
@@ -687,42 +691,112 @@ void colsum_grouped(const std::vector<Tensor>& Xs, const std::vector<Tensor>& ou
 }
 
 // ---------------------------------------------------------------- fp8
-void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
+void gemm_fp8(const Tensor& A, const Tensor& B, const optional<Tensor>& C, const optional<Tensor>& bias,
               const Tensor& sa, const Tensor& sb, const optional<Tensor>& C8,
               const optional<Tensor>& sc8, const optional<Tensor>& amax, int64_t M, int64_t N,
               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldc8, int64_t epi,
               int64_t cfg, int64_t afmt, int64_t cfmt, const optional<Tensor>& aux, int64_t ldaux,
-              double beta) {
+              double beta, const optional<Tensor>& aux8, const optional<Tensor>& colsum_out,
+              double colsum_beta, const optional<Tensor>& ws) {
   check_f8_fmt(A, afmt, "A8");
   check_f8_fmt(B, 0, "B8");
-  check_bf16(C, "C");
+  TORCH_CHECK(C.has_value() || C8.has_value() || colsum_out.has_value(), "gemm_fp8: no output");
+  if (C.has_value()) {
+    check_bf16(*C, "C");
+    TORCH_CHECK(C->numel() >= (M - 1) * ldc + N && ldc % 8 == 0, "gemm_fp8: C extent / ldc");
+  } else {
+    TORCH_CHECK(beta == 0.0 && !(epi & 16), "gemm_fp8: beta / C = dequant(C8) need C");
+  }
   check_f32(sa, "sa");
   check_f32(sb, "sb");
   TORCH_CHECK(K % 128 == 0 && lda % 16 == 0 && ldb % 16 == 0, "gemm_fp8: K % 128, ld % 16");
   TORCH_CHECK(A.numel() >= (M - 1) * lda + K && B.numel() >= (N - 1) * ldb + K, "gemm_fp8: A/B extent");
-  TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc % 8 == 0, "gemm_fp8: C extent / ldc");
   if (bias.has_value()) check_f32(*bias, "bias");
   const int64_t epi_id = epi & 15;  // (flag 16: C = dequant(C8))
   TORCH_CHECK((epi & ~int64_t(31)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
   TORCH_CHECK(!(epi & 16) || C8.has_value(), "gemm_fp8: C = dequant(C8) needs C8");
   TORCH_CHECK(epi_id == 0 || epi_id == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
-  TORCH_CHECK(epi_id != 3 || (aux.has_value() && aux->numel() >= (M - 1) * ldaux + N),
-              "gemm_fp8: the ReLU-backward epilogue needs aux [M, >= N]");
-  if (aux.has_value()) check_bf16(*aux, "aux");
+  TORCH_CHECK(epi_id != 3 || aux.has_value() != aux8.has_value(),
+              "gemm_fp8: the ReLU-backward epilogue needs exactly one of aux (bf16) / aux8 (e4m3)");
+  if (aux.has_value()) {
+    check_bf16(*aux, "aux");
+    TORCH_CHECK(aux->numel() >= (M - 1) * ldaux + N, "gemm_fp8: aux extent");
+  }
+  if (aux8.has_value()) {
+    check_f8_fmt(*aux8, 0, "aux8");
+    TORCH_CHECK(aux8->numel() >= (M - 1) * ldaux + N && ldaux % 8 == 0, "gemm_fp8: aux8 extent");
+  }
   TORCH_CHECK((afmt == 0 || afmt == 1) && (cfmt == 0 || cfmt == 1), "gemm_fp8: formats are 0 / 1");
   if (C8.has_value()) {
     check_f8_fmt(*C8, cfmt, "C8");
     TORCH_CHECK(sc8.has_value() && C8->numel() >= (M - 1) * ldc8 + N && ldc8 % 8 == 0, "gemm_fp8: C8");
   }
+  if (colsum_out.has_value()) {
+    check_f32(*colsum_out, "colsum_out");
+    TORCH_CHECK(colsum_out->is_contiguous() && colsum_out->numel() == N && cfg == 0,
+                "gemm_fp8: colsum_out is [N] f32 (128x128 tile config)");
+    TORCH_CHECK(ws.has_value() && ws->scalar_type() == at::kFloat &&
+                    ws->numel() >= ((M + 127) / 128) * 2 * N,
+                "gemm_fp8: colsum workspace [ceil(M/128)*2, N] f32");
+  }
   c10::DeviceGuard g(A.device());
-  const int rc = tdg_gemm_fp8(A.data_ptr(), B.data_ptr(), C.data_ptr(),
+  const int rc = tdg_gemm_fp8(A.data_ptr(), B.data_ptr(), C ? C->data_ptr() : nullptr,
                               bias ? bias->data_ptr<float>() : nullptr, sa.data_ptr<float>(),
                               sb.data_ptr<float>(), C8 ? C8->data_ptr() : nullptr,
                               sc8 ? sc8->data_ptr<float>() : nullptr, amax_ptr(amax), (int)M,
                               (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)ldc8, (int)epi,
                               (int)cfg, (int)afmt, (int)cfmt, aux ? aux->data_ptr() : nullptr,
-                              (int)ldaux, (float)beta, stream_of(A));
+                              (int)ldaux, (float)beta, aux8 ? aux8->data_ptr() : nullptr,
+                              colsum_out ? colsum_out->data_ptr<float>() : nullptr,
+                              (float)colsum_beta, ws ? ws->data_ptr<float>() : nullptr,
+                              stream_of(A));
   check_err(rc, "tdg gemm_fp8");
+}
+
+// fp8 weight gradients: Cs[i][M,N] (f32, =|+= beta) = dequant(As[i][T,M]^T (e5m2)
+// @ Bs[i][T,N] (e4m3)), token-major operands, one ragged launch.
+void wgrad_fp8(const std::vector<Tensor>& As, const std::vector<Tensor>& Bs,
+               const std::vector<Tensor>& Cs, const std::vector<Tensor>& sas,
+               const std::vector<Tensor>& sbs, double beta) {
+  const size_t P = As.size();
+  TORCH_CHECK(P >= 1 && P <= 64 && Bs.size() == P && Cs.size() == P && sas.size() == P &&
+                  sbs.size() == P,
+              "wgrad_fp8: 1..64 problems");
+  const int64_t T = As[0].size(0);
+  std::vector<const void*> a(P), b(P);
+  std::vector<float*> c(P);
+  std::vector<const float*> sa(P), sb(P);
+  std::vector<int> sh(5 * P);
+  for (size_t i = 0; i < P; ++i) {
+    check_f8_fmt(As[i], 1, "A8 (e5m2 gradient)");
+    check_f8_fmt(Bs[i], 0, "B8 (e4m3 activation)");
+    check_f32(Cs[i], "C");
+    check_f32(sas[i], "sa");
+    check_f32(sbs[i], "sb");
+    TORCH_CHECK(As[i].dim() == 2 && Bs[i].dim() == 2 && Cs[i].dim() == 2, "wgrad_fp8: 2-D tensors");
+    TORCH_CHECK(As[i].size(0) == T && Bs[i].size(0) == T, "wgrad_fp8: one token count");
+    TORCH_CHECK(As[i].stride(1) == 1 && Bs[i].stride(1) == 1 && Cs[i].stride(1) == 1,
+                "wgrad_fp8: unit inner stride");
+    const int64_t M = Cs[i].size(0), N = Cs[i].size(1);
+    TORCH_CHECK(As[i].size(1) == M && Bs[i].size(1) == N, "wgrad_fp8: shapes");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(As[i].data_ptr()) % 16) == 0 &&
+                    (reinterpret_cast<uintptr_t>(Bs[i].data_ptr()) % 16) == 0,
+                "wgrad_fp8: operands 16-byte aligned");
+    a[i] = As[i].data_ptr();
+    b[i] = Bs[i].data_ptr();
+    c[i] = Cs[i].data_ptr<float>();
+    sa[i] = sas[i].data_ptr<float>();
+    sb[i] = sbs[i].data_ptr<float>();
+    sh[5 * i] = (int)M;
+    sh[5 * i + 1] = (int)N;
+    sh[5 * i + 2] = (int)As[i].stride(0);
+    sh[5 * i + 3] = (int)Bs[i].stride(0);
+    sh[5 * i + 4] = (int)Cs[i].stride(0);
+  }
+  c10::DeviceGuard g(As[0].device());
+  check_err(tdg_wgrad_fp8(a.data(), b.data(), c.data(), sa.data(), sb.data(), (int)P, sh.data(),
+                          (int)T, (float)beta, stream_of(As[0])),
+            "tdg wgrad_fp8");
 }
 
 void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
@@ -944,9 +1018,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),
-        py::arg("bias_out") = std::vector<c10::optional<Tensor>>{});
+        py::arg("bias_out") = std::vector<c10::optional<Tensor>>{}, py::arg("impl") = 0);
   m.def("colsum_grouped", &colsum_grouped);
-  m.def("gemm_fp8", &gemm_fp8);
+  m.def("gemm_fp8", &gemm_fp8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
+        py::arg("sa"), py::arg("sb"), py::arg("C8"), py::arg("sc8"), py::arg("amax"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("ldc8"),
+        py::arg("epi"), py::arg("cfg"), py::arg("afmt"), py::arg("cfmt"), py::arg("aux"),
+        py::arg("ldaux"), py::arg("beta"), py::arg("aux8") = py::none(),
+        py::arg("colsum_out") = py::none(), py::arg("colsum_beta") = 0.0, py::arg("ws") = py::none());
+  m.def("wgrad_fp8", &wgrad_fp8);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_quant_multi", &fp8_quant_multi);
   m.def("fp8_scale_update", &fp8_scale_update);

@@ -25,6 +25,7 @@
 // MatMuls of the reference (distributed_training_transformer/
 // transformer_model.py:119-122, 165, 172-174); backward stays bf16.
 #include "tdg_common.h"
+#include "tdg_reduce.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -147,13 +148,23 @@ struct F8Extra {
   int ldaux;
   float beta;
   int cdeq;  // C = dequant(C8) instead of the unrounded value (epi flag F8_EPI_CDEQ)
+  // ReLU-backward mask from an 8-bit copy of the activation (aux8 != 0 <=> the
+  // e4m3 ReLU output is positive) instead of the bf16 aux
+  const uint8_t* aux8;
+  // column-sum partials of the stored (bf16-rounded) output: row tm * WM + wm
+  // of colsum[rows][N] per wave row of each tile (the bias gradient of the
+  // layer whose output gradient this is; folded by the host launcher)
+  float* colsum;
 };
 
 // Epilogue: dequant, bias, relu -> per-wave bf16 LDS image -> 16-byte
 // stores (ReLU-backward mask and beta applied per 8-column chunk) + the
 // optional fp8 copy (format CF) and its amax. Called after a barrier that
 // ends every wave's reads of the pipeline stages.
-template <int BM, int BN, int WM, int WN, int EPI, int CF = 0>
+// PRE_OK: prefetch the ReLU mask / old C of every chunk before the image is
+// written (off for the 256x256 one-wave tiles: 32 chunks per lane would not
+// fit in registers; those load per chunk instead)
+template <int BM, int BN, int WM, int WN, int EPI, int CF = 0, bool PRE_OK = true>
 struct F8Epi {
   static constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -176,9 +187,11 @@ struct F8Epi {
     // the ReLU mask / old C of every chunk this lane stores, loaded before
     // the image is written (one memory latency per tile, not per chunk)
     constexpr int ITER = (WTM * CPR) / 64;
-    constexpr bool PRE = EPI == F8_EPI_DRELU;
+    constexpr bool PRE = EPI == F8_EPI_DRELU && PRE_OK;
+    static_assert(64 % CPR == 0, "a lane keeps its column chunk across iterations");
     short8_t pre_aux[PRE ? ITER : 1], pre_c[PRE ? ITER : 1];
     const bool vec_ok = (ldc & 7) == 0 && (EPI != F8_EPI_DRELU || (ex.ldaux & 7) == 0);
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (PRE) {
 #pragma unroll
       for (int tt = 0; tt < ITER; ++tt) {
@@ -188,7 +201,14 @@ struct F8Epi {
         const int n = n0 + wn * WTN + ch * 8;
         pre_aux[tt] = pre_c[tt] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
         if (vec_ok && m < M && n + 8 <= N) {
-          pre_aux[tt] = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
+          if (ex.aux8) {  // 8 mask bytes -> 0 / 1 halves (only the sign of the mask is used)
+            const uint2 b = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              pre_aux[tt][e] = ((e < 4 ? b.x >> (8 * e) : b.y >> (8 * (e - 4))) & 0xffu) ? 0x3f80 : 0;
+          } else {
+            pre_aux[tt] = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
+          }
           if (ex.beta != 0.f) pre_c[tt] = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
         }
       }
@@ -226,8 +246,18 @@ struct F8Epi {
           if constexpr (PRE) {
             mk = pre_aux[tt];
             old = pre_c[tt];
-          } else if (ex.beta != 0.f) {
-            old = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
+          } else {
+            if constexpr (EPI == F8_EPI_DRELU) {
+              if (ex.aux8) {
+                const uint2 b = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                  mk[e] = ((e < 4 ? b.x >> (8 * e) : b.y >> (8 * (e - 4))) & 0xffu) ? 0x3f80 : 0;
+              } else {
+                mk = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
+              }
+            }
+            if (ex.beta != 0.f) old = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
           }
         }
 #pragma unroll
@@ -235,13 +265,19 @@ struct F8Epi {
           if (!vec && n + e >= N) break;
           float f = bf2f((bf16_t)v[e]);
           if constexpr (EPI == F8_EPI_DRELU) {
-            const float a = vec ? bf2f((bf16_t)mk[e]) : bf2f(ex.aux[(size_t)m * ex.ldaux + n + e]);
+            const float a = vec ? bf2f((bf16_t)mk[e])
+                                : (ex.aux8 ? (ex.aux8[(size_t)m * ex.ldaux + n + e] ? 1.f : 0.f)
+                                           : bf2f(ex.aux[(size_t)m * ex.ldaux + n + e]));
             if (!(a > 0.f)) f = 0.f;
           }
           if (ex.beta != 0.f)
             f += ex.beta * (vec ? bf2f((bf16_t)old[e]) : bf2f(C[(size_t)m * ldc + n + e]));
           v[e] = (short)f2bf(f);
         }
+      }
+      if (ex.colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += bf2f((bf16_t)v[e]);  // (columns past N: never stored)
       }
       int lo = 0, hi = 0;
       if (C8) {
@@ -267,10 +303,12 @@ struct F8Epi {
           }
         }
       }
-      if (n + 8 <= N) {
-        *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
-      } else {
-        for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
+      if (C) {
+        if (n + 8 <= N) {
+          *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
+        } else {
+          for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
+        }
       }
       if (C8) {
         if (n + 8 <= N) {
@@ -280,6 +318,19 @@ struct F8Epi {
           const uint8_t* c8 = reinterpret_cast<const uint8_t*>(&hi);
           for (int e = 0; e < 8 && n + e < N; ++e) C8[(size_t)m * ldc8 + n + e] = e < 4 ? b8[e] : c8[e - 4];
         }
+      }
+    }
+    if (ex.colsum) {  // lanes with equal lane % CPR hold the same columns
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
+      const int n = n0 + wn * WTN + (lane % CPR) * 8;
+      float* prow = ex.colsum + (size_t)((m0 / BM) * WM + wm) * N;
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < N) prow[n + e] = csum[e];
       }
     }
     if (C8 && amax_out) {  // one atomic per workgroup, spread over AMAX_SPREAD words
@@ -389,6 +440,457 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   f8::lds_barrier();
   F8Epi<BM, BN, WM, WN, EPI, CF>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc,
                                       ldc8, m0, n0, wid, lane, tid, ex);
+}
+
+// ---------------------------------------------------------------------------
+// 256x256 tiles at ONE wave per SIMD (4 waves, 2 x 2, each 128 x 128: the
+// 8 x 8 accumulator fragments live in AGPRs). Why: at 128x128 tiles the fp8
+// MFMA consumes its operands twice as fast as bf16 does, so the LDS-DMA
+// stream (32 KiB per 512-cycle K tile per CU, ~34 TB/s chip-wide) meets the
+// L2 bandwidth and the kernel ran no faster than bf16; a 256x256 tile halves
+// the bytes per FLOP.
+//
+// A K tile (128 bytes deep) is four 16 KiB half-tile images: A0 (rows 0..63
+// of both wave rows), A1 (rows 64..127 of both), B0 / B1 likewise for the
+// columns, double-buffered (128 KiB). Four phases of 16 MFMAs per wave --
+// (a0,b0) (a0,b1) (a1,b1) (a1,b0) -- and every phase reads the fragments
+// the NEXT phase needs behind its MFMAs:
+//   P0: MFMA a0 x b0   reads B1(t)
+//   P1: MFMA a0 x b1   reads A1(t)
+//   P2: MFMA a1 x b1   reads A0(t+1)   (a0 registers are free after P1)
+//   P3: MFMA a1 x b0   reads B0(t+1)   (per column, behind its MFMAs)
+// Each phase starts with lgkmcnt(0) (last phase's reads are this phase's
+// operands) + a counted vmcnt + one barrier; the LDS-DMA of tile t+2's
+// halves goes into the buffers tile t's halves just vacated, one half per
+// phase (A0 in P0, B0 in P1, B1 in P2, A1 in P3), so five halves (80 KiB)
+// are in flight per CU in the steady state and every half has six phases to
+// land.
+namespace f8w1 {
+constexpr int HB = 128 * BK8;  // bytes of a half-tile image
+// image row x (0..127) of half h -> tile row / column
+__device__ __forceinline__ int remap(int x, int h) { return (x >> 6) * 128 + h * 64 + (x & 63); }
+}  // namespace f8w1
+
+template <int EPI, int AF = 0, int CF = 0>
+__global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
+    uint8_t* __restrict__ C8, const float* __restrict__ sc8, unsigned* __restrict__ amax_out,
+    int M, int N, int K, int lda, int ldb, int ldc, int ldc8, F8Extra ex) {
+  constexpr int NW = 4, TM = 8, TN = 8;
+  constexpr int HB = f8w1::HB, SB = 4 * HB;  // stage: A0, A1, B0, B1
+  using G = f8::Stage<128, NW>;               // 4 pieces of 1 KiB per wave per half
+  static_assert(G::P == 4, "half-tile = 4 pieces per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = K / BK8;  // host guarantees K % 128 == 0
+
+  G g;
+  g.init(wid, lane);
+  // per piece: byte offset of its 16-byte chunk (remapped image row, clamped
+  // to the operand) for each half; the host guarantees 32-bit extents
+  uint32_t aoff[2][4], boff[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int ra = m0 + f8w1::remap(g.row[i], h), rb = n0 + f8w1::remap(g.row[i], h);
+      ra = ra < M ? ra : M - 1;
+      rb = rb < N ? rb : N - 1;
+      aoff[h][i] = (uint32_t)ra * (uint32_t)lda + (uint32_t)g.col[i];
+      boff[h][i] = (uint32_t)rb * (uint32_t)ldb + (uint32_t)g.col[i];
+    }
+  // half q of tile kt: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (issue order)
+  auto issue = [&](int kt, int q) {
+    char* st = smem + (kt & 1) * SB;
+    const int k0 = kt * BK8;
+    const bool isA = q == 0 || q == 3;
+    const int h = (q == 0 || q == 1) ? 0 : 1;
+    char* dst = st + (isA ? h : 2 + h) * HB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint8_t* src = (isA ? A + aoff[h][i] : B + boff[h][i]) + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + (wid * 4 + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 fa[TM], fb[TN];
+  const int ar = wm * 64, br = wn * 64;  // this wave's rows / columns in a half image
+
+  // prologue: tiles 0 and 1 in flight; A0(0), B0(0) landed and read
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issue(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue(1, q);
+    f8::wait_vmcnt<24>();
+  } else {
+    f8::wait_vmcnt<8>();
+  }
+  f8::lds_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fa[i] = f8::frag(smem + 0 * HB, ar + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[j] = f8::frag(smem + 2 * HB, br + 16 * j, lane);
+
+  auto mfma = [&](int i, int j) {
+    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], AF, 0,
+                                                                 0, 127, 0, 127);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * SB;
+    const char* nx = smem + ((kt + 1) & 1) * SB;
+    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
+    // ---- P0: a0 x b0; read B1(kt); issue A0(kt+2)
+    // B1(kt) landed: younger issues A1(kt), A0/B0/B1/A1(kt+1) -- or fewer at the tail
+    if (more1) f8::wait_vmcnt<20>();
+    else f8::wait_vmcnt<4>();
+    f8::lds_barrier();  // (lgkmcnt(0): last phase's fragment reads)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tdg::tie(fb[j]);
+    if (more2) issue(kt + 2, 0);
+#pragma unroll
+    for (int j = 4; j < 8; ++j) fb[j] = f8::frag(st + 3 * HB, br + 16 * (j - 4), lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P1: a0 x b1; read A1(kt); issue B0(kt+2)
+    // A1(kt) landed: younger A0/B0/B1/A1(kt+1), A0(kt+2)
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<16>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+#pragma unroll
+    for (int j = 4; j < 8; ++j) tdg::tie(fb[j]);
+    if (more2) issue(kt + 2, 1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) fa[i] = f8::frag(st + 1 * HB, ar + 16 * (i - 4), lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 4; j < 8; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P2: a1 x b1; read A0(kt+1); issue B1(kt+2)
+    // A0(kt+1) landed: younger B0/B1/A1(kt+1), A0/B0(kt+2)
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<12>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+#pragma unroll
+    for (int i = 4; i < 8; ++i) tdg::tie(fa[i]);
+    if (more2) issue(kt + 2, 2);
+    if (more1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = f8::frag(nx + 0 * HB, ar + 16 * i, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 4; j < 8; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P3: a1 x b0; read B0(kt+1) per column behind its MFMAs; issue A1(kt+2)
+    // B0(kt+1) landed: younger B1/A1(kt+1), A0/B0/B1(kt+2)
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<8>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+    if (more1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
+    }
+    if (more2) issue(kt + 2, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 4; i < 8; ++i) mfma(i, j);
+      __builtin_amdgcn_s_setprio(0);
+      if (more1) fb[j] = f8::frag(nx + 2 * HB, br + 16 * j, lane);
+    }
+  }
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  f8::lds_barrier();
+  F8Epi<256, 256, 2, 2, EPI, CF, false>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N,
+                                             ldc, ldc8, m0, n0, wid, lane, tid, ex);
+}
+
+// ---------------------------------------------------------------------------
+// fp8 weight gradients: dW[m][n] (f32, =|+= beta) = alpha * sum_t dY8[t][m] X8[t][n],
+// alpha = 1 / (scale(dY8) scale(X8)), with dY8 the e5m2 gradient and X8 the
+// e4m3 activation copy the forward / backward already produced, both
+// TOKEN-major ([T][ld]): the reduction runs over rows, so the operand images
+// are [128 tokens][m bytes] and the MFMA fragments (32 consecutive tokens of
+// one m per lane) come from ds_read_b64_tr_b8, the gfx950 transposing read of
+// 8-bit data (per 16-lane group: lane 2q+p addresses row q, bytes 8p..8p+7 of
+// a 16-byte block; lane i receives column i of the 8 rows -- verified with
+// exact data, scripts/probes/tr_b8_probe.hip). No transposed copies.
+//
+// Ragged launch (one per flush): up to 64 problems in up to 8 shape classes,
+// 256x256 tiles at one wave per SIMD, the phase / half-tile schedule of
+// gemm_fp8_w1_kernel (two 64 KiB stages of 128 tokens). Half-image rows are
+// 128 bytes; 16-byte chunk c of token row t sits at chunk c ^ sw(t),
+// sw(t) = ((t >> 1) & 3) | ((t >> 5) & 1) << 2, which makes every 32-lane
+// half of a transposing fragment read touch all 64 banks once.
+constexpr int WF8_MAXP = 64, WF8_MAXC = 8;
+struct WF8Class {
+  int M, N, lda, ldb, ldc, tiles_m, tiles_n, tile_start, prob_start;
+};
+struct WF8Args {
+  const uint8_t* A[WF8_MAXP];  // dY8 [T][lda] (e5m2)
+  const uint8_t* B[WF8_MAXP];  // X8  [T][ldb] (e4m3)
+  float* C[WF8_MAXP];          // dW  [M][ldc] f32
+  const float* sa[WF8_MAXP];   // scale of A (one float, device)
+  const float* sb[WF8_MAXP];
+  WF8Class cls[WF8_MAXC];
+  int ncls;
+};
+
+namespace wf8 {
+__device__ __forceinline__ int sw(int t) { return ((t >> 1) & 3) | (((t >> 5) & 1) << 2); }
+// byte offset of (token row t, image column x) in a [128][128 B] half image
+__device__ __forceinline__ int off(int t, int x) { return t * 128 + ((((x >> 4) ^ sw(t)) & 7) << 4) + (x & 15); }
+// transposing 8-byte read (untracked: the caller waits with lgkmcnt)
+__device__ __forceinline__ uint64_t tr8(const void* p) {
+  uint64_t r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+// MFMA fragment of image columns base..base+15 (one per lane & 15), tokens
+// 32 (lane >> 4) .. +31: four transposing reads of 8 tokens
+__device__ __forceinline__ i32x8 frag(const char* img, int base, int lane) {
+  const int g = lane >> 4, w = lane & 15, q = w >> 1, p = w & 1;
+  uint64_t r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = 32 * g + 8 * j + q;
+    r[j] = tr8(img + off(t, base + 8 * p));
+  }
+  return i32x8{(int)r[0], (int)(r[0] >> 32), (int)r[1], (int)(r[1] >> 32),
+               (int)r[2], (int)(r[2] >> 32), (int)r[3], (int)(r[3] >> 32)};
+}
+}  // namespace wf8
+
+__global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int T, float beta) {
+  constexpr int TM = 8, TN = 8;
+  constexpr int HB = f8w1::HB, SB = 4 * HB;  // stage: A0, A1, B0, B1 (16 KiB each)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  WF8Class cl = args.cls[0];
+#pragma unroll
+  for (int i = 1; i < WF8_MAXC; ++i)
+    if (i < args.ncls && t0 >= args.cls[i].tile_start) cl = args.cls[i];
+  const int M = cl.M, N = cl.N, lda = cl.lda, ldb = cl.ldb, ldc = cl.ldc;
+  const int tpp = cl.tiles_m * cl.tiles_n;
+  const int lt = t0 - cl.tile_start;
+  const int pr = cl.prob_start + lt / tpp;
+  const int tt = lt % tpp;
+  int tm, tn;
+  if (cl.tiles_n <= cl.tiles_m) {
+    tn = tt % cl.tiles_n;
+    tm = tt / cl.tiles_n;
+  } else {
+    tm = tt % cl.tiles_m;
+    tn = tt / cl.tiles_m;
+  }
+  const uint8_t* __restrict__ A = args.A[pr];
+  const uint8_t* __restrict__ B = args.B[pr];
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = T / 128;  // host guarantees T % 128 == 0
+
+  // DMA pieces: per half image 16 pieces of 8 token rows x 128 B; wave wid
+  // issues pieces 4 wid .. 4 wid + 3. Lane: token row 8 piece + lane / 8,
+  // chunk position lane % 8 <- operand chunk (lane % 8) ^ sw(row)
+  uint32_t aoff[2][4], boff[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wid * 4 + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ wf8::sw(row);
+      const int x = c * 16;
+      int ma = m0 + f8w1::remap(x, h), nb = n0 + f8w1::remap(x, h);
+      ma = ma + 16 <= M ? ma : 0;  // past the operand: never stored (M % 16 == 0)
+      nb = nb + 16 <= N ? nb : 0;
+      aoff[h][i] = (uint32_t)row * (uint32_t)lda + (uint32_t)ma;
+      boff[h][i] = (uint32_t)row * (uint32_t)ldb + (uint32_t)nb;
+    }
+  // half q of tile kt: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (issue order)
+  auto issue = [&](int kt, int q) {
+    char* st = smem + (kt & 1) * SB;
+    const bool isA = q == 0 || q == 3;
+    const int h = (q == 0 || q == 1) ? 0 : 1;
+    char* dst = st + (isA ? h : 2 + h) * HB;
+    const size_t trow = (size_t)kt * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint8_t* src = isA ? A + trow * lda + aoff[h][i] : B + trow * ldb + boff[h][i];
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + (wid * 4 + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 fa[TM], fb[TN];
+  const int ar = wm * 64, br = wn * 64;
+
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issue(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue(1, q);
+    f8::wait_vmcnt<24>();
+  } else {
+    f8::wait_vmcnt<8>();
+  }
+  f8::lds_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fa[i] = wf8::frag(smem + 0 * HB, ar + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[j] = wf8::frag(smem + 2 * HB, br + 16 * j, lane);
+
+  // swapped operands: lane holds 4 consecutive n of one m (16-byte stores)
+  auto mfma = [&](int i, int j) {
+    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[j], fa[i], acc[i][j], 0, 1,
+                                                                 0, 127, 0, 127);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * SB;
+    const char* nx = smem + ((kt + 1) & 1) * SB;
+    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
+    if (more1) f8::wait_vmcnt<20>();
+    else f8::wait_vmcnt<4>();
+    f8::lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tdg::tie(fb[j]);
+    if (more2) issue(kt + 2, 0);
+#pragma unroll
+    for (int j = 4; j < 8; ++j) fb[j] = wf8::frag(st + 3 * HB, br + 16 * (j - 4), lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<16>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+#pragma unroll
+    for (int j = 4; j < 8; ++j) tdg::tie(fb[j]);
+    if (more2) issue(kt + 2, 1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) fa[i] = wf8::frag(st + 1 * HB, ar + 16 * (i - 4), lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 4; j < 8; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<12>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+#pragma unroll
+    for (int i = 4; i < 8; ++i) tdg::tie(fa[i]);
+    if (more2) issue(kt + 2, 2);
+    if (more1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = wf8::frag(nx + 0 * HB, ar + 16 * i, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 4; j < 8; ++j) mfma(i, j);
+    __builtin_amdgcn_s_setprio(0);
+    if (more2) f8::wait_vmcnt<20>();
+    else if (more1) f8::wait_vmcnt<8>();
+    else f8::wait_vmcnt<0>();
+    f8::lds_barrier();
+    if (more1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
+    }
+    if (more2) issue(kt + 2, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 4; i < 8; ++i) mfma(i, j);
+      __builtin_amdgcn_s_setprio(0);
+      if (more1) fb[j] = wf8::frag(nx + 2 * HB, br + 16 * j, lane);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // epilogue: acc[i][j] lane holds dW[m = mw + 16 i + (lane & 15)][n = nw + 16 j + 4 (lane >> 4) .. +3]
+  const float alpha = 1.f / (args.sa[pr][0] * args.sb[pr][0]);
+  float* __restrict__ Cp = args.C[pr];
+  const int mw = m0 + wm * 128, nw = n0 + wn * 128;
+  const int cl16 = lane & 15, g4 = 4 * (lane >> 4);
+  const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(Cp) & 15) == 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = mw + 16 * i + cl16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = nw + 16 * j + g4;
+      float* c = Cp + (size_t)m * ldc + n;
+      f32x4 v = acc[i][j] * alpha;
+      if (vec && n + 4 <= N) {
+        if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(c);
+        *reinterpret_cast<f32x4*>(c) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < N) c[e] = v[e] + (beta != 0.f ? beta * c[e] : 0.f);
+      }
+    }
+  }
 }
 
 // y8 = e4m3(x * scale[0]); amax_out = max|x| (both optional sides)
@@ -546,6 +1048,25 @@ int launch_f8(const void* A, const void* B, void* C, const float* bias, const fl
   return 0;
 }
 
+template <int EPI, int AF = 0, int CF = 0>
+int launch_f8_w1(const void* A, const void* B, void* C, const float* bias, const float* sa,
+                 const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
+                 int lda, int ldb, int ldc, int ldc8, const F8Extra& ex, hipStream_t st) {
+  constexpr int img = 4 * 128 * (128 * 2 + 16) + 64;  // epilogue images + amax scratch
+  constexpr int lds = std::max(2 * 4 * f8w1::HB, img);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_fp8_w1_kernel<EPI, AF, CF>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int tiles = cdiv(M, 256) * cdiv(N, 256);
+  hipLaunchKernelGGL((gemm_fp8_w1_kernel<EPI, AF, CF>), dim3(tiles), dim3(256), lds, st,
+                     (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C, bias, sa, sb, (uint8_t*)C8,
+                     sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
+  return 0;
+}
+
 template <int EPI>
 int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, const float* sa,
              const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
@@ -560,6 +1081,9 @@ int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, 
     TDG_F8(3, 256, 128, 4, 2, 2)
     TDG_F8(4, 128, 128, 2, 4, 3)
     TDG_F8(8, 256, 128, 4, 2, 3)
+    case 9:  // 256x256, one wave per SIMD (gemm_fp8_w1_kernel)
+      if ((long long)M * lda >= (1LL << 32) || (long long)N * ldb >= (1LL << 32)) return -3;
+      return launch_f8_w1<EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
     default:
       TDG_F8(5, 64, 128, 2, 2, 2)
   }
@@ -570,16 +1094,47 @@ int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, 
 // afmt / cfmt: formats of A and of the C8 copy (0 e4m3, 1 e5m2). The e5m2-A
 // backward GEMMs (ReLU-backward dgrad with an e5m2 copy of its output; the
 // plain dgrad accumulating into C) run on the 128x128 tile only.
+static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float* bias,
+                             const float* sa, const float* sb, void* C8, const float* sc8,
+                             unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
+                             int ldc8, int epi, int cfg, int afmt, int cfmt, const F8Extra& ex,
+                             hipStream_t st);
+
+// aux8: the ReLU-backward mask as 8-bit activations (instead of bf16 aux);
+// colsum_out: also colsum_out[N] (=|+= colsum_beta) the column sums of the
+// stored output (bias gradient), via partials in ws (>= rows * N floats,
+// rows = ceil(M / BM) * WM of the tile config; the 128x128 tile: M / 64).
+// C may be null (then only C8 and / or the column sums are produced).
 extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias,
                             const float* sa, const float* sb, void* C8, const float* sc8,
                             unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
                             int ldc8, int epi, int cfg, int afmt, int cfmt, const void* aux,
-                            int ldaux, float beta, hipStream_t st) {
+                            int ldaux, float beta, const void* aux8, float* colsum_out,
+                            float colsum_beta, float* ws, hipStream_t st) {
   if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
   const int cdeq = (epi & F8_EPI_CDEQ) != 0;
   epi &= ~F8_EPI_CDEQ;
   if (cdeq && !C8) return -2;
-  const F8Extra ex{(const bf16_t*)aux, ldaux, beta, cdeq};
+  if (!C && (beta != 0.f || cdeq)) return -2;
+  if (colsum_out && (!ws || cfg != 0)) return -2;  // (partials: the 128x128 / 2x2 tile)
+  const F8Extra ex{(const bf16_t*)aux, ldaux, beta, cdeq, (const uint8_t*)aux8,
+                   colsum_out ? ws : nullptr};
+  if (colsum_out) {
+    const int rc = tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc,
+                                     ldc8, epi, cfg, afmt, cfmt, ex, st);
+    if (rc) return rc;
+    launch_reduce_partials(ws, colsum_out, N, cdiv(M, 128) * 2, colsum_beta, st);
+    return 0;
+  }
+  return tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, epi,
+                           cfg, afmt, cfmt, ex, st);
+}
+
+static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float* bias,
+                             const float* sa, const float* sb, void* C8, const float* sc8,
+                             unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
+                             int ldc8, int epi, int cfg, int afmt, int cfmt, const F8Extra& ex,
+                             hipStream_t st) {
   if (afmt == 0 && cfmt == 0) {
     switch (epi) {
       case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
@@ -589,6 +1144,12 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
     }
   }
   if (afmt == 1 && cfmt == 1) {
+    if (cfg == 9 && (long long)M * lda < (1LL << 32) && (long long)N * ldb < (1LL << 32)) {
+      if (epi == F8_EPI_DRELU)
+        return launch_f8_w1<F8_EPI_DRELU, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      if (epi == F8_EPI_NONE)
+        return launch_f8_w1<F8_EPI_NONE, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    }
     if (epi == F8_EPI_DRELU)
       return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
     if (epi == F8_EPI_NONE)
@@ -644,5 +1205,50 @@ extern "C" int tdg_fp8_dequant(const void* x8, float* y, long long n, float inv_
                                hipStream_t st) {
   hipLaunchKernelGGL(fp8_dequant_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                      (const uint8_t*)x8, y, n, inv_scale);
+  return 0;
+}
+
+// fp8 weight gradients (wgrad_fp8_kernel): P <= 64 problems sharing the token
+// count T (T % 128 == 0), consecutive problems of equal shape form a class
+// (<= 8 classes). shapes[5 i ..] = (M, N, lda, ldb, ldc); A[i] e5m2 [T][lda],
+// B[i] e4m3 [T][ldb], C[i] f32 [M][ldc]; sa / sb: one-float scales.
+extern "C" int tdg_wgrad_fp8(const void* const* A, const void* const* B, float* const* C,
+                             const float* const* sa, const float* const* sb, int P,
+                             const int* shapes, int T, float beta, hipStream_t st) {
+  if (P < 1 || P > WF8_MAXP || T <= 0 || T % 128) return -2;
+  WF8Args args{};
+  int ncls = 0, tiles = 0;
+  for (int i = 0; i < P; ++i) {
+    const int* s = shapes + 5 * i;
+    const int M = s[0], N = s[1], lda = s[2], ldb = s[3], ldc = s[4];
+    if (M <= 0 || N <= 0 || M % 16 || N % 16 || lda % 16 || ldb % 16 || lda < M || ldb < N)
+      return -3;
+    if ((long long)T * lda >= (1LL << 31) || (long long)T * ldb >= (1LL << 31)) return -9;
+    const bool same = ncls > 0 && args.cls[ncls - 1].M == M && args.cls[ncls - 1].N == N &&
+                      args.cls[ncls - 1].lda == lda && args.cls[ncls - 1].ldb == ldb &&
+                      args.cls[ncls - 1].ldc == ldc;
+    if (!same) {
+      if (ncls == WF8_MAXC) return -5;
+      WF8Class& c = args.cls[ncls++];
+      c.M = M; c.N = N; c.lda = lda; c.ldb = ldb; c.ldc = ldc;
+      c.tiles_m = cdiv(M, 256); c.tiles_n = cdiv(N, 256);
+      c.tile_start = tiles; c.prob_start = i;
+    }
+    tiles += cdiv(M, 256) * cdiv(N, 256);
+    args.A[i] = (const uint8_t*)A[i];
+    args.B[i] = (const uint8_t*)B[i];
+    args.C[i] = C[i];
+    args.sa[i] = sa[i];
+    args.sb[i] = sb[i];
+  }
+  args.ncls = ncls;
+  constexpr int lds = 2 * 4 * f8w1::HB;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)wgrad_fp8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad_fp8_kernel, dim3(tiles), dim3(256), lds, st, args, T, beta);
   return 0;
 }

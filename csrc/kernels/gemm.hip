@@ -16,7 +16,7 @@ namespace tdg {
                           int ldc, bool f32, float alpha, float beta, int tile_cfg,              \
                           hipStream_t st);                                                       \
   int gemm_ragged_##NAME(const R256Args& args, int tiles, int K, bool f32, float alpha,         \
-                         float beta, hipStream_t st);
+                         float beta, int impl, hipStream_t st);
 TDG_DECL(nt)
 TDG_DECL(nn)
 TDG_DECL(tn)
@@ -170,7 +170,8 @@ extern "C" int tdg_gemm_grouped(const void* const* A, const void* const* B, void
 // problem is a run of its own). Returns 0 on success.
 extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, int P,
                                const int* shapes, int K, int a_kc, int b_kc, int out_f32,
-                               float alpha, float beta, float* const* bias_out, hipStream_t st) {
+                               float alpha, float beta, float* const* bias_out, int impl,
+                               hipStream_t st) {
   if (P < 1 || P > R256_MAXP) return -2;
   R256Args args{};
   int ncls = 0, tiles = 0;
@@ -201,9 +202,10 @@ extern "C" int tdg_gemm_ragged(const void* const* A, const void* const* B, void*
     if (args.bias_out[i] && a_kc) return -7;  // row sums need the MN-contiguous A path
   }
   args.ncls = ncls;
-  if (a_kc && b_kc) return gemm_ragged_nt(args, tiles, K, out_f32 != 0, alpha, beta, st);
-  if (a_kc && !b_kc) return out_f32 ? -4 : gemm_ragged_nn(args, tiles, K, false, alpha, beta, st);
-  if (!a_kc && !b_kc) return gemm_ragged_tn(args, tiles, K, out_f32 != 0, alpha, beta, st);
+  if (impl != 0 && (a_kc || b_kc)) return -4;  // (pipelined: TN weight gradients only)
+  if (a_kc && b_kc) return gemm_ragged_nt(args, tiles, K, out_f32 != 0, alpha, beta, 0, st);
+  if (a_kc && !b_kc) return out_f32 ? -4 : gemm_ragged_nn(args, tiles, K, false, alpha, beta, 0, st);
+  if (!a_kc && !b_kc) return gemm_ragged_tn(args, tiles, K, out_f32 != 0, alpha, beta, impl, st);
   return -4;
 }
 

@@ -517,6 +517,116 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Ragged weight-gradient launch on the software-pipelined main loop (Pipe,
+// gemm_pipe.h) at ONE wave per SIMD: 256x256 tiles, 2 x 2 waves of 128 x 128
+// (the 8 x 8 accumulator fragments live in AGPRs), 32-deep K tiles in an
+// NS-slot LDS-DMA ring. Per FLOP a 128 x 128 wave tile reads 2/3 of the LDS
+// fragment bytes of the lock-step kernel's 128 x 64, and nothing waits in
+// bulk (fragment reads and DMA issue behind the MFMA rows). TN only (both
+// operands token-major: dY^T, X), f32 out (alpha, beta), fused bias sums for
+// the tiles of the first N-column (the wn == 0 waves sum their A fragments).
+template <int NS>
+__global__ __launch_bounds__(256) void wgrad_pipe_kernel(const R256Args args, int K, float alpha,
+                                                         float beta) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 2;
+  using P = Pipe<BM, BN, WM, WN, NS, false, false>;
+  constexpr int TM = P::TM, TN = P::TN, A_BYTES = P::A_BYTES, PT = P::PT;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  static_assert(NS >= 3, "ring: refilled, being read, landed");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  R256Class cl = args.cls[0];
+#pragma unroll
+  for (int i = 1; i < R256_MAXC; ++i)
+    if (i < args.ncls && t0 >= args.cls[i].tile_start) cl = args.cls[i];
+  const int M = cl.M, N = cl.N, lda = cl.lda, ldb = cl.ldb, ldc = cl.ldc;
+  const int tpp = cl.tiles_m * cl.tiles_n;
+  const int lt = t0 - cl.tile_start + cl.t_first;
+  const int p = cl.prob_start + lt / tpp;
+  const int t = lt % tpp;
+  int tm, tn;
+  if (cl.tiles_n <= cl.tiles_m) {
+    tn = t % cl.tiles_n;
+    tm = t / cl.tiles_n;
+  } else {
+    tm = t % cl.tiles_m;
+    tn = t / cl.tiles_m;
+  }
+  float* __restrict__ bias_out = args.bias_out[p];
+  const bool do_bs = bias_out != nullptr && tn == 0 && wn == 0;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / PK;
+
+  typename P::SA sa;
+  typename P::SBt sb;
+  // byte extents of the MN-contiguous operands ([K][ld]) for the buffer resources
+  sa.init(args.A[p], lda, M, m0, (int)(((long long)(K - 1) * lda + M) * 2), wid, lane);
+  sb.init(args.B[p], ldb, N, n0, (int)(((long long)(K - 1) * ldb + N) * 2), wid, lane);
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bs[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bs[i] = 0.f;
+
+  const int abase = wm * WTM, bbase = wn * WTN;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) P::stage(sa, sb, smem, s, wid);
+  wait_tiles<PT, NS - 2>(min(NS - 1, nk) - 1);
+  __builtin_amdgcn_s_barrier();
+  typename P::FA fa[TM];
+  typename P::FBt fb[TN], fbn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    lgkm_wait<15 - P::FBt::NI>();
+    fb[j].read(smem + A_BYTES, bbase + 16 * j, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    lgkm_wait<15 - P::FA::NI>();
+    fa[i].read(smem, abase + 16 * i, lane);
+  }
+  if (NS - 1 < nk) P::stage(sa, sb, smem, NS - 1, wid);
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    P::template ktile_bs<true>(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase, bs, do_bs);
+    P::template ktile_bs<true>(kt + 1, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase, bs, do_bs);
+  }
+  if (kt < nk)
+    P::template ktile_bs<true>(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase, bs, do_bs);
+
+  if (do_bs) {  // lanes l, l+16, l+32, l+48 hold disjoint k subsets of row l & 15
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float b = bs[i];
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      const int m = m0 + abase + 16 * i + lane;
+      if (lane < 16 && m < M) bias_out[m] = alpha * b + (beta != 0.f ? beta * bias_out[m] : 0.f);
+    }
+  }
+
+  lgkm_wait<0>();
+  wait_vmcnt<0>();
+  lds_barrier();
+  {
+    using Epi = EpiLds<EPI_NONE, true, TM, TN, 32>;
+    static_assert(4 * Epi::BYTES <= NS * P::SB, "epilogue images fit in the stages");
+    void* Cv = args.C[p];
+    Epi::run(smem + wid * Epi::BYTES, acc, lane, Cv, ldc, M, N, m0 + wm * WTM, n0 + wn * WTN, alpha,
+             beta, nullptr, nullptr, 0, epi_vec_ok<EPI_NONE, true>(Cv, ldc, nullptr, 0));
+  }
+}
+
 // Split-K reduction: C = sum_z slab[z] (+beta*C) with the epilogue.
 template <int EPI, bool OUT_F32>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, void* __restrict__ Cv,
@@ -621,6 +731,29 @@ int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t*
   }
 }
 
+// Ragged TN weight gradients on the one-wave-per-SIMD pipelined loop (f32 out).
+template <int NS>
+int launch_wgrad_pipe(const R256Args& args, int tiles, int K, float alpha, float beta,
+                      hipStream_t st) {
+  if (K % PK != 0 || K <= 0 || tiles <= 0) return -3;
+  for (int c = 0; c < args.ncls; ++c) {
+    const R256Class& cl = args.cls[c];
+    if (cl.lda % 8 || cl.ldb % 8) return -6;
+    if (((long long)(K - 1) * cl.lda + cl.M) * 2 >= 0x7fffffffLL ||
+        ((long long)(K - 1) * cl.ldb + cl.N) * 2 >= 0x7fffffffLL)
+      return -9;
+  }
+  constexpr int lds = NS * (256 + 256) * PK * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_pipe_kernel<NS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((wgrad_pipe_kernel<NS>), dim3(tiles), dim3(256), lds, st, args, K, alpha, beta);
+  return 0;
+}
+
 // One shape class of G problems (G == 1: a plain GEMM). Returns the tile count.
 inline int r256_single(R256Args& a, const bf16_t* const* A, const bf16_t* const* B,
                        void* const* C, int G, int M, int N, int lda, int ldb, int ldc) {
@@ -668,7 +801,7 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
                   const bf16_t* aux, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
                   float alpha, float beta, int splits, float* ws, hipStream_t st,
                   const GemmGroup* grp = nullptr, int G = 1) {
-  if (tile_cfg >= 20 && tile_cfg <= 24) {
+  if (tile_cfg >= 20 && tile_cfg <= 26) {
     // software-pipelined kernel (one problem, no split-K); else cfg 0
     if (!grp && splits <= 1) {
       bool ok = false;
@@ -684,6 +817,8 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
         // one wave per SIMD, 128x128 per wave (accumulators beyond 256 VGPRs)
         TDG_PIPE(23, 256, 256, 2, 2, 4)
         TDG_PIPE(24, 256, 256, 2, 2, 5)
+        TDG_PIPE(25, 256, 128, 2, 2, 6)
+        TDG_PIPE(26, 128, 256, 2, 2, 6)
         default: break;
       }
 #undef TDG_PIPE
@@ -784,7 +919,11 @@ int dispatch_epi(int epi, bool f32, int tile_cfg, const bf16_t* A, const bf16_t*
     return 0;                                                                                   \
   }                                                                                             \
   int gemm_ragged_##NAME(const R256Args& args, int tiles, int K, bool f32, float alpha,         \
-                         float beta, hipStream_t st) {                                          \
+                         float beta, int impl, hipStream_t st) {                                \
+    if constexpr (!AK && !BKc) {                                                                \
+      if (f32 && impl == 1) return launch_wgrad_pipe<4>(args, tiles, K, alpha, beta, st);       \
+      if (f32 && impl == 2) return launch_wgrad_pipe<5>(args, tiles, K, alpha, beta, st);       \
+    }                                                                                           \
     if (f32)                                                                                    \
       return launch_256<AK, BKc, EPI_NONE, true>(args, tiles, nullptr, nullptr, K, 0, alpha, beta, \
                                                 st);                                             \

@@ -198,6 +198,20 @@ struct Pipe {
                                                f32x4 (&acc)[TM][TN], const SA& sa, const SBt& sb,
                                                char* smem, int lane, int wid, int abase,
                                                int bbase) {
+    float none[TM];
+    ktile_bs<false>(kt, nk, FB, FN, fa, acc, sa, sb, smem, lane, wid, abase, bbase, none, false);
+  }
+  // BS: also accumulate the sums over k of the A fragments (bs[i]: row
+  // abase + 16 i + (lane & 15), this lane's k subset) when do_bs -- the fused
+  // bias gradient of a weight-gradient tile (A = dY^T), from registers the
+  // MFMAs already hold
+  template <bool BS>
+  static __device__ __forceinline__ void ktile_bs(int kt, int nk, FBt (&FB)[TN],
+                                                  FBt (&FN)[TN], FA (&fa)[TM],
+                                                  f32x4 (&acc)[TM][TN], const SA& sa,
+                                                  const SBt& sb, char* smem, int lane, int wid,
+                                                  int abase, int bbase, float (&bs)[TM],
+                                                  bool do_bs) {
     if (kt + 1 < nk) {
       // tile kt+1 landed (this wave's pieces), then everyone's; every wave
       // also finished reading tile kt-1, whose slot is refilled below.
@@ -229,6 +243,17 @@ struct Pipe {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(FB[j].get(), a, acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (BS) {
+        if (do_bs) {
+          const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3f803f80);
+          float b = bs[i];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            b = __builtin_amdgcn_fdot2_f32_bf16(
+                __builtin_bit_cast(bf16x2_t, (short2_t){a[2 * e], a[2 * e + 1]}), one, b, false);
+          bs[i] = b;
+        }
+      }
       throttle<FA>();
       fa[i].read(nx, abase + 16 * i, lane);
       // this wave's DMA pieces of tile rt, spread over the MFMA rows

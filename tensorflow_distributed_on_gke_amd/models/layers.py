@@ -149,9 +149,10 @@ class WgradQueue:
         # deferred LayerNorm dgamma/dbeta/bias partial folds (one launch per flush)
         self.reductions = []
         self.reduced_params = []
+        self.fp8_items = []
 
     def boundary(self) -> None:
-        if self.flush_at_boundary and not self._chunking() and (self.items or self.reductions):
+        if self.flush_at_boundary and not self._chunking() and (self.items or self.reductions or self.fp8_items):
             self.flush()
 
     @staticmethod
@@ -171,6 +172,8 @@ class WgradQueue:
         """A decoder or encoder layer's backward is complete."""
         self._layer_ends += 1
         last = self.layers_per_step > 0 and self._layer_ends >= self.layers_per_step
+        if self._chunking() and self.fp8_items:
+            self._flush_fp8()  # (its gradients join the next all-reduce span)
         if not self._chunking() or not self.items:
             return
         if last or not all(self._ragged_ok(it) for it in self.items):
@@ -185,11 +188,32 @@ class WgradQueue:
     def add(self, dy2, x2, N, w: Param, b: Optional[Param], beta: float, rt: "RunCtx"):
         self.items.append((dy2, x2, N, w, b, beta, rt))
 
+    def add_fp8(self, dy8, sa, x8, sb, w: Param, beta: float, rt: "RunCtx"):
+        """An fp8 weight gradient (ops.fp8.wgrad_fp8), launched with the
+        next flush / layer end as one ragged fp8 launch."""
+        self.fp8_items.append((dy8, sa, x8, sb, w, beta, rt))
+
+    def _flush_fp8(self) -> None:
+        if not self.fp8_items:
+            return
+        by_beta = {}
+        for it in self.fp8_items:
+            by_beta.setdefault(it[5], []).append(it)
+        for beta, its in by_beta.items():
+            # equal shapes adjacent (one class each)
+            its.sort(key=lambda it: (it[4].shape, it[0].stride(0), it[2].stride(0)))
+            fp8.wgrad_fp8([it[0] for it in its], [it[1] for it in its], [it[2] for it in its],
+                          [it[3] for it in its], [it[4].grad for it in its], beta)
+        for it in self.fp8_items:
+            _ready(it[6], it[4])
+        self.fp8_items = []
+
     def step_done(self) -> None:
         """End of a backward: the layer-end count restarts."""
         self._layer_ends = 0
 
     def flush(self) -> None:
+        self._flush_fp8()
         if self.items:
             if RAGGED_WGRAD and all(self._ragged_ok(it) for it in self.items):
                 self._launch_prefix(sum(self._tiles(it) for it in self.items) - self._cursor)
@@ -666,6 +690,8 @@ class FFNBlockFn(torch.autograd.Function):
         x2 = x.reshape(B * L, d)
         ctx.p = (w1, b1, w2, b2, gamma, beta)
         ctx.meta = (site, rt)
+        ctx.f8 = None
+        ctx.lean = False
         if x.is_cuda and rt.fp8 is not None:
             st = rt.fp8
             xs, hs = st.ffn_slots[id(w1)]
@@ -675,8 +701,17 @@ class FFNBlockFn(torch.autograd.Function):
             if x8 is None:
                 x8 = fp8.quantize(x2, st.meta, xs)
             x8 = x8.view(x2.shape)
-            h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs)
+            # lean: the backward runs entirely on the e4m3 copies (fp8 weight
+            # gradients, ReLU mask from h8), so the bf16 hidden is not written
+            lean = (rt.training and rt.wgrad is not None and fp8.WGRAD_FP8
+                    and st.ffn_bwd_slots.get(id(w1)) is not None
+                    and fp8.wgrad_fp8_ok(B * L, d, w1.shape[0]))
+            h, h8 = fp8.gemm_fp8(x8, w1_8, b1.master, st.meta, xs, s1, relu=True, out8_slot=hs,
+                                 want_y=not lean)
             f, _ = fp8.gemm_fp8(h8, w2_8, b2.master, st.meta, hs, s2)
+            # the e4m3 copies feed the fp8 weight gradients of the backward
+            ctx.f8 = (x8, h8) if rt.training else None
+            ctx.lean = lean
         elif x.is_cuda:
             h = K.linear_fwd(x2, w1.compute, b1.master, relu=True)
             f = None  # second projection fused with the LayerNorm below
@@ -687,7 +722,7 @@ class FFNBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(h, w2, b2, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, f.view(B, L, d), gamma, beta, site, rt)
-        ctx.save_for_backward(x2, h)
+        ctx.save_for_backward(x2, h if h is not None else x2)  # (lean: h unused)
         return y
 
     @staticmethod
@@ -696,13 +731,15 @@ class FFNBlockFn(torch.autograd.Function):
         site, rt = ctx.meta
         x2, h = ctx.saved_tensors
         B, L, d = dy.shape
-        ff = h.shape[1]
+        ff = w1.shape[0]
         bt = _beta(rt)
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
-            _wgrad(rt, ds2, h, d, w2)
             bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if rt.fp8 is not None else None
+            f8w = ctx.lean
+            if not f8w:
+                _wgrad(rt, ds2, h, d, w2)
             if bw is not None:
                 # fp8 backward: e5m2 gradients x e4m3 transposed weights on the
                 # block-scaled MFMA; the ReLU-backward dgrad also emits the e5m2
@@ -714,10 +751,26 @@ class FFNBlockFn(torch.autograd.Function):
                 ds8 = fp8.quantize(ds2, st.gmeta, gs)
                 w2t8, s2t = st.weights.get(w2, transposed=True)
                 w1t8, s1t = st.weights.get(w1, transposed=True)
-                dpre = torch.empty(M, ff, dtype=ds2.dtype, device=ds2.device)
-                dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, dpre, relu_aux=h,
-                                           out8_slot=gh)
-                _wgrad(rt, dpre, x2, ff, w1, b1)
+                if f8w:
+                    # lean fp8 backward: the ReLU-backward dgrad writes only
+                    # the e5m2 dpre8 and, from its epilogue, b1's gradient
+                    # (column sums); the mask is the forward's e4m3 hidden h8;
+                    # weight gradients: e5m2 gradients x the forward's e4m3
+                    # inputs (FFN1 input x8, hidden h8), token-major
+                    x8, h8 = ctx.f8
+                    xs, hs = st.ffn_slots[id(w1)]
+                    dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, None,
+                                               relu_aux8=h8.view(M, ff), out8_slot=gh,
+                                               colsum_out=b1.grad, colsum_beta=bt)
+                    _ready(rt, b1)
+                    q = rt.wgrad
+                    q.add_fp8(ds8.view(M, d), st.gmeta.s(gs), h8.view(M, ff), st.meta.s(hs), w2, bt, rt)
+                    q.add_fp8(dpre8.view(M, ff), st.gmeta.s(gh), x8.view(M, d), st.meta.s(xs), w1, bt, rt)
+                else:
+                    dpre = torch.empty(M, ff, dtype=ds2.dtype, device=ds2.device)
+                    dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, dpre, relu_aux=h,
+                                               out8_slot=gh)
+                    _wgrad(rt, dpre, x2, ff, w1, b1)
                 fp8.gemm_bf8_dgrad(dpre8, st.gmeta, gh, w1t8, st.meta, s1t, dh.view(M, d), beta=1.0)
                 return (dh.view(B, L, d),) + (None,) * 8
             if w2.compute_t is not None:  # NT layout against W2^T (ParamStore.add_transposed)

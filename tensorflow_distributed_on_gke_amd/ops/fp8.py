@@ -14,8 +14,11 @@ epilogue), e4m3 x e4m3 GEMM on the block-scaled MFMA (csrc/kernels/fp8.hip),
 bf16 out. Backward (`Fp8State(backward=True)`): the two FFN dgrads run as
 e5m2-gradient x e4m3-transposed-weight GEMMs (the ReLU-backward one emits the
 e5m2 copy of its output for the other, which accumulates the residual
-gradient); gradient scales live in a second, e5m2 `Fp8Meta`. Weight
-gradients, the attention backward and the optimizer stay bf16 / fp32.
+gradient); gradient scales live in a second, e5m2 `Fp8Meta`. The FFN weight
+gradients run in fp8 too (`wgrad_fp8`: e5m2 gradient x the forward's e4m3
+activation copy, both token-major, through the transposing LDS reads); the
+attention backward, the other weight gradients and the optimizer stay bf16 /
+fp32.
 Measured on Transformer-big seq 512: 14.77-14.83 vs 14.85-14.99 ms/step with
 the FFN backward in bf16 (profiles/r3s2/fp8_backward_ab.txt).
 """
@@ -34,7 +37,11 @@ BF8 = torch.float8_e5m2  # gradient format of the fp8 backward
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
 AMAX_WORDS = 64 * 32  # per slot (csrc/include/tdg_common.h AMAX_WORDS)
-_CANDS = (0, 1, 2, 3, 4, 5, 8)
+_CANDS = (0, 1, 2, 3, 4, 5, 8, 9)
+# FFN weight gradients in fp8 (wgrad_fp8) when the step runs the fp8 backward
+WGRAD_FP8 = True
+# tile config of the e5m2 x e4m3 backward GEMMs (0: 128x128 / 4 waves; 9: 256x256 at one wave per SIMD)
+BWD_CFG = 0
 _TUNED: Dict[tuple, int] = {}
 
 
@@ -87,21 +94,24 @@ def dequantize(x8: torch.Tensor, scale: float) -> torch.Tensor:
 
 
 def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
-             out8_slot: Optional[int] = None, cfg: Optional[int] = None, c_deq: bool = False
-             ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+             out8_slot: Optional[int] = None, cfg: Optional[int] = None, c_deq: bool = False,
+             want_y: bool = True) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """y[M,N] = dequant(a8[M,K] @ b8[N,K]^T) + bias (relu), bf16, on the
     block-scaled e4m3 MFMA (csrc/kernels/fp8.hip); with out8_slot also
     y8 = e4m3(y * scale[out8_slot]) (amax recorded). c_deq (needs out8_slot):
     y = y8 / scale instead, the exact values the e4m3 consumer of y8 sees
     (scales are powers of two), so a backward reading y is consistent with
-    a forward that ran on y8."""
+    a forward that ran on y8. want_y = False (needs out8_slot): only y8 is
+    written (y is None)."""
     M, Kd = a8.shape
     N = b8.shape[0]
     y8 = torch.empty(M, N, dtype=FP8, device=a8.device) if out8_slot is not None else None
     if c_deq and y8 is None:
         raise ValueError("gemm_fp8: c_deq needs out8_slot")
+    if not want_y and (y8 is None or c_deq):
+        raise ValueError("gemm_fp8: want_y=False needs out8_slot and no c_deq")
     epi = (2 if relu else (1 if bias is not None else 0)) | (16 if c_deq else 0)
-    y = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=a8.device) if want_y else None
 
     def run(c):
         C().gemm_fp8(a8, b8, y, bias, meta.s(ia), meta.s(ib), y8,
@@ -110,7 +120,7 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
                      M, N, Kd, a8.stride(0), b8.stride(0), N, N, epi, c, 0, 0, None, 0, 0.0)
 
     if cfg is None:
-        key = (M, N, Kd, epi, y8 is not None)
+        key = (M, N, Kd, epi, y8 is not None, want_y)
         cfg = _TUNED.get(key)
         if cfg is None:
             if K.AUTOTUNE and a8.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -123,21 +133,51 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
 
 
 def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8t, wmeta: Fp8Meta, iw: int,
-                   out: torch.Tensor, relu_aux: Optional[torch.Tensor] = None, beta: float = 0.0,
-                   out8_slot: Optional[int] = None) -> Optional[torch.Tensor]:
+                   out: Optional[torch.Tensor], relu_aux: Optional[torch.Tensor] = None,
+                   beta: float = 0.0, out8_slot: Optional[int] = None, cfg: Optional[int] = None,
+                   relu_aux8: Optional[torch.Tensor] = None, colsum_out: Optional[torch.Tensor] = None,
+                   colsum_beta: float = 0.0) -> Optional[torch.Tensor]:
     """Backward GEMM on the block-scaled MFMA: out[M,N] (=|+= beta) dequant(
     g8[M,K] (e5m2 gradient) @ w8t[N,K]^T (e4m3 transposed weight)), bf16;
-    relu_aux: zero where relu_aux <= 0 (ReLU backward); out8_slot: also the
-    e5m2 copy of out in gmeta's slot (returned, amax recorded)."""
+    relu_aux: zero where relu_aux <= 0 (ReLU backward), or relu_aux8: zero
+    where the e4m3 ReLU output is 0; out8_slot: also the e5m2 copy of out in
+    gmeta's slot (returned, amax recorded); colsum_out[N] (=|+= colsum_beta):
+    the column sums of the (bf16-rounded) output -- a bias gradient -- from
+    the epilogue (128x128 tiles). out may be None (nothing but the e5m2 copy
+    and the sums is written)."""
     M, Kd = g8.shape
     N = w8t.shape[0]
     o8 = torch.empty(M, N, dtype=BF8, device=g8.device) if out8_slot is not None else None
+    aux = relu_aux if relu_aux is not None else relu_aux8
+    c = BWD_CFG if cfg is None else cfg
+    ws = None
+    if colsum_out is not None:
+        c = 0
+        ws = K.workspace("fp8_colsum", math.ceil(M / 128) * 2 * N, g8.device)
     C().gemm_fp8(g8, w8t, out, None, gmeta.s(ig), wmeta.s(iw), o8,
                  gmeta.s(out8_slot) if o8 is not None else None,
                  gmeta.a(out8_slot) if o8 is not None else None,
-                 M, N, Kd, g8.stride(0), w8t.stride(0), out.stride(0), N, 3 if relu_aux is not None else 0,
-                 0, 1, 1, relu_aux, relu_aux.stride(0) if relu_aux is not None else 0, beta)
+                 M, N, Kd, g8.stride(0), w8t.stride(0), out.stride(0) if out is not None else N, N,
+                 3 if aux is not None else 0, c, 1, 1, relu_aux,
+                 aux.stride(0) if aux is not None else 0, beta, aux8=relu_aux8,
+                 colsum_out=colsum_out, colsum_beta=colsum_beta, ws=ws)
     return o8
+
+
+def wgrad_fp8(dy8s, sas, x8s, sbs, dws, beta: float = 0.0) -> None:
+    """dws[i][M,N] (f32, =|+= beta) = dequant(dy8s[i][T,M]^T @ x8s[i][T,N]):
+    weight gradients from the e5m2 gradient and the e4m3 activation copies
+    the step already holds (token-major, read through the transposing LDS
+    path: csrc/kernels/fp8.hip wgrad_fp8_kernel), one launch per 64
+    problems. sas / sbs: the one-element scale tensors of each operand."""
+    for c0 in range(0, len(dws), 64):
+        sl = slice(c0, c0 + 64)
+        C().wgrad_fp8(list(dy8s[sl]), list(x8s[sl]), list(dws[sl]), list(sas[sl]), list(sbs[sl]),
+                      float(beta))
+
+
+def wgrad_fp8_ok(T: int, M: int, N: int) -> bool:
+    return T % 128 == 0 and M % 16 == 0 and N % 16 == 0
 
 
 def choose_fp8(M: int, N: int, Kd: int) -> int:

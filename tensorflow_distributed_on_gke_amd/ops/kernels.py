@@ -300,6 +300,10 @@ def wgrad_grouped(dys, xs, dws, beta: float = 0.0) -> None:
 
 
 RAGGED_MAX_PROBLEMS, RAGGED_MAX_SHAPES = 64, 8
+# main loop of the ragged weight-gradient launch: 0 = lock-step 256x256 tiles
+# at 2 waves per SIMD (gemm256_kernel), 1 / 2 = the pipelined loop at one wave
+# per SIMD with a 4 / 5-slot LDS ring (wgrad_pipe_kernel)
+WGRAD_IMPL = 0
 
 
 def wgrad_ragged(dys, xs, dws, beta: float = 0.0, biases=None, ranges=None) -> None:
@@ -321,7 +325,7 @@ def wgrad_ragged(dys, xs, dws, beta: float = 0.0, biases=None, ranges=None) -> N
         shapes += [dw.shape[0], x.shape[1], dy.stride(0), x.stride(0), dw.stride(0)]
         shapes += [0, -1] if r is None else [int(r[0]), int(r[1])]
     C().gemm_ragged(list(dys), list(xs), list(dws), shapes, M, False, False, 1.0, beta,
-                    list(biases) if biases is not None else [])
+                    list(biases) if biases is not None else [], impl=WGRAD_IMPL)
 
 
 def colsum_grouped(xs, outs, beta: float = 0.0) -> None:

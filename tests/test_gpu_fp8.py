@@ -32,7 +32,8 @@ def test_quantize_matches_torch_e4m3():
     assert meta.amax_values()[i].item() == 0.0
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (8192, 2048, 512), (64, 64, 128)])
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (8192, 2048, 512), (64, 64, 128),
+                                   (700, 600, 1024)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_fp8(M, N, K, epi):
     torch.manual_seed(0)
@@ -71,9 +72,10 @@ def test_quantize_matches_torch_e5m2():
     assert meta.scale[i].item() == 2.0 ** math.floor(math.log2(57344.0 / 30.0))
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128)])
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128), (600, 520, 1024)])
 @pytest.mark.parametrize("relu,beta", [(True, 0.0), (False, 1.0)])
-def test_gemm_bf8_dgrad(M, N, K, relu, beta):
+@pytest.mark.parametrize("cfg", [0, 9])
+def test_gemm_bf8_dgrad(M, N, K, relu, beta, cfg):
     """out (=|+= beta) dequant(g8 e5m2 @ w8t e4m3^T), ReLU-backward mask, and
     the e5m2 copy of the output, against an fp32 reference."""
     torch.manual_seed(1)
@@ -90,7 +92,7 @@ def test_gemm_bf8_dgrad(M, N, K, relu, beta):
         ref = ref * (aux.float() > 0)
     ref = ref + beta * out.float()
     o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux=aux, beta=beta,
-                          out8_slot=io if relu else None)
+                          out8_slot=io if relu else None, cfg=cfg)
     err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
     assert err < 1e-2, err
     if relu:
@@ -298,3 +300,90 @@ def test_fp8_attention_gradients_consistent(causal, Lq, Lk):
         # the only roundings left (a P inconsistent with the forward's LSE
         # shows as errors of order 1)
         assert err < 5e-2, (name, err)
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_fp8_ragged(beta):
+    """fp8 weight gradients (transposing-read TN kernel): e5m2 dY^T x e4m3 X
+    over tokens, several shape classes in one launch (incl. a strided view and
+    a non-multiple-of-256 size), against fp32 of the dequantised operands."""
+    torch.manual_seed(11)
+    T = 1024
+    specs = [(1024, 256), (1024, 256), (256, 1024), (512, 512), (272, 400)]
+    gm, am = F.Fp8Meta(DEV, fmt=1), F.Fp8Meta(DEV)
+    dys, xs, dws, sas, sbs, refs = [], [], [], [], [], []
+    for i, (M, N) in enumerate(specs):
+        ga, ab = gm.slot(f"g{i}"), am.slot(f"x{i}")
+        gm.scale[ga], am.scale[ab] = 2.0 ** (12 + i % 3), 2.0 ** (4 - i % 2)
+        ld = M + 64 if i == 3 else M
+        dy = (torch.randn(T, ld, device=DEV) * 1e-3).bfloat16()
+        x = torch.randn(T, N, device=DEV).bfloat16()
+        dy8 = F.quantize(dy, gm, ga).view(T, ld)[:, :M]
+        x8 = F.quantize(x, am, ab).view(T, N)
+        dw = torch.randn(M, N, device=DEV)
+        refs.append((dy8.float() / gm.scale[ga]).t() @ (x8.float() / am.scale[ab]) + beta * dw)
+        dys.append(dy8), xs.append(x8), dws.append(dw), sas.append(gm.s(ga)), sbs.append(am.s(ab))
+    F.wgrad_fp8(dys, sas, xs, sbs, dws, beta)
+    for i, (dw, ref) in enumerate(zip(dws, refs)):
+        err = (dw - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+        assert err < 1e-4, (i, specs[i], err)
+
+
+def test_fp8_ffn_wgrad_matches_bf16_path(monkeypatch):
+    """The FFN weight gradients of an fp8 step: fp8 path vs the bf16 ragged
+    path on the same (e4m3-rounded) forward -- within fp8 gradient noise."""
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
+
+    cfg = model_config("tiny", src_vocab=64, tgt_vocab=64, dropout=0.0)
+    data = SyntheticPairs(batch=16, src_len=16, tgt_len=17, src_vocab=64, tgt_vocab=64, copy_task=True, seed=0)
+    src, tgt = (t.cuda() for t in data.batch(0))
+    grads = {}
+    for mode in (False, True):
+        monkeypatch.setattr(F, "WGRAD_FP8", mode)
+        m = Transformer(cfg).build("cuda", seed=1)
+        st = F.Fp8State(m)
+        rt = RunCtx(training=True, dropout=0.0, seed=3, store=m.store, fp8=st,
+                    ctr=torch.zeros(1, dtype=torch.int64, device="cuda"))
+        rt.wgrad = WgradQueue()
+        rt.wgrad.layers_per_step = 2 * cfg.layers
+        m.loss_and_backward(src, tgt, rt, 1.0)
+        torch.cuda.synchronize()
+        grads[mode] = {n: p.grad.clone() for n, p in ((l.ff1.w.name, l.ff1.w) for l in m.enc_layers)}
+        grads[mode].update({l.ff2.w.name: l.ff2.w.grad.clone() for l in m.enc_layers})
+    for n, g16 in grads[False].items():
+        g8 = grads[True][n]
+        rel = ((g8 - g16).norm() / g16.norm()).item()
+        assert rel < 0.1, (n, rel)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (1024, 4096, 1024)])
+@pytest.mark.parametrize("with_c", [True, False])
+def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c):
+    """The lean fp8 FFN backward's ReLU-backward dgrad: mask from the e4m3
+    hidden (h8 != 0), optional bf16 output, e5m2 copy, and the bias gradient
+    (column sums of the bf16-rounded output, accumulated with beta) from the
+    epilogue partials."""
+    torch.manual_seed(4)
+    wm, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
+    iw, ig, io, ih = wm.slot("w"), gm.slot("g"), gm.slot("o"), wm.slot("h")
+    wm.scale[iw], gm.scale[ig], gm.scale[io], wm.scale[ih] = 512.0, 2.0 ** 20, 2.0 ** 10, 8.0
+    g = (torch.randn(M, K, device=DEV) * 1e-3).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    h = torch.relu(torch.randn(M, N, device=DEV)).bfloat16()
+    h8 = F.quantize(h, wm, ih).view(M, N)
+    g8, w8 = F.quantize(g, gm, ig), F.quantize(w, wm, iw)
+    ref = ((g8.float() / 2.0 ** 20) @ (w8.float() / 512.0).t()) * (h8.float() != 0)
+    out = torch.empty(M, N, device=DEV).bfloat16() if with_c else None
+    bsum = torch.randn(N, device=DEV)
+    bref = bsum + ref.bfloat16().float().sum(0)
+    o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux8=h8, out8_slot=io,
+                          colsum_out=bsum, colsum_beta=1.0)
+    o8ref = (ref * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
+    assert (o8.view(torch.uint8) == o8ref.view(torch.uint8)).float().mean().item() > 0.995
+    if with_c:
+        err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+        assert err < 1e-2, err
+    berr = (bsum - bref).abs().max().item() / (bref.abs().max().item() + 1e-12)
+    assert berr < 1e-3, berr

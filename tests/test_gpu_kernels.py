@@ -140,9 +140,12 @@ def test_gemm256_nn_tn(M, N, K, beta, cfg):
     _close(y, ref, 1e-2, "gemm256 NT bias relu")
 
 
-def test_wgrad_ragged():
+@pytest.mark.parametrize("impl", [0, 1, 2])
+def test_wgrad_ragged(impl, monkeypatch):
     """All deferred weight gradients of a model in ONE ragged 256x256 launch:
-    5 shapes (incl. a padded-vocab operand, ld 7040 for 7010 rows), 17 problems."""
+    5 shapes (incl. a padded-vocab operand, ld 7040 for 7010 rows), 17 problems.
+    impl 0: lock-step loop; 1 / 2: pipelined loop at one wave per SIMD."""
+    monkeypatch.setattr(kk, "WGRAD_IMPL", impl)
     T = 512
     spec = [(1536, 512)] * 3 + [(512, 512)] * 6 + [(2048, 512)] * 3 + [(512, 2048)] * 4 + [(7010, 512)]
     dys, xs, dws, refs = [], [], [], []
