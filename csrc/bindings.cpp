@@ -32,7 +32,8 @@ int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float
                const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, int accumulate, int skip_reduce,
-               int rpb, hipStream_t st);
+               int rpb, void* ds8, const float* s8, unsigned* amax8,
+               hipStream_t st);
 int tdg_reduce_partials_multi(const float* const* parts, float* const* outs, const int* nparts,
                               int G, int N, float beta, hipStream_t st);
 int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe, void* out, int M,
@@ -441,7 +442,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
             const optional<Tensor>& dres, const Tensor& dgamma, const Tensor& dbeta,
             const optional<Tensor>& dbias, const Tensor& ws, double p, int64_t seed,
             const optional<Tensor>& ctr, int64_t site, bool accumulate, bool skip_reduce,
-            int64_t rpb) {
+            int64_t rpb, const optional<Tensor>& ds8, const optional<Tensor>& s8,
+            const optional<Tensor>& amax8) {
   check_bf16(dy, "dy");
   check_contig(dy, "dy");
   const int64_t D = dy.size(-1), M = dy.numel() / D;
@@ -463,7 +465,12 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
   TORCH_CHECK(gamma.numel() == D && dgamma.numel() == D && dbeta.numel() == D, "ln_bwd: D");
   if (dbias.has_value()) {
     check_f32(*dbias, "dbias");
-    TORCH_CHECK(dbias->numel() == D && ds.has_value(), "ln_bwd: dbias needs ds");
+    TORCH_CHECK(dbias->numel() == D && (ds.has_value() || ds8.has_value()), "ln_bwd: dbias needs ds");
+  }
+  if (ds8.has_value()) {
+    check_f8_fmt(*ds8, 1, "ds8 (e5m2)");
+    TORCH_CHECK(ds8->numel() == dy.numel() && ds8->is_contiguous() && s8.has_value(), "ln_bwd: ds8");
+    check_f32(*s8, "s8");
   }
   check_f32(ws, "ws");
   TORCH_CHECK(rpb == 16 || rpb == 32 || rpb == 64, "ln_bwd: rows per block 16 / 32 / 64");
@@ -475,7 +482,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
       dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(),
       dbeta.data_ptr<float>(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
       ws.data_ptr<float>(), (int)M, (int)D, (float)p, (uint64_t)seed, ctr_ptr(ctr),
-      (uint64_t)site, accumulate, skip_reduce, (int)rpb, stream_of(dy));
+      (uint64_t)site, accumulate, skip_reduce, (int)rpb, ds8 ? ds8->data_ptr() : nullptr,
+      s8 ? s8->data_ptr<float>() : nullptr, amax_ptr(amax8), stream_of(dy));
   check_err(rc, "tdg ln_bwd");
 }
 

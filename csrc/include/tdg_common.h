@@ -291,6 +291,14 @@ __device__ __forceinline__ int pack2_e4m3(float a, float b, int old) {
   b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
   return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
 }
+// OCP e5m2 (gfx950 bf8): the gradient format of the fp8 backward
+constexpr float E5M2_MAX_F = 57344.f;
+template <bool HI>
+__device__ __forceinline__ int pack2_e5m2c(float a, float b, int old) {
+  a = fminf(fmaxf(a, -E5M2_MAX_F), E5M2_MAX_F);
+  b = fminf(fmaxf(b, -E5M2_MAX_F), E5M2_MAX_F);
+  return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
+}
 __device__ __forceinline__ void atomic_amax(unsigned* p, float v) {
   atomicMax(p, __float_as_uint(fabsf(v)));
 }

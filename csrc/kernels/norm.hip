@@ -20,7 +20,9 @@ namespace tdg {
 
 // e4m3 copy of one LayerNorm output row (delayed per-tensor scale s8) for an
 // fp8 GEMM; the row's |y| max folded into am.
-template <int D>
+// FMT 0: e4m3 (a LayerNorm output for an fp8 forward GEMM), 1: e5m2 (the
+// backward's sublayer gradient ds for an fp8 dgrad / weight gradient)
+template <int D, int FMT = 0>
 __device__ __forceinline__ void ln_row_y8(const RowVec<D / 64>& o, float s8, uint8_t* __restrict__ y8,
                                           size_t rbase, int lane, float& am) {
   constexpr int VEC = D / 64;
@@ -31,8 +33,13 @@ __device__ __forceinline__ void ln_row_y8(const RowVec<D / 64>& o, float s8, uin
   for (int i = 0; i < VEC; i += 2) {
     const float a = bf2f(f2bf(o.v[i])), b = bf2f(f2bf(o.v[i + 1]));
     am = fmaxf(am, fmaxf(fabsf(a), fabsf(b)));
-    if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
-    else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+    if constexpr (FMT == 0) {
+      if ((i & 2) == 0) w[i / 4] = pack2_e4m3<false>(a * s8, b * s8, w[i / 4]);
+      else w[i / 4] = pack2_e4m3<true>(a * s8, b * s8, w[i / 4]);
+    } else {
+      if ((i & 2) == 0) w[i / 4] = pack2_e5m2c<false>(a * s8, b * s8, w[i / 4]);
+      else w[i / 4] = pack2_e5m2c<true>(a * s8, b * s8, w[i / 4]);
+    }
   }
   uint8_t* dst = y8 + rbase + lane * RowMap<VEC>::W;
   if constexpr (VEC == 2) {
@@ -101,9 +108,11 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     const float* __restrict__ gamma, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ ds_out,
     const bf16_t* __restrict__ dres_in, float* __restrict__ part_g, float* __restrict__ part_b,
     float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
-    const long long* ctr, uint64_t site, int iters) {
+    const long long* ctr, uint64_t site, int iters, uint8_t* __restrict__ ds8,
+    const float* __restrict__ s8p, unsigned* __restrict__ amax8) {
   constexpr int VEC = D / 64;
   __shared__ float red[NWV][D];
+  float am8 = 0.f;  // |ds| max of the e5m2 copy
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float ag[VEC], ab[VEC], as[VEC];
 #pragma unroll
@@ -159,8 +168,9 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < VEC; ++i) ds.v[i] = ((km >> i) & 1u) ? dh.v[i] * sc : 0.f;
     }
-    if (ds_out) {
-      ds.store_row(ds_out + rbase, lane, wds);
+    if (ds_out || ds8) {
+      if (ds_out) ds.store_row(ds_out + rbase, lane, wds);
+      if (ds8) ln_row_y8<D, 1>(ds, s8p[0], ds8, rbase, lane, am8);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
     }
@@ -188,6 +198,17 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     }
     __syncthreads();
   }
+  if (ds8) {  // one atomic per block (spread amax words)
+    am8 = wave_max(am8);
+    if (lane == 0) red[0][w] = am8;
+    __syncthreads();
+    if (threadIdx.x == 0 && amax8) {
+      float m = 0.f;
+#pragma unroll
+      for (int k = 0; k < NWV; ++k) m = fmaxf(m, red[0][k]);
+      atomic_amax(amax_word(amax8, blockIdx.x), m);
+    }
+  }
 }
 
 }  // namespace tdg
@@ -213,7 +234,8 @@ template <int D>
 void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
-              int accumulate, int skip_reduce, int rpb, hipStream_t st) {
+              int accumulate, int skip_reduce, int rpb, void* ds8, const float* s8, unsigned* amax8,
+              hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
   // rpb rows per block (kernels.py ln_bwd_nparts): 16 on 4 waves, 32 / 64 on
   // 8 waves (fewer partial rows for the fold); RPW rows per wave per pass
@@ -226,12 +248,12 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
     hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                        (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
-                       max(1, rpb / (RPW * 4)));
+                       max(1, rpb / (RPW * 4)), (uint8_t*)ds8, s8, amax8);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 8>), dim3(nb), dim3(512), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                        (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
-                       max(1, rpb / (RPW * 8)));
+                       max(1, rpb / (RPW * 8)), (uint8_t*)ds8, s8, amax8);
   if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
@@ -262,11 +284,13 @@ extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, 
                           const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,
                           uint64_t seed, const long long* ctr, uint64_t site, int accumulate,
-                          int skip_reduce, int rpb, hipStream_t st) {
+                          int skip_reduce, int rpb, void* ds8, const float* s8, unsigned* amax8,
+                          hipStream_t st) {
   if (rpb != 16 && rpb != 32 && rpb != 64) return -2;
+  if (ds8 && !s8) return -2;
 #define TDG_LN_B(DD)                                                                              \
   ln_bwd_d<DD>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, \
-               ctr, site, accumulate, skip_reduce, rpb, st);                                      \
+               ctr, site, accumulate, skip_reduce, rpb, ds8, s8, amax8, st);                     \
   return 0;
   switch (D) {
     case 128: TDG_LN_B(128)

@@ -351,16 +351,27 @@ def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
     return (h - mean) * rstd * gamma.master + beta.master, (h, mean, rstd, ks)
 
 
-def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt: RunCtx):
+def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt: RunCtx,
+            ds8_slot: Optional[int] = None):
     """Returns (dh, ds): dh = dL/d(residual input) (fresh, writable), ds =
     dL/d(sublayer output). Also writes dgamma, dbeta and the sublayer's output
-    bias gradient (sum of ds over rows)."""
+    bias gradient (sum of ds over rows). ds8_slot (GPU, fp8 backward): ds is
+    returned as its e5m2 copy only (scale slot ds8_slot of rt.fp8.gmeta,
+    amax recorded), the bf16 ds is not written."""
     h, mean, rstd, ks = saved
     if dy.is_cuda:
         q = rt.wgrad
+        ds8 = s8 = a8 = None
+        if ds8_slot is not None:
+            gm = rt.fp8.gmeta
+            ds8 = torch.empty(dy.shape, dtype=gm.dtype, device=dy.device)
+            s8, a8 = gm.s(ds8_slot), gm.a(ds8_slot)
         dh, ds = K.ln_bwd(dy.contiguous(), h, mean, rstd, gamma.master, gamma.grad, beta.grad,
-                          sub_bias.grad, rt.p, rt.seed, rt.ctr, site, want_ds=True,
-                          accumulate=rt.accumulate, defer=q.reductions if q is not None else None)
+                          sub_bias.grad, rt.p, rt.seed, rt.ctr, site, want_ds=ds8 is None,
+                          accumulate=rt.accumulate, defer=q.reductions if q is not None else None,
+                          ds8=ds8, s8=s8, amax8=a8)
+        if ds8 is not None:
+            ds = ds8
         if q is not None:  # folded (and reported ready) with the next wgrad flush
             q.reduced_params += [(rt, gamma), (rt, beta), (rt, sub_bias)]
             return dh, ds
@@ -733,22 +744,23 @@ class FFNBlockFn(torch.autograd.Function):
         B, L, d = dy.shape
         ff = w1.shape[0]
         bt = _beta(rt)
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt)
+        f8w = ctx.lean
+        bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if (dy.is_cuda and rt.fp8 is not None) else None
+        # lean fp8 backward: the LayerNorm backward emits ds directly in e5m2
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt, ds8_slot=bw[0] if f8w else None)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
-            bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if rt.fp8 is not None else None
-            f8w = ctx.lean
             if not f8w:
                 _wgrad(rt, ds2, h, d, w2)
             if bw is not None:
                 # fp8 backward: e5m2 gradients x e4m3 transposed weights on the
                 # block-scaled MFMA; the ReLU-backward dgrad also emits the e5m2
                 # copy of its output for the next dgrad, which accumulates the
-                # residual gradient already in dh (weight gradients stay bf16)
+                # residual gradient already in dh
                 st = rt.fp8
                 gs, gh = bw
                 M = B * L
-                ds8 = fp8.quantize(ds2, st.gmeta, gs)
+                ds8 = ds2 if f8w else fp8.quantize(ds2, st.gmeta, gs)
                 w2t8, s2t = st.weights.get(w2, transposed=True)
                 w1t8, s1t = st.weights.get(w1, transposed=True)
                 if f8w:

@@ -419,21 +419,24 @@ def ln_bwd_nparts(M: int, D: int) -> int:
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
-           dres=None, accumulate=False, defer=None):
+           dres=None, accumulate=False, defer=None, ds8=None, s8=None, amax8=None):
     """`defer` (a list): leave the dgamma / dbeta / dbias partial sums in a
     per-site workspace and append their fold to `defer` (run later, all
-    LayerNorms of a backward in one launch, by reduce_partials_multi)."""
+    LayerNorms of a backward in one launch, by reduce_partials_multi).
+    ds8 (e5m2, shape of dy) with scale s8 / amax slot amax8: also the e5m2
+    copy of ds for an fp8 backward; with want_ds=False the bf16 ds is then
+    not written at all (the bias column sums still come from ds)."""
     D = dy.shape[-1]
     M = dy.numel() // D
     dh = torch.empty_like(dy)
-    need_ds = (want_ds and (p > 0 or dres is not None)) or dbias is not None
+    need_ds = (want_ds and (p > 0 or dres is not None)) or (dbias is not None and ds8 is None)
     ds = torch.empty_like(dy) if need_ds else None
     if defer is None:
         ws = workspace("ln_bwd", 3 * ln_bwd_nparts(M, D) * D, dy.device)
     else:  # partials must survive until the fold: one workspace per site
         ws = workspace(f"ln_bwd_part_{site}", 3 * ln_bwd_nparts(M, D) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
-               accumulate, defer is not None, ln_bwd_rpb(D))
+               accumulate, defer is not None, ln_bwd_rpb(D), ds8, s8, amax8)
     if defer is not None:
         nb = ln_bwd_nparts(M, D)
         outs = [dgamma, dbeta] + ([dbias] if dbias is not None else [])

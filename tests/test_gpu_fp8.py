@@ -380,10 +380,51 @@ def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c):
     bref = bsum + ref.bfloat16().float().sum(0)
     o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux8=h8, out8_slot=io,
                           colsum_out=bsum, colsum_beta=1.0)
-    o8ref = (ref * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
-    assert (o8.view(torch.uint8) == o8ref.view(torch.uint8)).float().mean().item() > 0.995
+    # (the kernel quantises the bf16-rounded value; compare values: masked
+    # elements are +0 from the kernel, -0 in ref * 0)
+    o8ref = (ref.bfloat16().float() * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
+    assert (o8.float() == o8ref.float()).float().mean().item() > 0.995
     if with_c:
         err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
         assert err < 1e-2, err
     berr = (bsum - bref).abs().max().item() / (bref.abs().max().item() + 1e-12)
     assert berr < 1e-3, berr
+
+
+@pytest.mark.parametrize("D", [512, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_ln_bwd_emits_e5m2_ds(D, p):
+    """LayerNorm backward with the e5m2 copy of ds (the lean fp8 FFN
+    backward): equal to quantising the bf16 ds, amax recorded, same dh and
+    bias column sums as the bf16 path."""
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    torch.manual_seed(6)
+    M = 1000
+    x = torch.randn(M, D, device=DEV).bfloat16()
+    s = torch.randn(M, D, device=DEV).bfloat16()
+    g, b = torch.rand(D, device=DEV) + 0.5, torch.randn(D, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    y, h, mean, rstd = kk.ln_fwd(x, s, g, b, p, 7, ctr, 3)
+    dy = torch.randn(M, D, device=DEV).bfloat16()
+    gm = F.Fp8Meta(DEV, fmt=1)
+    i = gm.slot("ds")
+    gm.scale[i] = 2.0 ** 8
+    outs = {}
+    for mode in ("bf16", "e5m2"):
+        dg, dbt, dbias = (torch.zeros(D, device=DEV) for _ in range(3))
+        if mode == "bf16":
+            dh, ds = kk.ln_bwd(dy, h, mean, rstd, g, dg, dbt, dbias, p, 7, ctr, 3)
+        else:
+            ds8 = torch.empty(M, D, dtype=F.BF8, device=DEV)
+            dh, _ = kk.ln_bwd(dy, h, mean, rstd, g, dg, dbt, dbias, p, 7, ctr, 3, want_ds=False,
+                              ds8=ds8, s8=gm.s(i), amax8=gm.a(i))
+            ds = ds8
+        outs[mode] = (dh.clone(), ds.clone(), dg, dbt, dbias)
+    dh16, ds16, dg16, db16, bias16 = outs["bf16"]
+    dh8, ds8, dg8, db8, bias8 = outs["e5m2"]
+    assert torch.equal(dh16, dh8)
+    assert torch.equal(dg16, dg8) and torch.equal(db16, db8)
+    assert torch.allclose(bias16, bias8, rtol=1e-5, atol=1e-5)
+    want = F.quantize(ds16, gm, i, record=False)
+    assert (ds8.view(torch.uint8) == want.view(torch.uint8)).float().mean().item() > 0.999
+    assert abs(gm.amax_values()[i].item() - ds16.float().abs().max().item()) <= 1e-6 * ds16.float().abs().max().item()
