@@ -137,7 +137,8 @@ __device__ __forceinline__ int pack2_f8(float a, float b, int old) {
 
 }  // namespace f8
 
-enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2, F8_EPI_DRELU = 3 };
+enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2, F8_EPI_DRELU = 3, F8_EPI_DRELU8 = 4 };
+// (F8_EPI_DRELU8: the ReLU-backward mask from F8Extra::aux8, host-selected)
 // flag on top of the epilogue id: C = dequant(C8) (needs C8)
 constexpr int F8_EPI_CDEQ = 16;
 
@@ -171,6 +172,48 @@ struct F8Epi {
   static constexpr int SROW = WTN * 2 + 16;
   static constexpr int CPR = WTN / 8;
   static constexpr int LDS = NW * WTM * SROW + 64;  // images + amax scratch
+  // the ReLU mask / old C of every chunk a lane stores, loaded into registers
+  // by prefetch() BEFORE the main loop (the caller issues it ahead of the
+  // first LDS-DMA): loaded in the epilogue, their latency sat exposed once per
+  // tile round (the ReLU-backward dgrad 8192x4096x1024: ~30 us of ~90)
+  static constexpr int ITER = (WTM * CPR) / 64;
+  static constexpr bool DR = EPI == F8_EPI_DRELU || EPI == F8_EPI_DRELU8;  // ReLU backward
+  static constexpr bool A8 = EPI == F8_EPI_DRELU8;                          // 8-bit mask
+  static constexpr bool PRE = DR && PRE_OK;
+  // (the old C of a beta != 0 ReLU-backward GEMM is loaded in the epilogue:
+  // kept out of the prefetch so the kernel stays at two waves per SIMD)
+  struct Pre {
+    int4 aux[PRE && !A8 ? ITER : 1];  // bf16 mask chunk
+    uint2 aux8[PRE && A8 ? ITER : 1];  // 8 mask bytes
+  };
+  static __device__ __forceinline__ bool vec_ok(int ldc, const F8Extra& ex) {
+    return (ldc & 7) == 0 && (!DR || (ex.ldaux & 7) == 0);
+  }
+  // (the bf16 mask is prefetched at the start of the epilogue instead: 32
+  // more registers across the main loop would cost the second wave per SIMD)
+  static __device__ __forceinline__ void prefetch(Pre& pre, const bf16_t* __restrict__ C, int M, int N,
+                                                  int ldc, int m0, int n0, int wid, int lane,
+                                                  const F8Extra& ex) {
+    if constexpr (PRE && A8) {
+      const int wm = wid / WN, wn = wid % WN;
+      const bool vok = vec_ok(ldc, ex);
+#pragma unroll
+      for (int tt = 0; tt < ITER; ++tt) {
+        const int id = lane + 64 * tt;
+        const int row = id / CPR, ch = id % CPR;
+        const int m = m0 + wm * WTM + row;
+        const int n = n0 + wn * WTN + ch * 8;
+        if constexpr (A8) pre.aux8[tt] = uint2{0u, 0u};
+        else pre.aux[tt] = int4{0, 0, 0, 0};
+        if (vok && m < M && n + 8 <= N) {
+          if constexpr (A8)
+            pre.aux8[tt] = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
+          else
+            pre.aux[tt] = *reinterpret_cast<const int4*>(ex.aux + (size_t)m * ex.ldaux + n);
+        }
+      }
+    }
+  }
   static __device__ __forceinline__ void run(char* smem, const f32x4 (&acc)[TM][TN],
                                              bf16_t* __restrict__ C, const float* __restrict__ bias,
                                              const float* __restrict__ sa,
@@ -178,38 +221,29 @@ struct F8Epi {
                                              const float* __restrict__ sc8,
                                              unsigned* __restrict__ amax_out, int M, int N, int ldc,
                                              int ldc8, int m0, int n0, int wid, int lane, int tid,
-                                             const F8Extra& ex) {
+                                             const F8Extra& ex, const Pre& pre) {
     const int wm = wid / WN, wn = wid % WN;
     const float alpha = 1.f / (sa[0] * sb[0]);
     const float s8 = C8 ? sc8[0] : 0.f;
     char* wimg = smem + wid * (WTM * SROW);
     const int g = lane >> 4, cl = lane & 15;
-    // the ReLU mask / old C of every chunk this lane stores, loaded before
-    // the image is written (one memory latency per tile, not per chunk)
-    constexpr int ITER = (WTM * CPR) / 64;
-    constexpr bool PRE = EPI == F8_EPI_DRELU && PRE_OK;
     static_assert(64 % CPR == 0, "a lane keeps its column chunk across iterations");
-    short8_t pre_aux[PRE ? ITER : 1], pre_c[PRE ? ITER : 1];
-    const bool vec_ok = (ldc & 7) == 0 && (EPI != F8_EPI_DRELU || (ex.ldaux & 7) == 0);
+    short8_t pre_aux[PRE && !A8 ? ITER : 1];
+    const bool vec_ok = F8Epi::vec_ok(ldc, ex);
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (PRE) {
 #pragma unroll
       for (int tt = 0; tt < ITER; ++tt) {
-        const int id = lane + 64 * tt;
-        const int row = id / CPR, ch = id % CPR;
-        const int m = m0 + wm * WTM + row;
-        const int n = n0 + wn * WTN + ch * 8;
-        pre_aux[tt] = pre_c[tt] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
-        if (vec_ok && m < M && n + 8 <= N) {
-          if (ex.aux8) {  // 8 mask bytes -> 0 / 1 halves (only the sign of the mask is used)
-            const uint2 b = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              pre_aux[tt][e] = ((e < 4 ? b.x >> (8 * e) : b.y >> (8 * (e - 4))) & 0xffu) ? 0x3f80 : 0;
-          } else {
+        if constexpr (A8) {
+          // (raw mask bytes stay in pre.aux8: applied packed, below)
+        } else {
+          const int id = lane + 64 * tt;
+          const int row = id / CPR, ch = id % CPR;
+          const int m = m0 + wm * WTM + row;
+          const int n = n0 + wn * WTN + ch * 8;
+          pre_aux[tt] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+          if (vec_ok && m < M && n + 8 <= N)
             pre_aux[tt] = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
-          }
-          if (ex.beta != 0.f) pre_c[tt] = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
         }
       }
     }
@@ -237,38 +271,47 @@ struct F8Epi {
       const int n = n0 + wn * WTN + ch * 8;
       if (m >= M || n >= N) continue;
       short8_t v = *reinterpret_cast<const short8_t*>(wimg + row * SROW + ch * 16);
-      if (EPI == F8_EPI_DRELU || ex.beta != 0.f) {
+      const bool vec = n + 8 <= N && vec_ok;
+      if constexpr (A8) {
+        if (vec) {
+          // packed 8-bit mask: each mask byte -> 0 / 0xffff over its bf16
+          // half (no bf16 -> f32 -> bf16 round trip: the per-element form
+          // cost this epilogue ~20 us on 8192 x 4096)
+          uint2 mb;
+          if constexpr (PRE) mb = pre.aux8[tt];
+          else mb = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
+          uint32_t bx = mb.x, by = mb.y;
+          bx |= bx >> 4; bx |= bx >> 2; bx |= bx >> 1; bx &= 0x01010101u;
+          by |= by >> 4; by |= by >> 2; by |= by >> 1; by &= 0x01010101u;
+          u32x4_t dw = __builtin_bit_cast(u32x4_t, v);
+          dw[0] &= __builtin_amdgcn_perm(0u, bx, 0x0c010c00u) * 0xffffu;
+          dw[1] &= __builtin_amdgcn_perm(0u, bx, 0x0c030c02u) * 0xffffu;
+          dw[2] &= __builtin_amdgcn_perm(0u, by, 0x0c010c00u) * 0xffffu;
+          dw[3] &= __builtin_amdgcn_perm(0u, by, 0x0c030c02u) * 0xffffu;
+          v = __builtin_bit_cast(short8_t, dw);
+        }
+      }
+      if ((DR && !(A8 && vec)) || ex.beta != 0.f) {
         // 16-byte mask / old-C loads for whole aligned chunks (8 scalar
         // 2-byte loads per chunk made the ReLU-backward GEMM 2.4x slower)
-        const bool vec = n + 8 <= N && vec_ok;
         short8_t mk = v, old = v;
         if (vec) {
-          if constexpr (PRE) {
+          if constexpr (PRE && !A8) {
             mk = pre_aux[tt];
-            old = pre_c[tt];
-          } else {
-            if constexpr (EPI == F8_EPI_DRELU) {
-              if (ex.aux8) {
-                const uint2 b = *reinterpret_cast<const uint2*>(ex.aux8 + (size_t)m * ex.ldaux + n);
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                  mk[e] = ((e < 4 ? b.x >> (8 * e) : b.y >> (8 * (e - 4))) & 0xffu) ? 0x3f80 : 0;
-              } else {
-                mk = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
-              }
-            }
-            if (ex.beta != 0.f) old = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
+          } else if constexpr (DR && !A8) {
+            mk = *reinterpret_cast<const short8_t*>(ex.aux + (size_t)m * ex.ldaux + n);
           }
+          if (ex.beta != 0.f) old = *reinterpret_cast<const short8_t*>(C + (size_t)m * ldc + n);
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (!vec && n + e >= N) break;
           float f = bf2f((bf16_t)v[e]);
-          if constexpr (EPI == F8_EPI_DRELU) {
-            const float a = vec ? bf2f((bf16_t)mk[e])
-                                : (ex.aux8 ? (ex.aux8[(size_t)m * ex.ldaux + n + e] ? 1.f : 0.f)
-                                           : bf2f(ex.aux[(size_t)m * ex.ldaux + n + e]));
-            if (!(a > 0.f)) f = 0.f;
+          if constexpr (DR) {
+            float a;
+            if constexpr (A8) a = vec ? 1.f : (ex.aux8[(size_t)m * ex.ldaux + n + e] ? 1.f : 0.f);
+            else a = vec ? bf2f((bf16_t)mk[e]) : bf2f(ex.aux[(size_t)m * ex.ldaux + n + e]);
+            if (!(a > 0.f)) f = 0.f;  // (A8, vec: already masked above)
           }
           if (ex.beta != 0.f)
             f += ex.beta * (vec ? bf2f((bf16_t)old[e]) : bf2f(C[(size_t)m * ldc + n + e]));
@@ -380,6 +423,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = K / BK8;  // host guarantees K % 128 == 0
 
+  using Epi = F8Epi<BM, BN, WM, WN, EPI, CF>;
+  typename Epi::Pre pre;
+  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex);  // (older than every DMA)
   GA ga;
   GB gb;
   ga.init(wid, lane);
@@ -438,8 +484,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   }
 
   f8::lds_barrier();
-  F8Epi<BM, BN, WM, WN, EPI, CF>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc,
-                                      ldc8, m0, n0, wid, lane, tid, ex);
+  Epi::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
+           pre);
 }
 
 // ---------------------------------------------------------------------------
@@ -639,8 +685,10 @@ __global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   f8::lds_barrier();
-  F8Epi<256, 256, 2, 2, EPI, CF, false>::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N,
-                                             ldc, ldc8, m0, n0, wid, lane, tid, ex);
+  using Epi = F8Epi<256, 256, 2, 2, EPI, CF, false>;
+  typename Epi::Pre none;
+  Epi::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
+           none);
 }
 
 // ---------------------------------------------------------------------------
@@ -1144,6 +1192,11 @@ static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float*
     }
   }
   if (afmt == 1 && cfmt == 1) {
+    if (epi == F8_EPI_DRELU && ex.aux8) {
+      if (cfg == 9 && (long long)M * lda < (1LL << 32) && (long long)N * ldb < (1LL << 32))
+        return launch_f8_w1<F8_EPI_DRELU8, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU8, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    }
     if (cfg == 9 && (long long)M * lda < (1LL << 32) && (long long)N * ldb < (1LL << 32)) {
       if (epi == F8_EPI_DRELU)
         return launch_f8_w1<F8_EPI_DRELU, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
