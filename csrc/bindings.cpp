@@ -60,6 +60,10 @@ int tdg_gemm_ragged(const void* const* A, const void* const* B, void* const* C, 
 int tdg_wgrad_fp8(const void* const* A, const void* const* B, float* const* C,
                   const float* const* sa, const float* const* sb, int P, const int* shapes, int T,
                   float beta, hipStream_t st);
+int tdg_fp8_quant_colsum(const void* x, int ld, void* y8, int M, int N, const float* scale,
+                         unsigned* amax, float* part, int fmt, hipStream_t st);
+int tdg_fp8_quant_t(const void* const* src, void* const* dst, const int* slot, int G, int R, int C,
+                    const float* scale, unsigned* amax, hipStream_t st);
 int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* bias, const float* sa,
                  const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
                  int lda, int ldb, int ldc, int ldc8, int epi, int cfg, int afmt, int cfmt,
@@ -820,6 +824,55 @@ void fp8_quant(const Tensor& x, const Tensor& y8, const Tensor& scale,
                           amax_ptr(amax), (int)fmt, stream_of(x)), "tdg fp8_quant");
 }
 
+// y8 = fp8(x) (amax recorded) + per-256-row-block column sums of x into part
+void fp8_quant_colsum(const Tensor& x, const Tensor& y8, const Tensor& scale, const Tensor& amax,
+                      const Tensor& part, int64_t fmt) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "fp8_quant_colsum: x [M, N], unit inner stride");
+  const int64_t M = x.size(0), N = x.size(1);
+  check_f8_fmt(y8, fmt, "y8");
+  TORCH_CHECK(y8.is_contiguous() && y8.numel() == M * N, "fp8_quant_colsum: y8 [M, N]");
+  check_f32(scale, "scale");
+  check_f32(part, "part");
+  TORCH_CHECK(part.numel() >= ((M + 255) / 256) * N, "fp8_quant_colsum: part [ceil(M/256), N]");
+  TORCH_CHECK(N % 8 == 0 && x.stride(0) % 8 == 0, "fp8_quant_colsum: N, ld % 8");
+  c10::DeviceGuard g(x.device());
+  check_err(tdg_fp8_quant_colsum(x.data_ptr(), (int)x.stride(0), y8.data_ptr(), (int)M, (int)N,
+                                 scale.data_ptr<float>(), amax_ptr(amax), part.data_ptr<float>(),
+                                 (int)fmt, stream_of(x)),
+            "tdg fp8_quant_colsum");
+}
+
+// dsts[g] [C, R] e4m3 = transposed, quantised srcs[g] [R, C] bf16 (slot scales / amax)
+void fp8_quant_t(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts,
+                 const std::vector<int64_t>& slots, const Tensor& scale, const Tensor& amax) {
+  const int n = (int)srcs.size();
+  TORCH_CHECK(n >= 1 && n <= 64 && (int)dsts.size() == n && (int)slots.size() == n,
+              "fp8_quant_t: 1..64 weights");
+  check_f32(scale, "scale");
+  TORCH_CHECK(amax.numel() == 2048 * scale.numel(), "fp8_quant_t: amax is [slots, 2048]");
+  const int64_t R = srcs[0].size(0), C = srcs[0].size(1);
+  std::vector<const void*> sp(n);
+  std::vector<void*> dp(n);
+  std::vector<int> sl(n);
+  for (int i = 0; i < n; ++i) {
+    check_bf16(srcs[i], "src");
+    check_contig(srcs[i], "src");
+    check_f8_fmt(dsts[i], 0, "dst");
+    TORCH_CHECK(srcs[i].dim() == 2 && srcs[i].size(0) == R && srcs[i].size(1) == C &&
+                    dsts[i].is_contiguous() && dsts[i].numel() == R * C,
+                "fp8_quant_t: same-shape [R, C] sources, [C, R] destinations");
+    TORCH_CHECK(slots[i] >= 0 && slots[i] < scale.numel(), "fp8_quant_t: slot range");
+    sp[i] = srcs[i].data_ptr();
+    dp[i] = dsts[i].data_ptr();
+    sl[i] = (int)slots[i];
+  }
+  c10::DeviceGuard g(scale.device());
+  check_err(tdg_fp8_quant_t(sp.data(), dp.data(), sl.data(), n, (int)R, (int)C,
+                            scale.data_ptr<float>(), amax_ptr(amax), stream_of(scale)),
+            "tdg fp8_quant_t");
+}
+
 void fp8_quant_multi(const std::vector<Tensor>& xs, const std::vector<Tensor>& ys,
                      const std::vector<int64_t>& slots, const Tensor& scale, const Tensor& amax) {
   const int n = (int)xs.size();
@@ -1035,6 +1088,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ldaux"), py::arg("beta"), py::arg("aux8") = py::none(),
         py::arg("colsum_out") = py::none(), py::arg("colsum_beta") = 0.0, py::arg("ws") = py::none());
   m.def("wgrad_fp8", &wgrad_fp8);
+  m.def("fp8_quant_colsum", &fp8_quant_colsum);
+  m.def("fp8_quant_t", &fp8_quant_t);
   m.def("fp8_quant", &fp8_quant);
   m.def("fp8_quant_multi", &fp8_quant_multi);
   m.def("fp8_scale_update", &fp8_scale_update);

@@ -941,6 +941,125 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
   }
 }
 
+// Quantise a [M, N] bf16 gradient (row stride ld) to fp8 (FMT) AND write the
+// per-row-block column sums of the bf16 values (part[blockIdx.y][N], folded
+// later: the bias gradient of the layer whose output gradient this is) in
+// one pass. Block: 256 columns (32 lanes x 8) x 8 row lanes, QC_ROWS rows.
+constexpr int QC_ROWS = 256;
+template <int FMT>
+__global__ __launch_bounds__(256) void fp8_quant_colsum_kernel(const bf16_t* __restrict__ x, int ld,
+                                                               uint8_t* __restrict__ y8, int M,
+                                                               int N, const float* __restrict__ scale,
+                                                               unsigned* __restrict__ amax_out,
+                                                               float* __restrict__ part) {
+  __shared__ float red[8][256 + 4];
+  __shared__ float redm[4];
+  const float s = scale[0];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int n = blockIdx.x * 256 + cl * 8;
+  const int r0 = blockIdx.y * QC_ROWS;
+  const int r1 = min(M, r0 + QC_ROWS);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float amax = 0.f;
+  if (n < N) {  // (host: N % 8 == 0, ld % 8 == 0)
+    for (int r = r0 + rl; r < r1; r += 8) {
+      const short8_t v = *reinterpret_cast<const short8_t*>(x + (size_t)r * ld + n);
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = bf2f((bf16_t)v[e]);
+        cs[e] += f[e];
+        amax = fmaxf(amax, fabsf(f[e]));
+      }
+      int lo = f8::pack2_f8<FMT, false>(f[0] * s, f[1] * s, 0);
+      lo = f8::pack2_f8<FMT, true>(f[2] * s, f[3] * s, lo);
+      int hi = f8::pack2_f8<FMT, false>(f[4] * s, f[5] * s, 0);
+      hi = f8::pack2_f8<FMT, true>(f[6] * s, f[7] * s, hi);
+      *reinterpret_cast<int2*>(y8 + (size_t)r * N + n) = make_int2(lo, hi);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cl * 8 + e] = cs[e];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  const int c = threadIdx.x;  // one column per thread
+  if (blockIdx.x * 256 + c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][c];
+    part[(size_t)blockIdx.y * N + blockIdx.x * 256 + c] = t;
+  }
+  if (threadIdx.x == 0 && amax_out)
+    f8::atomic_amax(amax_word(amax_out, blockIdx.y * gridDim.x + blockIdx.x),
+                    fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])));
+}
+
+// Transposing e4m3 quantisation of same-shape weights: dst[g] [C][R] =
+// e4m3(src[g] [R][C]^T * scale[slot[g]]), amax into amax[slot[g]] -- the
+// transposed weight copies of the fp8 dgrads straight from the bf16 compute
+// copy (no bf16 transposed copy). 64 x 64 tiles through LDS.
+constexpr int QT_MAXG = 64;
+struct QuantTGroup {
+  const bf16_t* src[QT_MAXG];
+  uint8_t* dst[QT_MAXG];
+  int slot[QT_MAXG];
+};
+__global__ __launch_bounds__(256) void fp8_quant_t_kernel(QuantTGroup grp, int R, int C,
+                                                          const float* __restrict__ scale,
+                                                          unsigned* __restrict__ amax) {
+  __shared__ float tile[64][65];
+  __shared__ float redm[4];
+  const bf16_t* __restrict__ src = grp.src[blockIdx.y];
+  uint8_t* __restrict__ dst = grp.dst[blockIdx.y];
+  const int slot = grp.slot[blockIdx.y];
+  const float s = scale[slot];
+  const int tiles_c = (C + 63) / 64;
+  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+  const int tid = threadIdx.x;
+  float am = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k;
+    const int r = id >> 3, c = (id & 7) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool in = r0 + r < R && c0 + c + e < C;
+      const float f = in ? bf2f(src[(size_t)(r0 + r) * C + c0 + c + e]) : 0.f;
+      tile[r][c + e] = f;
+      am = fmaxf(am, fabsf(f));
+    }
+  }
+  __syncthreads();
+  // dst row = source column (c0 + c), 8 consecutive source rows per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k;
+    const int c = id >> 3, r = (id & 7) * 8;
+    if (c0 + c >= C) continue;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = tile[r + e][c] * s;
+    int lo = f8::pack2_f8<0, false>(f[0], f[1], 0);
+    lo = f8::pack2_f8<0, true>(f[2], f[3], lo);
+    int hi = f8::pack2_f8<0, false>(f[4], f[5], 0);
+    hi = f8::pack2_f8<0, true>(f[6], f[7], hi);
+    uint8_t* d = dst + (size_t)(c0 + c) * R + r0 + r;
+    if (r0 + r + 8 <= R && (R % 8) == 0) {
+      *reinterpret_cast<int2*>(d) = make_int2(lo, hi);
+    } else {
+      for (int e = 0; e < 8 && r0 + r + e < R; ++e)
+        d[e] = (uint8_t)(((e < 4 ? lo : hi) >> (8 * (e & 3))) & 0xff);
+    }
+  }
+  am = wave_max(am);
+  if ((tid & 63) == 0) redm[tid >> 6] = am;
+  __syncthreads();
+  if (tid == 0)
+    f8::atomic_amax(amax_word(amax + (size_t)slot * AMAX_WORDS, blockIdx.x),
+                    fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])));
+}
+
 // y8 = e4m3(x * scale[0]); amax_out = max|x| (both optional sides)
 template <int FMT>
 __global__ __launch_bounds__(256) void fp8_quant_kernel(const bf16_t* __restrict__ x,
@@ -1303,5 +1422,35 @@ extern "C" int tdg_wgrad_fp8(const void* const* A, const void* const* B, float* 
     attr = true;
   }
   hipLaunchKernelGGL(wgrad_fp8_kernel, dim3(tiles), dim3(256), lds, st, args, T, beta);
+  return 0;
+}
+
+// y8 [M, N] (contiguous) = fp8(x * scale) of x [M, N] (row stride ld), amax
+// recorded, and part[ceil(M / 256)][N] = per-row-block column sums of x.
+extern "C" int tdg_fp8_quant_colsum(const void* x, int ld, void* y8, int M, int N,
+                                    const float* scale, unsigned* amax, float* part, int fmt,
+                                    hipStream_t st) {
+  if (N % 8 || ld % 8 || M <= 0) return -2;
+  const dim3 grid(cdiv(N, 256), cdiv(M, QC_ROWS));
+  if (fmt == 1)
+    hipLaunchKernelGGL(fp8_quant_colsum_kernel<1>, grid, dim3(256), 0, st, (const bf16_t*)x, ld,
+                       (uint8_t*)y8, M, N, scale, amax, part);
+  else
+    hipLaunchKernelGGL(fp8_quant_colsum_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)x, ld,
+                       (uint8_t*)y8, M, N, scale, amax, part);
+  return 0;
+}
+
+extern "C" int tdg_fp8_quant_t(const void* const* src, void* const* dst, const int* slot, int G,
+                               int R, int C, const float* scale, unsigned* amax, hipStream_t st) {
+  if (G < 1 || G > QT_MAXG || R < 1 || C < 1) return -2;
+  QuantTGroup g{};
+  for (int i = 0; i < G; ++i) {
+    g.src[i] = (const bf16_t*)src[i];
+    g.dst[i] = (uint8_t*)dst[i];
+    g.slot[i] = slot[i];
+  }
+  const int tiles = cdiv(R, 64) * cdiv(C, 64);
+  hipLaunchKernelGGL(fp8_quant_t_kernel, dim3(tiles, G), dim3(256), 0, st, g, R, C, scale, amax);
   return 0;
 }

@@ -322,6 +322,34 @@ def _wgrad(rt: RunCtx, dy2, x2, N: int, w: Param, b: Optional[Param] = None) -> 
     _ready(rt, w, *([b] if b is not None else []))
 
 
+def _attn_lean(rt: RunCtx, M: int, w_in: Param, w_out: Optional[Param], d: int) -> bool:
+    """Attention block with fp8 projections in forward and backward (fp8
+    state with ATTN_PROJ_FP8; weight gradients through the deferred queue)."""
+    st = rt.fp8
+    return (st is not None and rt.training and rt.wgrad is not None and fp8.ATTN_PROJ_FP8
+            and id(w_in) in st.proj_bwd and (w_out is None or id(w_out) in st.attn_out)
+            and fp8.wgrad_fp8_ok(M, d, d))
+
+
+def _fp8_grad_bias(g: torch.Tensor, g_slot: int, b: Param, rt: RunCtx, key: str):
+    """e5m2 copy of the bf16 gradient g [M, N] and, from the same pass, the
+    bias gradient (column sums) -- folded with the queue's other deferred
+    column reductions at the next flush (one launch)."""
+    st = rt.fp8
+    g8, part, nparts = fp8.quantize_colsum(g, st.gmeta, g_slot, key)
+    q = rt.wgrad
+    q.reductions.append((part, b.grad, nparts, g.shape[1], _beta(rt)))
+    q.reduced_params.append((rt, b))
+    return g8
+
+
+def _fp8_dgrad_into(g8, g_slot: int, w: Param, out: torch.Tensor, rt: RunCtx, beta: float) -> None:
+    """out (=|+= beta) dequant(g8 (e5m2) @ w) against w's transposed e4m3 copy."""
+    st = rt.fp8
+    wt8, swt = st.weights.get(w, transposed=True)
+    fp8.gemm_bf8_dgrad(g8, st.gmeta, g_slot, wt8, st.meta, swt, out, beta=beta)
+
+
 # =============================================================================== LN helpers
 def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int, rt: RunCtx):
     """GPU block tail y = LN(x + dropout(a2 @ w^T + b)) -> (y, saved): the
@@ -475,9 +503,11 @@ class SelfAttnBlockFn(torch.autograd.Function):
         ctx.p = (wqkv, bqkv, wo, bo, gamma, beta)
         ctx.meta = (heads, causal, scale, site, rt)
         x2 = x.reshape(B * L, d)
+        ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * L, wqkv, wo, d)
+        kx = [] if lean else None
         if x.is_cuda:
             f8 = rt.fp8 is not None and K.attn_fwd_fp8_ok(L, L, hd)
-            r = rt.fp8.linear(x2, wqkv, bqkv, want8=f8) if rt.fp8 is not None else None
+            r = rt.fp8.linear(x2, wqkv, bqkv, want8=f8, keep_x8=kx) if rt.fp8 is not None else None
             qkv, qkv8 = (r[0], r[1]) if f8 and r is not None else (r, None)
             if qkv is None:
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
@@ -497,7 +527,12 @@ class SelfAttnBlockFn(torch.autograd.Function):
             s = o.reshape(B * L, d) @ wo.master.t() + bo.master
         if rt.attn_maps is not None:
             rt.attn_maps[site] = attention_probs(q5[:, :, 0], q5[:, :, 1], kv_len, causal, scale)
-        if s is None:
+        ctx.f8a = None
+        if lean:  # e4m3 output projection; keep the e4m3 operands for the backward
+            s, o8 = rt.fp8.out_proj(o.view(B * L, d), wo, bo)
+            ctx.f8a = (kx[0], kx[1], o8)
+            y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
+        elif s is None:
             y, ctx.ln = _proj_ln_fwd(o.view(B * L, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
@@ -513,6 +548,8 @@ class SelfAttnBlockFn(torch.autograd.Function):
         M = B * L
         hd = d // heads
         bt = _beta(rt)
+        if ctx.lean:
+            return SelfAttnBlockFn._backward_fp8(ctx, dy)
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         q5 = qkv.view(B, L, 3, heads, hd)
@@ -540,6 +577,38 @@ class SelfAttnBlockFn(torch.autograd.Function):
         dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
         return (dx.view(B, L, d),) + (None,) * 11
 
+    @staticmethod
+    def _backward_fp8(ctx, dy):
+        """Lean fp8 backward: e5m2 ds from the LayerNorm backward -> O-proj
+        dgrad (e5m2 x e4m3 Wo^T) -> bf16 attention backward -> e5m2 dQ|dK|dV
+        -> input-projection dgrad (into the residual gradient); both weight
+        gradients in fp8 from the saved e4m3 operands."""
+        wqkv, bqkv, wo, bo, gamma, beta = ctx.p
+        heads, causal, scale, site, rt = ctx.meta
+        x2, qkv, o, aux, kv_len = ctx.saved_tensors
+        B, L, d = dy.shape
+        M, hd, bt = B * L, d // heads, _beta(rt)
+        st = rt.fp8
+        x8, xs, o8 = ctx.f8a
+        os_, go = st.attn_out[id(wo)]
+        dh, ds8 = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, ds8_slot=go)
+        ds8 = ds8.view(M, d)
+        do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
+        _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
+        q5 = qkv.view(B, L, 3, heads, hd)
+        dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
+        g5 = dqkv.view(B, L, 3, heads, hd)
+        K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
+                   g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
+        gq = st.proj_bwd[id(wqkv)]
+        dqkv8 = _fp8_grad_bias(dqkv, gq, bqkv, rt, f"qkv{site}")
+        _fp8_dgrad_into(dqkv8, gq, wqkv, dh.view(M, d), rt, 1.0)
+        q = rt.wgrad
+        q.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
+        q.add_fp8(dqkv8, st.gmeta.s(gq), x8, st.meta.s(xs), wqkv, bt, rt)
+        q.layer_end()  # self-attention is a layer's first block
+        return (dh.view(B, L, d),) + (None,) * 11
+
 
 # =============================================================================== cross-attention
 class CrossKVFn(torch.autograd.Function):
@@ -553,10 +622,15 @@ class CrossKVFn(torch.autograd.Function):
         ctx.p = (wkv, bkv)
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
         ctx.save_for_backward(e2)
+        ctx.lean = lean = enc.is_cuda and _attn_lean(rt, B * S, wkv, None, d)
+        kx = [] if lean else None
+        ctx.f8a = None
         if enc.is_cuda:
             kv = None
             if rt.fp8 is not None:
-                r = rt.fp8.linear(e2.contiguous(), wkv, bkv, want8=True)
+                r = rt.fp8.linear(e2.contiguous(), wkv, bkv, want8=True, keep_x8=kx)
+                if lean and r is not None:
+                    ctx.f8a = tuple(kx)
                 if r is not None:  # its e4m3 copy feeds the decoders' e4m3 attention
                     kv = r[0]
                     rt.fp8.kv8 = (r[1].view(B, S, -1), r[2])
@@ -578,6 +652,20 @@ class CrossKVFn(torch.autograd.Function):
         ctx.kvh.buf = None
         N = wkv.shape[0]
         bt = _beta(rt)
+        if e2.is_cuda and ctx.f8a is not None:
+            # lean fp8: e5m2 dK|dV of every decoder layer -> one dgrad + fp8
+            # weight gradient against the encoder output's e4m3 copy
+            st = rt.fp8
+            x8, xs = ctx.f8a
+            gk = st.proj_bwd[id(wkv)]
+            dkv8 = _fp8_grad_bias(dkv.contiguous(), gk, bkv, rt, "kv")
+            rt.wgrad.add_fp8(dkv8, st.gmeta.s(gk), x8, st.meta.s(xs), wkv, bt, rt)
+            rt.wgrad.boundary()
+            denc = torch.empty(B * S, d, dtype=torch.bfloat16, device=dkv.device)
+            _fp8_dgrad_into(dkv8, gk, wkv, denc, rt, 0.0)
+            if rt.store is not None:
+                rt.store.release_point()
+            return denc.view(B, S, d), None, None, None, None
         if e2.is_cuda:
             _wgrad(rt, dkv, e2, N, wkv, bkv)
             if rt.wgrad is not None:
@@ -613,9 +701,11 @@ class CrossAttnBlockFn(torch.autograd.Function):
             if kv_all.is_contiguous() else None
         if kv5 is None:
             raise ValueError("kv_all must be contiguous")
+        ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * T, wq, wo, d)
+        kx = [] if lean else None
         if x.is_cuda:
             f8 = (rt.fp8 is not None and rt.fp8.kv8 is not None and K.attn_fwd_fp8_ok(T, S, hd))
-            r = rt.fp8.linear(x2, wq, bq, want8=f8) if rt.fp8 is not None else None
+            r = rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx) if rt.fp8 is not None else None
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
             if q is None:
                 q = K.linear_fwd(x2, wq.compute, bq.master)
@@ -639,7 +729,12 @@ class CrossAttnBlockFn(torch.autograd.Function):
             s = o.reshape(B * T, d) @ wo.master.t() + bo.master
         if rt.attn_maps is not None:
             rt.attn_maps[site] = attention_probs(q.view(B, T, heads, hd), kv5[:, :, 0], kv_len, False, scale)
-        if s is None:
+        ctx.f8a = None
+        if lean:  # e4m3 output projection; keep the e4m3 operands for the backward
+            s, o8 = rt.fp8.out_proj(o.view(B * T, d), wo, bo)
+            ctx.f8a = (kx[0], kx[1], o8)
+            y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
+        elif s is None:
             y, ctx.ln = _proj_ln_fwd(o.view(B * T, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
@@ -661,6 +756,25 @@ class CrossAttnBlockFn(torch.autograd.Function):
         dkv_all = kvh.buf.view(B, S, -1)
         kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
         g5 = dkv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+        if ctx.lean:
+            st = rt.fp8
+            x8, xs, o8 = ctx.f8a
+            os_, go = st.attn_out[id(wo)]
+            dh, ds8 = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, ds8_slot=go)
+            ds8 = ds8.view(M, d)
+            do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
+            _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
+            dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
+            K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
+                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
+                       g5[:, :, 1], kv_len, scale, False)
+            gq = st.proj_bwd[id(wq)]
+            dq8 = _fp8_grad_bias(dq, gq, bq, rt, f"q{site}")
+            _fp8_dgrad_into(dq8, gq, wq, dh.view(M, d), rt, 1.0)
+            rt.wgrad.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
+            rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)
+            dkv_ret = dkv_all if layer == 0 else None
+            return (dh.view(B, T, d), dkv_ret) + (None,) * 12
         dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:

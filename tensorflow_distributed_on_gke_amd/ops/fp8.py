@@ -40,6 +40,9 @@ AMAX_WORDS = 64 * 32  # per slot (csrc/include/tdg_common.h AMAX_WORDS)
 _CANDS = (0, 1, 2, 3, 4, 5, 8, 9)
 # FFN weight gradients in fp8 (wgrad_fp8) when the step runs the fp8 backward
 WGRAD_FP8 = True
+# attention projections in fp8 too (Fp8State(backward=True)): output
+# projection forward, every projection dgrad and weight gradient
+ATTN_PROJ_FP8 = True
 # tile config of the e5m2 x e4m3 backward GEMMs (0: 128x128 / 4 waves; 9: 256x256 at one wave per SIMD)
 BWD_CFG = 0
 _TUNED: Dict[tuple, int] = {}
@@ -87,6 +90,18 @@ def quantize(x: torch.Tensor, meta: Fp8Meta, i: int, out: Optional[torch.Tensor]
         out = torch.empty(x.shape, dtype=meta.dtype, device=x.device)
     C().fp8_quant(x.contiguous(), out, meta.s(i), meta.a(i) if record else None, meta.fmt)
     return out
+
+
+def quantize_colsum(x: torch.Tensor, meta: Fp8Meta, i: int, key: str):
+    """(x8, part, nparts): fp8 copy of the 2-D bf16 x (amax recorded) and the
+    per-256-row-block column sums of x in a per-`key` workspace [nparts, N] --
+    fold them into a bias gradient (ops.kernels.reduce_partials_multi)."""
+    M, N = x.shape
+    nparts = math.ceil(M / 256)
+    x8 = torch.empty(M, N, dtype=meta.dtype, device=x.device)
+    part = K.workspace("qcs_" + key, nparts * N, x.device)[: nparts * N]
+    C().fp8_quant_colsum(x, x8, meta.s(i), meta.a(i), part, meta.fmt)
+    return x8, part, nparts
 
 
 def dequantize(x8: torch.Tensor, scale: float) -> torch.Tensor:
@@ -218,8 +233,9 @@ class Fp8Weights:
         self.by_param: Dict[int, Tuple[torch.Tensor, int]] = {}
 
     def add(self, param, transposed: bool = False) -> Tuple[torch.Tensor, int]:
-        """transposed: an e4m3 copy of param.compute_t (the [in, out] layout a
-        dgrad reads K-contiguous; ParamStore.add_transposed keeps it)."""
+        """transposed: an e4m3 copy of the weight transposed ([in, out], the
+        layout a dgrad reads K-contiguous), quantised straight from the bf16
+        compute copy by the transposing kernel (fp8_quant_t)."""
         shape = (param.shape[1], param.shape[0]) if transposed else param.shape
         w8 = torch.empty(shape, dtype=FP8, device=self.meta.device)
         slot = self.meta.slot(("wt:" if transposed else "w:") + param.name)
@@ -234,13 +250,24 @@ class Fp8Weights:
         return (id(param), transposed) in self.by_param
 
     def refresh(self) -> None:
-        """All weight copies in one launch per 64 weights (fp8_quant_multi),
-        each with its own scale and amax slot."""
-        for c0 in range(0, len(self.items), 64):
-            chunk = self.items[c0:c0 + 64]
-            C().fp8_quant_multi([p.compute_t if t else p.compute for p, _, _, t in chunk],
+        """All weight copies, each with its own scale and amax slot: the plain
+        ones in one launch per 64 weights (fp8_quant_multi), the transposed
+        ones one launch per weight shape (fp8_quant_t)."""
+        plain = [it for it in self.items if not it[3]]
+        for c0 in range(0, len(plain), 64):
+            chunk = plain[c0:c0 + 64]
+            C().fp8_quant_multi([p.compute for p, _, _, _ in chunk],
                                 [w8 for _, w8, _, _ in chunk], [slot for _, _, slot, _ in chunk],
                                 self.meta.scale, self.meta.amax)
+        groups: Dict[tuple, list] = {}
+        for it in self.items:
+            if it[3]:
+                groups.setdefault(tuple(it[0].shape), []).append(it)
+        for its in groups.values():
+            for c0 in range(0, len(its), 64):
+                chunk = its[c0:c0 + 64]
+                C().fp8_quant_t([p.compute for p, _, _, _ in chunk], [w8 for _, w8, _, _ in chunk],
+                                [slot for _, _, slot, _ in chunk], self.meta.scale, self.meta.amax)
 
     def calibrate(self) -> None:
         """Initial weight scales from their actual amax."""
@@ -257,8 +284,10 @@ class Fp8State:
     batched cross-attention K|V of the encoder output. Each of their inputs is
     the output of a LayerNorm (which then emits the e4m3 copy, `ln_slots`),
     except the first layer's Q|K|V input (the embedding), quantised by its
-    own kernel. The attention output projections stay bf16: their input, the
-    attention output, would need a separate quantisation pass."""
+    own kernel. With ATTN_PROJ_FP8 the attention output projections run e4m3
+    too (the attention output is quantised once), and the backward of every
+    attention projection -- dgrad and weight gradient -- runs on e5m2
+    gradients."""
 
     def __init__(self, model, margin: int = 0, backward: bool = True):
 
@@ -292,8 +321,6 @@ class Fp8State:
             feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
             self.ln_slots[id(feeder.gamma)] = xs
             if backward:
-                model.store.add_transposed(layer.ff1.w)
-                model.store.add_transposed(layer.ff2.w)
                 self.weights.add(layer.ff1.w, transposed=True)
                 self.weights.add(layer.ff2.w, transposed=True)
                 self.ffn_bwd_slots[id(layer.ff1.w)] = (self.gmeta.slot(f"gs:{id(layer)}"),
@@ -314,13 +341,35 @@ class Fp8State:
             proj(layer.qkv1.w, dec[i - 1].ln3 if i else None)
             proj(layer.q2.w, layer.ln1)
         proj(model.cross_kv.w, enc[-1].ln2)
+
+        # fp8 attention projections (ATTN_PROJ_FP8, with `backward`): the
+        # output projection runs e4m3 in the forward (input: the attention
+        # output, quantised once -- `attn_out`: weight -> (O slot, e5m2 slot
+        # of its output gradient ds)) and its dgrad / weight gradient on the
+        # e5m2 ds the LayerNorm backward emits; the input projections' dgrad
+        # and weight gradient run on the e5m2 copy of the attention backward's
+        # dQ|dK|dV (`proj_bwd`: weight -> e5m2 slot) against transposed e4m3
+        # weights and the forward's e4m3 input
+        self.attn_out: Dict[int, Tuple[int, int]] = {}
+        self.proj_bwd: Dict[int, int] = {}
+        if backward and ATTN_PROJ_FP8:
+            outs = [l.o.w for l in enc] + [w for l in dec for w in (l.o1.w, l.o2.w)]
+            for w in outs:
+                self.weights.add(w)
+                self.weights.add(w, transposed=True)
+                self.attn_out[id(w)] = (self.meta.slot("o:" + w.name), self.gmeta.slot("go:" + w.name))
+            ins = [l.qkv.w for l in enc] + [w for l in dec for w in (l.qkv1.w, l.q2.w)] + [model.cross_kv.w]
+            for w in ins:
+                self.weights.add(w, transposed=True)
+                self.proj_bwd[id(w)] = self.gmeta.slot("gp:" + w.name)
         self.weights.calibrate()
 
-    def linear(self, x2: torch.Tensor, w, b, want8: bool = False):
+    def linear(self, x2: torch.Tensor, w, b, want8: bool = False, keep_x8: Optional[list] = None):
         """y = x2 @ w^T + b with e4m3 operands when `w` is an fp8 attention
         projection (the input's e4m3 copy comes from its LayerNorm, else it is
         quantised here); None otherwise. want8: also the e4m3 copy of y from
-        the GEMM epilogue -- returns (y, y8, scale slot of y8)."""
+        the GEMM epilogue -- returns (y, y8, scale slot of y8). keep_x8 (a
+        list): receives (x8, its scale slot) for the fp8 weight gradient."""
         xs = self.proj_slots.get(id(w))
         if xs is None:
             return None
@@ -328,12 +377,26 @@ class Fp8State:
         x8 = self.stash.pop(xs, None)
         if x8 is None:
             x8 = quantize(x2, self.meta, xs)
+        x8 = x8.view(x2.shape)
+        if keep_x8 is not None:
+            keep_x8[:] = [x8, xs]
         ys = self.out_slots[id(w)] if want8 else None
         # want8: y is the dequantised y8 (the attention backward reads y and
         # must see the operands the e4m3 attention forward used)
-        y, y8 = gemm_fp8(x8.view(x2.shape), w8, b.master, self.meta, xs, ws, out8_slot=ys,
-                         c_deq=want8)
+        y, y8 = gemm_fp8(x8, w8, b.master, self.meta, xs, ws, out8_slot=ys, c_deq=want8)
         return (y, y8, ys) if want8 else y
+
+    def out_proj(self, o2: torch.Tensor, w, b):
+        """Attention output projection in e4m3 (ATTN_PROJ_FP8): o2 quantised
+        once (its e4m3 copy also feeds the weight gradient). Returns (s, o8)
+        or None when w is not covered."""
+        sl = self.attn_out.get(id(w))
+        if sl is None:
+            return None
+        o8 = quantize(o2.contiguous(), self.meta, sl[0]).view(o2.shape)
+        w8, ws = self.weights.get(w)
+        s, _ = gemm_fp8(o8, w8, b.master, self.meta, sl[0], ws)
+        return s, o8
 
     def after_step(self) -> None:
         self.meta.update()

@@ -428,3 +428,79 @@ def test_ln_bwd_emits_e5m2_ds(D, p):
     want = F.quantize(ds16, gm, i, record=False)
     assert (ds8.view(torch.uint8) == want.view(torch.uint8)).float().mean().item() > 0.999
     assert abs(gm.amax_values()[i].item() - ds16.float().abs().max().item()) <= 1e-6 * ds16.float().abs().max().item()
+
+
+def test_fp8_attention_projection_grads_match_bf16_path(monkeypatch):
+    """Attention projections in fp8 (e4m3 O-projection forward, e5m2 x e4m3
+    dgrads and weight gradients of every projection) vs the same step with
+    those projections in bf16: the projection weight / bias gradients agree
+    within fp8 gradient noise, and the loss matches."""
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
+
+    cfg = model_config("tiny", src_vocab=64, tgt_vocab=64, dropout=0.0)
+    data = SyntheticPairs(batch=16, src_len=16, tgt_len=17, src_vocab=64, tgt_vocab=64, copy_task=True, seed=0)
+    src, tgt = (t.cuda() for t in data.batch(0))
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(F, "ATTN_PROJ_FP8", mode)
+        m = Transformer(cfg).build("cuda", seed=1)
+        st = F.Fp8State(m)
+        assert bool(st.attn_out) == mode
+        rt = RunCtx(training=True, dropout=0.0, seed=3, store=m.store, fp8=st,
+                    ctr=torch.zeros(1, dtype=torch.int64, device="cuda"))
+        rt.wgrad = WgradQueue()
+        rt.wgrad.layers_per_step = 2 * cfg.layers
+        out = m.loss_and_backward(src, tgt, rt, 1.0)
+        torch.cuda.synchronize()
+        ps = []
+        for l in m.enc_layers:
+            ps += [l.qkv.w, l.qkv.b, l.o.w]
+        for l in m.dec_layers:
+            ps += [l.qkv1.w, l.q2.w, l.q2.b, l.o2.w]
+        ps += [m.cross_kv.w, m.cross_kv.b]
+        res[mode] = (float(out[0]), {p.name: p.grad.clone() for p in ps})
+    (l16, g16), (l8, g8) = res[False], res[True]
+    assert abs(l8 - l16) < 0.02 * abs(l16)
+    for n, a in g16.items():
+        rel = ((g8[n] - a).norm() / (a.norm() + 1e-12)).item()
+        assert rel < 0.15, (n, rel)
+
+
+@pytest.mark.parametrize("R,NC", [(1024, 3072), (300, 520), (64, 8)])
+def test_quant_t_matches_transpose_then_quantize(R, NC):
+    """The transposing weight quantisation equals quantising the transposed
+    weight, with each weight's amax in its own slot."""
+    torch.manual_seed(8)
+    meta = F.Fp8Meta(DEV)
+    ws = [(torch.randn(R, NC, device=DEV) * (i + 1) * 0.02).bfloat16() for i in range(3)]
+    slots = [meta.slot(f"w{i}") for i in range(3)]
+    for i, s in enumerate(slots):
+        meta.scale[s] = 2.0 ** (6 - i)
+    want = [F.quantize(w.t().contiguous(), meta, s, record=False) for w, s in zip(ws, slots)]
+    got = [torch.empty(NC, R, dtype=F.FP8, device=DEV) for _ in ws]
+    C().fp8_quant_t(ws, got, slots, meta.scale, meta.amax)
+    for g, w in zip(got, want):
+        assert torch.equal(g.view(torch.uint8), w.view(torch.uint8).view(NC, R))
+    am = meta.amax_values()
+    for w, s in zip(ws, slots):
+        assert am[s].item() == w.float().abs().max().item()
+
+
+def test_quant_colsum():
+    """e5m2 quantisation fused with per-row-block column sums (input-projection
+    bias gradients), strided input."""
+    torch.manual_seed(9)
+    gm = F.Fp8Meta(DEV, fmt=1)
+    i = gm.slot("g")
+    gm.scale[i] = 2.0 ** 10
+    base = (torch.randn(1000, 3080, device=DEV) * 0.01).bfloat16()
+    x = base[:, :3072]
+    x8, part, nparts = F.quantize_colsum(x, gm, i, "test")
+    want = F.quantize(x.contiguous(), gm, i, record=False).view(1000, 3072)
+    assert torch.equal(x8.view(torch.uint8), want.view(torch.uint8))
+    cs = part.view(nparts, 3072).sum(0)
+    ref = x.float().sum(0)
+    assert torch.allclose(cs, ref, rtol=1e-4, atol=1e-4)
+    assert gm.amax_values()[i].item() == x.float().abs().max().item()
