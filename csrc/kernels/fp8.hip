@@ -452,7 +452,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
 #pragma unroll
   for (int j = 0; j < TN; ++j) fb[j] = f8::frag(smem + A_BYTES, bbase + 16 * j, lane);
 
-  for (int kt = 0; kt < nk; ++kt) {
+  // MODE 2: tile kt + STAGES exists (steady, branch-free); 1: kt + 1 exists
+  // (tail: drain, no issue); 0: the last tile. With the tail's branches
+  // inside one loop body the compiler sank the MFMAs past the wait, barrier,
+  // DMA issue and fragment reads into the latch (scripts/isa_loops.py).
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
     tdg::lgkm_wait<0>();
 #pragma unroll
     for (int i = 0; i < TM; ++i) tdg::tie(fa[i]);
@@ -466,11 +471,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], AF,
                                                                      0, 0, 127, 0, 127);
     __builtin_amdgcn_s_setprio(0);
-    if (kt + 1 < nk) {
-      if (kt + STAGES - 1 < nk) f8::wait_vmcnt<(STAGES - 2) * PT>();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MODE >= 1) {
+      if constexpr (MODE == 2) f8::wait_vmcnt<(STAGES - 2) * PT>();
       else f8::wait_vmcnt<0>();
       f8::lds_barrier();
-      if (kt + STAGES < nk) {
+      if constexpr (MODE == 2) {
         char* ns = smem + (kt % STAGES) * SB;
         ga.issue(A, lda, M, m0, (kt + STAGES) * BK8, ns, wid);
         gb.issue(B, ldb, N, n0, (kt + STAGES) * BK8, ns + A_BYTES, wid);
@@ -481,7 +487,14 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = f8::frag(nx + A_BYTES, bbase + 16 * j, lane);
     }
-  }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + STAGES < nk; ++kt) kstep(kt, std::integral_constant<int, 2>{});
+#pragma unroll
+  for (int d = 0; d < STAGES - 1; ++d)
+    if (kt + 1 < nk) kstep(kt++, std::integral_constant<int, 1>{});
+  kstep(kt, std::integral_constant<int, 0>{});
 
   f8::lds_barrier();
   Epi::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
@@ -604,20 +617,22 @@ __global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
     acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], AF, 0,
                                                                  0, 127, 0, 127);
   };
-  for (int kt = 0; kt < nk; ++kt) {
+  // branch-free steady step + tail instantiations (see wgrad_fp8_kernel)
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
+    constexpr bool more1 = MODE >= 1, more2 = MODE == 2;
     const char* st = smem + (kt & 1) * SB;
     const char* nx = smem + ((kt + 1) & 1) * SB;
-    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
     // ---- P0: a0 x b0; read B1(kt); issue A0(kt+2)
     // B1(kt) landed: younger issues A1(kt), A0/B0/B1/A1(kt+1) -- or fewer at the tail
-    if (more1) f8::wait_vmcnt<20>();
+    if constexpr (more1) f8::wait_vmcnt<20>();
     else f8::wait_vmcnt<4>();
     f8::lds_barrier();  // (lgkmcnt(0): last phase's fragment reads)
 #pragma unroll
     for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) tdg::tie(fb[j]);
-    if (more2) issue(kt + 2, 0);
+    if constexpr (more2) issue(kt + 2, 0);
 #pragma unroll
     for (int j = 4; j < 8; ++j) fb[j] = f8::frag(st + 3 * HB, br + 16 * (j - 4), lane);
     __builtin_amdgcn_s_setprio(1);
@@ -626,15 +641,16 @@ __global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- P1: a0 x b1; read A1(kt); issue B0(kt+2)
     // A1(kt) landed: younger A0/B0/B1/A1(kt+1), A0(kt+2)
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<16>();
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<16>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
 #pragma unroll
     for (int j = 4; j < 8; ++j) tdg::tie(fb[j]);
-    if (more2) issue(kt + 2, 1);
+    if constexpr (more2) issue(kt + 2, 1);
 #pragma unroll
     for (int i = 4; i < 8; ++i) fa[i] = f8::frag(st + 1 * HB, ar + 16 * (i - 4), lane);
     __builtin_amdgcn_s_setprio(1);
@@ -643,16 +659,17 @@ __global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
 #pragma unroll
       for (int j = 4; j < 8; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- P2: a1 x b1; read A0(kt+1); issue B1(kt+2)
     // A0(kt+1) landed: younger B0/B1/A1(kt+1), A0/B0(kt+2)
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<12>();
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<12>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
 #pragma unroll
     for (int i = 4; i < 8; ++i) tdg::tie(fa[i]);
-    if (more2) issue(kt + 2, 2);
-    if (more1) {
+    if constexpr (more2) issue(kt + 2, 2);
+    if constexpr (more1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = f8::frag(nx + 0 * HB, ar + 16 * i, lane);
     }
@@ -662,26 +679,32 @@ __global__ __launch_bounds__(256) void gemm_fp8_w1_kernel(
 #pragma unroll
       for (int j = 4; j < 8; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- P3: a1 x b0; read B0(kt+1) per column behind its MFMAs; issue A1(kt+2)
     // B0(kt+1) landed: younger B1/A1(kt+1), A0/B0/B1(kt+2)
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<8>();
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<8>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
-    if (more1) {
+    if constexpr (more1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
     }
-    if (more2) issue(kt + 2, 3);
+    if constexpr (more2) issue(kt + 2, 3);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 4; i < 8; ++i) mfma(i, j);
       __builtin_amdgcn_s_setprio(0);
-      if (more1) fb[j] = f8::frag(nx + 2 * HB, br + 16 * j, lane);
+      if constexpr (more1) fb[j] = f8::frag(nx + 2 * HB, br + 16 * j, lane);
     }
-  }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) kstep(kt, std::integral_constant<int, 2>{});
+  if (kt + 1 < nk) kstep(kt++, std::integral_constant<int, 1>{});
+  kstep(kt, std::integral_constant<int, 0>{});
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   f8::lds_barrier();
@@ -841,18 +864,27 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
     acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[j], fa[i], acc[i][j], 0, 1,
                                                                  0, 127, 0, 127);
   };
-  for (int kt = 0; kt < nk; ++kt) {
+  // One K-step (128 tokens) in four phases. MODE 2: tiles kt+1 and kt+2
+  // exist; 1: only kt+1; 0: the last tile. The steady loop is branch-free
+  // (the tail steps are separate instantiations): with `if (more2)` branches
+  // inside the body the compiler sank all 64 MFMAs of a step out of their
+  // phases into the loop latch, behind every wait and barrier (measured ISA,
+  // scripts/isa_loops.py), which serialised the DMA / LDS work and the MFMAs.
+  // sched_barrier(0) pins each phase's boundary.
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
+    constexpr bool more1 = MODE >= 1, more2 = MODE == 2;
     const char* st = smem + (kt & 1) * SB;
     const char* nx = smem + ((kt + 1) & 1) * SB;
-    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
-    if (more1) f8::wait_vmcnt<20>();
+    // ---- P0: a0 x b0; read B1(kt); issue A0(kt+2)
+    if constexpr (more1) f8::wait_vmcnt<20>();
     else f8::wait_vmcnt<4>();
     f8::lds_barrier();
 #pragma unroll
     for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) tdg::tie(fb[j]);
-    if (more2) issue(kt + 2, 0);
+    if constexpr (more2) issue(kt + 2, 0);
 #pragma unroll
     for (int j = 4; j < 8; ++j) fb[j] = wf8::frag(st + 3 * HB, br + 16 * (j - 4), lane);
     __builtin_amdgcn_s_setprio(1);
@@ -861,13 +893,15 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
 #pragma unroll
       for (int j = 0; j < 4; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<16>();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- P1: a0 x b1; read A1(kt); issue B0(kt+2)
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<16>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
 #pragma unroll
     for (int j = 4; j < 8; ++j) tdg::tie(fb[j]);
-    if (more2) issue(kt + 2, 1);
+    if constexpr (more2) issue(kt + 2, 1);
 #pragma unroll
     for (int i = 4; i < 8; ++i) fa[i] = wf8::frag(st + 1 * HB, ar + 16 * (i - 4), lane);
     __builtin_amdgcn_s_setprio(1);
@@ -876,14 +910,16 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
 #pragma unroll
       for (int j = 4; j < 8; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<12>();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- P2: a1 x b1; read A0(kt+1); issue B1(kt+2)
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<12>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
 #pragma unroll
     for (int i = 4; i < 8; ++i) tdg::tie(fa[i]);
-    if (more2) issue(kt + 2, 2);
-    if (more1) {
+    if constexpr (more2) issue(kt + 2, 2);
+    if constexpr (more1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = wf8::frag(nx + 0 * HB, ar + 16 * i, lane);
     }
@@ -893,24 +929,31 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
 #pragma unroll
       for (int j = 4; j < 8; ++j) mfma(i, j);
     __builtin_amdgcn_s_setprio(0);
-    if (more2) f8::wait_vmcnt<20>();
-    else if (more1) f8::wait_vmcnt<8>();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- P3: a1 x b0; read B0(kt+1) per column behind its MFMAs; issue A1(kt+2)
+    if constexpr (more2) f8::wait_vmcnt<20>();
+    else if constexpr (more1) f8::wait_vmcnt<8>();
     else f8::wait_vmcnt<0>();
     f8::lds_barrier();
-    if (more1) {
+    if constexpr (more1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) tdg::tie(fa[i]);
     }
-    if (more2) issue(kt + 2, 3);
+    if constexpr (more2) issue(kt + 2, 3);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 4; i < 8; ++i) mfma(i, j);
       __builtin_amdgcn_s_setprio(0);
-      if (more1) fb[j] = wf8::frag(nx + 2 * HB, br + 16 * j, lane);
+      if constexpr (more1) fb[j] = wf8::frag(nx + 2 * HB, br + 16 * j, lane);
     }
-  }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) kstep(kt, std::integral_constant<int, 2>{});
+  if (kt + 1 < nk) kstep(kt++, std::integral_constant<int, 1>{});
+  kstep(kt, std::integral_constant<int, 0>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 

@@ -9,7 +9,7 @@ from tensorflow_distributed_on_gke_amd.ops import fp8 as F
 from tensorflow_distributed_on_gke_amd.ops import kernels as kk
 
 T, reps = 8192, int(os.environ.get("REPS", "10"))
-spec = [(4096, 1024), (1024, 4096)] * 6
+spec = [(4096, 1024)] * 6 + [(1024, 4096)] * 6
 gm, am = F.Fp8Meta("cuda", fmt=1), F.Fp8Meta("cuda")
 dys, xs, dws, sas, sbs, d16, x16 = [], [], [], [], [], [], []
 for i, (M, N) in enumerate(spec):
