@@ -343,8 +343,37 @@ struct EpiLds {
     f32x4 bn[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) bn[j] = load_bias4<EPI>(bias, nw0 + 16 * j + 4 * g, N);
+    using VecT = typename std::conditional<OUT_F32, f32x4, short8_t>::type;
+    // Epilogue operands not prefetched by the caller (ReLU mask, beta * C_old)
+    // are loaded per pass BEFORE the image is written, all ITER chunks in
+    // flight at once. Loaded inside the store loop, each chunk's load sat
+    // behind its own s_waitcnt vmcnt(0): ITER (8-16) serial memory round trips
+    // per wave at the end of every tile (measured ISA of gemm256<NN, DRELU>).
+    // Out-of-range chunks load the operand's first chunk instead (branch-free;
+    // the value is never used).
+    constexpr bool AUX8 = EPI == EPI_DRELU && EPC == 8;
+    const bool loc_aux = AUX8 && !(PRE && use_aux) && vok;
+    const bool loc_c = !(PRE && use_c) && beta != 0.f && vok;
 #pragma unroll
     for (int p = 0; p < TM * 16 / RPASS; ++p) {
+      int4 la[ITER], lc[ITER];
+      if (loc_aux || loc_c) {
+#pragma unroll
+        for (int t = 0; t < ITER; ++t) {
+          const int id = lane + 64 * t;
+          const int m = mw0 + p * RPASS + id / CPR, n = nw0 + (id % CPR) * EPC;
+          const bool in = m < M && n + EPC <= N;
+          if (loc_aux) {
+            const bf16_t* a = in ? aux + (size_t)m * ldaux + n : aux;
+            la[t] = *reinterpret_cast<const int4*>(a);
+          }
+          if (loc_c) {
+            const char* c = in ? reinterpret_cast<const char*>(Cv) + ((size_t)m * ldc + n) * ES
+                               : reinterpret_cast<const char*>(Cv);
+            lc[t] = *reinterpret_cast<const int4*>(c);
+          }
+        }
+      }
       // 1) accumulators (alpha, bias, relu applied) -> image
 #pragma unroll
       for (int ii = 0; ii < RPASS / 16; ++ii) {
@@ -379,16 +408,14 @@ struct EpiLds {
         const int n = nw0 + ch * EPC;
         // vector types only (a reinterpret_cast of a local array would put
         // it in private memory)
-        using VecT = typename std::conditional<OUT_F32, f32x4, short8_t>::type;
         VecT vals = *reinterpret_cast<const VecT*>(wimg + row * SP + ch * 16);
         if (m >= M || n >= N) continue;
         char* cp = reinterpret_cast<char*>(Cv) + ((size_t)m * ldc + n) * ES;
         if (vok && n + EPC <= N) {
           if constexpr (EPI == EPI_DRELU) {
             if constexpr (EPC == 8) {
-              const short8_t x = (PRE && use_aux)
-                                     ? __builtin_bit_cast(short8_t, pre_aux[t])
-                                     : *reinterpret_cast<const short8_t*>(aux + (size_t)m * ldaux + n);
+              // vok: either the caller prefetched the mask or la[] holds it
+              const short8_t x = __builtin_bit_cast(short8_t, (PRE && use_aux) ? pre_aux[t] : la[t]);
 #pragma unroll
               for (int e = 0; e < 8; ++e)
                 if (!(bf2f((bf16_t)x[e]) > 0.f)) vals[e] = 0;
@@ -400,8 +427,7 @@ struct EpiLds {
             }
           }
           if (beta != 0.f) {
-            const VecT old = (PRE && use_c) ? __builtin_bit_cast(VecT, pre_c[t])
-                                            : *reinterpret_cast<const VecT*>(cp);
+            const VecT old = __builtin_bit_cast(VecT, (PRE && use_c) ? pre_c[t] : lc[t]);
             if constexpr (OUT_F32) {
               vals += beta * old;
             } else {

@@ -183,12 +183,34 @@ def wgrad_fp8(dy8s, sas, x8s, sbs, dws, beta: float = 0.0) -> None:
     """dws[i][M,N] (f32, =|+= beta) = dequant(dy8s[i][T,M]^T @ x8s[i][T,N]):
     weight gradients from the e5m2 gradient and the e4m3 activation copies
     the step already holds (token-major, read through the transposing LDS
-    path: csrc/kernels/fp8.hip wgrad_fp8_kernel), one launch per 64
-    problems. sas / sbs: the one-element scale tensors of each operand."""
-    for c0 in range(0, len(dws), 64):
-        sl = slice(c0, c0 + 64)
-        C().wgrad_fp8(list(dy8s[sl]), list(x8s[sl]), list(dws[sl]), list(sas[sl]), list(sbs[sl]),
-                      float(beta))
+    path: csrc/kernels/fp8.hip wgrad_fp8_kernel). sas / sbs: the one-element
+    scale tensors of each operand. One launch per token count T, shape
+    classes adjacent, at most 64 problems in 8 shape classes per launch (the
+    kernel's argument block)."""
+    def key(i):
+        return (dy8s[i].shape[1], x8s[i].shape[1], dy8s[i].stride(0), x8s[i].stride(0),
+                dws[i].stride(0))
+
+    by_t = {}
+    for i in range(len(dws)):
+        by_t.setdefault(dy8s[i].shape[0], []).append(i)
+    for idx in by_t.values():
+        idx.sort(key=key)
+        launch, classes = [], []
+        for i in idx + [None]:
+            if i is not None:
+                k = key(i)
+                new_cls = not classes or classes[-1] != k
+                if len(launch) < 64 and (not new_cls or len(classes) < 8):
+                    launch.append(i)
+                    if new_cls:
+                        classes.append(k)
+                    continue
+            C().wgrad_fp8([dy8s[j] for j in launch], [x8s[j] for j in launch],
+                          [dws[j] for j in launch], [sas[j] for j in launch],
+                          [sbs[j] for j in launch], float(beta))
+            if i is not None:
+                launch, classes = [i], [key(i)]
 
 
 def wgrad_fp8_ok(T: int, M: int, N: int) -> bool:
