@@ -101,6 +101,8 @@ void check_bf16(const Tensor& t, const char* n) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, " must be bfloat16");
   TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
 }
+void check_f8_fmt(const Tensor& t, int64_t fmt, const char* n);
+unsigned* amax_ptr(const optional<Tensor>& t);
 void check_f32(const Tensor& t, const char* n) {
   TORCH_CHECK(t.scalar_type() == at::kFloat, n, " must be float32");
   TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
@@ -260,7 +262,9 @@ void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
 // per-tensor scales (x8 = e4m3(x * s), one-element f32 device tensors)
 void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Tensor& out,
                   const Tensor& lse, const optional<Tensor>& kv_len, const Tensor& sq,
-                  const Tensor& sk, const Tensor& sv, double scale, bool causal) {
+                  const Tensor& sk, const Tensor& sv, double scale, bool causal,
+                  const optional<Tensor>& out8, const optional<Tensor>& so8,
+                  const optional<Tensor>& amax8) {
   for (auto* t : {&q8, &k8, &v8}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat8_e4m3fn, "attn_fwd_fp8: e4m3 q/k/v");
     TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1 && t->size(3) == 64,
@@ -298,6 +302,16 @@ void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Te
   if (kv_len.has_value()) {
     TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
     a.kv_len = kv_len->data_ptr<int>();
+  }
+  if (out8.has_value()) {
+    check_f8_fmt(*out8, 0, "out8");
+    TORCH_CHECK(out8->sizes() == out.sizes() && out8->strides() == out.strides() && so8.has_value() &&
+                    amax8.has_value(),
+                "attn_fwd_fp8: out8 has out's shape / strides, with so8 and amax8");
+    check_f32(*so8, "so8");
+    a.out8 = (uint8_t*)out8->data_ptr();
+    a.so8 = so8->data_ptr<float>();
+    a.amax8 = amax_ptr(amax8);
   }
   a.sq8 = sq.data_ptr<float>();
   a.sk8 = sk.data_ptr<float>();
@@ -722,10 +736,17 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const optional<Tensor>& C, const
   check_f32(sa, "sa");
   check_f32(sb, "sb");
   TORCH_CHECK(K % 128 == 0 && lda % 16 == 0 && ldb % 16 == 0, "gemm_fp8: K % 128, ld % 16");
-  TORCH_CHECK(A.numel() >= (M - 1) * lda + K && B.numel() >= (N - 1) * ldb + K, "gemm_fp8: A/B extent");
+  // flag 32: B is N-contiguous [K][ldb] (a plain weight as its dgrad's B operand)
+  const bool bt = (epi & 32) != 0;
+  TORCH_CHECK(A.numel() >= (M - 1) * lda + K &&
+                  (bt ? B.numel() >= (K - 1) * ldb + N && ldb >= N && N % 16 == 0
+                      : B.numel() >= (N - 1) * ldb + K),
+              "gemm_fp8: A/B extent");
+  TORCH_CHECK(!bt || (cfg == 0 && afmt == 1 && cfmt == 1),
+              "gemm_fp8: N-contiguous B runs the e5m2 backward 128x128 config (cfg 0) only");
   if (bias.has_value()) check_f32(*bias, "bias");
   const int64_t epi_id = epi & 15;  // (flag 16: C = dequant(C8))
-  TORCH_CHECK((epi & ~int64_t(31)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
+  TORCH_CHECK((epi & ~int64_t(63)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
   TORCH_CHECK(!(epi & 16) || C8.has_value(), "gemm_fp8: C = dequant(C8) needs C8");
   TORCH_CHECK(epi_id == 0 || epi_id == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
   TORCH_CHECK(epi_id != 3 || aux.has_value() != aux8.has_value(),

@@ -27,5 +27,10 @@ struct AttnArgs {
   const float* sq8;
   const float* sk8;
   const float* sv8;
+  // optional e4m3 copy of O (attn_fwd_fp8): out8 = e4m3(bf16(O) * so8[0]),
+  // same element strides as out, amax recorded into the slot amax8
+  uint8_t* out8;
+  const float* so8;
+  unsigned* amax8;
 };
 }  // namespace tdg

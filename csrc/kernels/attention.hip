@@ -677,16 +677,42 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   float lu = l;
   lu += __shfl_xor(lu, 16, 64);
   lu += __shfl_xor(lu, 32, 64);
-  if (qrow >= a.Lq) return;
+  const bool valid = qrow < a.Lq;
   const float inv = lu > 0.f ? 1.f / (lu * 448.f * a.sv8[0]) : 0.f;
-  bf16_t* op = a.out + b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
+  const long long ooff = b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
+  bf16_t* op = a.out + ooff;
+  // e4m3 copy of O for the e4m3 output projection: from the bf16-rounded
+  // values (what quantising the bf16 O gives), wave amax -> one atomic
+  const float so = a.out8 ? a.so8[0] : 0.f;
+  float am = 0.f;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
-    const uint32_t lo = (uint32_t)f2bf(oacc[dt][0] * inv) | ((uint32_t)f2bf(oacc[dt][1] * inv) << 16);
-    const uint32_t hi = (uint32_t)f2bf(oacc[dt][2] * inv) | ((uint32_t)f2bf(oacc[dt][3] * inv) << 16);
-    *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    bf16_t e[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) e[r] = f2bf(oacc[dt][r] * inv);
+    if (valid) {
+      const uint32_t lo = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
+      const uint32_t hi = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
+    }
+    if (a.out8) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = bf2f(e[r]);
+        am = fmaxf(am, valid ? fabsf(v[r]) : 0.f);
+      }
+      int w8 = pack2_e4m3<false>(v[0] * so, v[1] * so, 0);
+      w8 = pack2_e4m3<true>(v[2] * so, v[3] * so, w8);
+      if (valid) *reinterpret_cast<int*>(a.out8 + ooff + 16 * dt + 4 * g) = w8;
+    }
   }
-  if (g == 0) a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + log2f(lu) : INFINITY;
+  if (a.out8) {
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 64));
+    if (lane == 0) atomic_amax(amax_word(a.amax8, blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z), am);
+  }
+  if (valid && g == 0) a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + log2f(lu) : INFINITY;
 }
 
 // ============================================================================ dK, dV

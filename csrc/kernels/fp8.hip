@@ -141,6 +141,9 @@ enum { F8_EPI_NONE = 0, F8_EPI_BIAS = 1, F8_EPI_BIAS_RELU = 2, F8_EPI_DRELU = 3,
 // (F8_EPI_DRELU8: the ReLU-backward mask from F8Extra::aux8, host-selected)
 // flag on top of the epilogue id: C = dequant(C8) (needs C8)
 constexpr int F8_EPI_CDEQ = 16;
+// host-side flag of tdg_gemm_fp8's epi: B is N-contiguous ([K][ldb], e.g. a
+// weight [out][in] as the B operand of its dgrad; 128x128 tile only)
+constexpr int F8_B_NCONTIG = 32;
 
 // Backward-GEMM extras: the ReLU mask operand (F8_EPI_DRELU: out = 0 where
 // aux <= 0) and C = alpha A B^T + beta C.
@@ -393,7 +396,65 @@ struct F8Epi {
 
 // AF: format of A (0 e4m3, 1 e5m2: the gradient operand of a dgrad), B is
 // e4m3; CF: format of the optional C8 copy.
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int AF = 0, int CF = 0>
+namespace wf8 {
+__device__ __forceinline__ int sw(int t) { return ((t >> 1) & 3) | (((t >> 5) & 1) << 2); }
+// byte offset of (token row t, image column x) in a [128][128 B] half image
+__device__ __forceinline__ int off(int t, int x) { return t * 128 + ((((x >> 4) ^ sw(t)) & 7) << 4) + (x & 15); }
+// transposing 8-byte read (untracked: the caller waits with lgkmcnt)
+__device__ __forceinline__ uint64_t tr8(const void* p) {
+  uint64_t r;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+// MFMA fragment of image columns base..base+15 (one per lane & 15), tokens
+// 32 (lane >> 4) .. +31: four transposing reads of 8 tokens
+__device__ __forceinline__ i32x8 frag(const char* img, int base, int lane) {
+  const int g = lane >> 4, w = lane & 15, q = w >> 1, p = w & 1;
+  uint64_t r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = 32 * g + 8 * j + q;
+    r[j] = tr8(img + off(t, base + 8 * p));
+  }
+  return i32x8{(int)r[0], (int)(r[0] >> 32), (int)r[1], (int)(r[1] >> 32),
+               (int)r[2], (int)(r[2] >> 32), (int)r[3], (int)(r[3] >> 32)};
+}
+}  // namespace wf8
+
+// global -> LDS staging of a 128 (K) x 128-byte (N) tile of an N-CONTIGUOUS
+// operand ([K][ld]: a weight [out][in] read as the B operand of its dgrad,
+// B(n, k) = W[k][n]) into the wf8 image (16-byte chunk c of row t at chunk
+// c ^ wf8::sw(t)); fragments come from wf8::frag (ds_read_b64_tr_b8), so the
+// dgrad needs no transposed weight copy. NW = 4 waves, 4 pieces of 8 rows
+// x 128 B each.
+template <int NW>
+struct StageT {
+  static constexpr int P = 16 / NW;
+  static_assert(P * NW == 16, "16 pieces of 1 KiB per 16 KiB image");
+  uint32_t off[P];
+  __device__ __forceinline__ void init(int wid, int lane, int n0, int N, int ld) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int row = (wid * P + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ wf8::sw(row);
+      int n = n0 + 16 * c;
+      n = n + 16 <= N ? n : 0;  // past the operand: never stored (N % 16 == 0)
+      off[i] = (uint32_t)row * (uint32_t)ld + (uint32_t)n;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ X, int ld, int k0, char* lds,
+                                        int wid) const {
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(X + (size_t)k0 * ld + off[i]),
+          (__attribute__((address_space(3))) void*)(lds + (wid * P + i) * 1024), 16, 0, 0);
+  }
+};
+
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int AF = 0, int CF = 0,
+          bool BT = false>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
@@ -403,7 +464,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int A_BYTES = BM * BK8, B_BYTES = BN * BK8, SB = A_BYTES + B_BYTES;
   using GA = f8::Stage<BM, NW>;
-  using GB = f8::Stage<BN, NW>;
+  // BT: B is N-contiguous ([K][ldb], StageT + transposing fragment reads)
+  static_assert(!BT || (BN == 128 && NW == 4), "N-contiguous B: 128-column tiles on 4 waves");
+  using GB = typename std::conditional<BT, StageT<NW>, f8::Stage<BN, NW>>::type;
   constexpr int PT = GA::P + GB::P;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -429,7 +492,16 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   GA ga;
   GB gb;
   ga.init(wid, lane);
-  gb.init(wid, lane);
+  if constexpr (BT) gb.init(wid, lane, n0, N, ldb);
+  else gb.init(wid, lane);
+  auto issue_b = [&](int k0, char* dst) {
+    if constexpr (BT) gb.issue(B, ldb, k0, dst, wid);
+    else gb.issue(B, ldb, N, n0, k0, dst, wid);
+  };
+  auto frag_b = [&](const char* img, int base) {
+    if constexpr (BT) return wf8::frag(img, base, lane);
+    else return f8::frag(img, base, lane);
+  };
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -440,7 +512,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   for (int s = 0; s < STAGES; ++s)
     if (s < nk) {
       ga.issue(A, lda, M, m0, s * BK8, smem + s * SB, wid);
-      gb.issue(B, ldb, N, n0, s * BK8, smem + s * SB + A_BYTES, wid);
+      issue_b(s * BK8, smem + s * SB + A_BYTES);
     }
   if (nk >= STAGES) f8::wait_vmcnt<(STAGES - 1) * PT>();
   else f8::wait_vmcnt<0>();
@@ -450,7 +522,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
 #pragma unroll
   for (int i = 0; i < TM; ++i) fa[i] = f8::frag(smem, abase + 16 * i, lane);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) fb[j] = f8::frag(smem + A_BYTES, bbase + 16 * j, lane);
+  for (int j = 0; j < TN; ++j) fb[j] = frag_b(smem + A_BYTES, bbase + 16 * j);
 
   // MODE 2: tile kt + STAGES exists (steady, branch-free); 1: kt + 1 exists
   // (tail: drain, no issue); 0: the last tile. With the tail's branches
@@ -479,13 +551,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
       if constexpr (MODE == 2) {
         char* ns = smem + (kt % STAGES) * SB;
         ga.issue(A, lda, M, m0, (kt + STAGES) * BK8, ns, wid);
-        gb.issue(B, ldb, N, n0, (kt + STAGES) * BK8, ns + A_BYTES, wid);
+        issue_b((kt + STAGES) * BK8, ns + A_BYTES);
       }
       const char* nx = smem + ((kt + 1) % STAGES) * SB;
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[i] = f8::frag(nx, abase + 16 * i, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = f8::frag(nx + A_BYTES, bbase + 16 * j, lane);
+      for (int j = 0; j < TN; ++j) fb[j] = frag_b(nx + A_BYTES, bbase + 16 * j);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -745,31 +817,6 @@ struct WF8Args {
   int ncls;
 };
 
-namespace wf8 {
-__device__ __forceinline__ int sw(int t) { return ((t >> 1) & 3) | (((t >> 5) & 1) << 2); }
-// byte offset of (token row t, image column x) in a [128][128 B] half image
-__device__ __forceinline__ int off(int t, int x) { return t * 128 + ((((x >> 4) ^ sw(t)) & 7) << 4) + (x & 15); }
-// transposing 8-byte read (untracked: the caller waits with lgkmcnt)
-__device__ __forceinline__ uint64_t tr8(const void* p) {
-  uint64_t r;
-  const uint32_t a = (uint32_t)(uintptr_t)p;
-  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r) : "v"(a) : "memory");
-  return r;
-}
-// MFMA fragment of image columns base..base+15 (one per lane & 15), tokens
-// 32 (lane >> 4) .. +31: four transposing reads of 8 tokens
-__device__ __forceinline__ i32x8 frag(const char* img, int base, int lane) {
-  const int g = lane >> 4, w = lane & 15, q = w >> 1, p = w & 1;
-  uint64_t r[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int t = 32 * g + 8 * j + q;
-    r[j] = tr8(img + off(t, base + 8 * p));
-  }
-  return i32x8{(int)r[0], (int)(r[0] >> 32), (int)r[1], (int)(r[1] >> 32),
-               (int)r[2], (int)(r[2] >> 32), (int)r[3], (int)(r[3] >> 32)};
-}
-}  // namespace wf8
 
 __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int T, float beta) {
   constexpr int TM = 8, TN = 8;
@@ -1239,7 +1286,7 @@ __global__ void fp8_dequant_kernel(const uint8_t* __restrict__ x8, float* __rest
 using namespace tdg;
 
 namespace {
-template <int BM, int BN, int WM, int WN, int ST, int EPI, int AF = 0, int CF = 0>
+template <int BM, int BN, int WM, int WN, int ST, int EPI, int AF = 0, int CF = 0, bool BT = false>
 int launch_f8(const void* A, const void* B, void* C, const float* bias, const float* sa,
               const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
               int lda, int ldb, int ldc, int ldc8, const F8Extra& ex, hipStream_t st) {
@@ -1247,12 +1294,12 @@ int launch_f8(const void* A, const void* B, void* C, const float* bias, const fl
   constexpr int lds = std::max(ST * (BM + BN) * BK8, img);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF>,
+    hipFuncSetAttribute((const void*)gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF, BT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF>), dim3(tiles),
+  hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF, BT>), dim3(tiles),
                      dim3(WM * WN * 64), lds, st, (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C,
                      bias, sa, sb, (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
   return 0;
@@ -1308,7 +1355,7 @@ static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float*
                              const float* sa, const float* sb, void* C8, const float* sc8,
                              unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
                              int ldc8, int epi, int cfg, int afmt, int cfmt, const F8Extra& ex,
-                             hipStream_t st);
+                             hipStream_t st, bool bt);
 
 // aux8: the ReLU-backward mask as 8-bit activations (instead of bf16 aux);
 // colsum_out: also colsum_out[N] (=|+= colsum_beta) the column sums of the
@@ -1323,7 +1370,9 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
                             float colsum_beta, float* ws, hipStream_t st) {
   if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
   const int cdeq = (epi & F8_EPI_CDEQ) != 0;
-  epi &= ~F8_EPI_CDEQ;
+  const bool bt = (epi & F8_B_NCONTIG) != 0;
+  epi &= ~(F8_EPI_CDEQ | F8_B_NCONTIG);
+  if (bt && (cfg != 0 || N % 16 != 0 || ldb < N || afmt != 1 || cfmt != 1)) return -6;
   if (cdeq && !C8) return -2;
   if (!C && (beta != 0.f || cdeq)) return -2;
   if (colsum_out && (!ws || cfg != 0)) return -2;  // (partials: the 128x128 / 2x2 tile)
@@ -1331,20 +1380,29 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
                    colsum_out ? ws : nullptr};
   if (colsum_out) {
     const int rc = tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc,
-                                     ldc8, epi, cfg, afmt, cfmt, ex, st);
+                                     ldc8, epi, cfg, afmt, cfmt, ex, st, bt);
     if (rc) return rc;
     launch_reduce_partials(ws, colsum_out, N, cdiv(M, 128) * 2, colsum_beta, st);
     return 0;
   }
   return tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, epi,
-                           cfg, afmt, cfmt, ex, st);
+                           cfg, afmt, cfmt, ex, st, bt);
 }
 
 static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float* bias,
                              const float* sa, const float* sb, void* C8, const float* sc8,
                              unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
                              int ldc8, int epi, int cfg, int afmt, int cfmt, const F8Extra& ex,
-                             hipStream_t st) {
+                             hipStream_t st, bool bt) {
+  if (bt) {  // e5m2 x N-contiguous e4m3 (validated by the caller: cfg 0)
+    if (epi == F8_EPI_DRELU && ex.aux8)
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU8, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    if (epi == F8_EPI_DRELU)
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    if (epi == F8_EPI_NONE)
+      return launch_f8<128, 128, 2, 2, 2, F8_EPI_NONE, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    return -1;
+  }
   if (afmt == 0 && cfmt == 0) {
     switch (epi) {
       case F8_EPI_NONE: return tiles_f8<F8_EPI_NONE>(cfg, A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);

@@ -344,10 +344,12 @@ def _fp8_grad_bias(g: torch.Tensor, g_slot: int, b: Param, rt: RunCtx, key: str)
 
 
 def _fp8_dgrad_into(g8, g_slot: int, w: Param, out: torch.Tensor, rt: RunCtx, beta: float) -> None:
-    """out (=|+= beta) dequant(g8 (e5m2) @ w) against w's transposed e4m3 copy."""
+    """out (=|+= beta) dequant(g8 (e5m2) @ w) against w's e4m3 copy (read
+    N-contiguous by the kernel, fp8.DGRAD_PLAIN_W; else its transposed copy)."""
     st = rt.fp8
-    wt8, swt = st.weights.get(w, transposed=True)
-    fp8.gemm_bf8_dgrad(g8, st.gmeta, g_slot, wt8, st.meta, swt, out, beta=beta)
+    wt8, swt = st.weights.get(w, transposed=not fp8.DGRAD_PLAIN_W)
+    fp8.gemm_bf8_dgrad(g8, st.gmeta, g_slot, wt8, st.meta, swt, out, beta=beta,
+                       w_plain=fp8.DGRAD_PLAIN_W)
 
 
 # =============================================================================== LN helpers
@@ -512,11 +514,14 @@ class SelfAttnBlockFn(torch.autograd.Function):
             if qkv is None:
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
+            o8e = None
             if qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
                 q85 = qkv8.view(B, L, 3, heads, hd)
                 s8 = rt.fp8.meta.s(r[2])
+                # (lean: the epilogue also emits the e4m3 O of the output projection)
+                o8e = rt.fp8.o8_for(wo, (B, L, heads, hd), x.device) if lean else None
                 o, aux = K.attn_fwd_fp8(q85[:, :, 0], q85[:, :, 1], q85[:, :, 2], s8, s8, s8, kv_len,
-                                        scale, causal)
+                                        scale, causal, *(o8e or ()))
             else:
                 o, aux = K.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, scale, causal)
             s = None  # projection fused with the LayerNorm below
@@ -529,7 +534,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
             rt.attn_maps[site] = attention_probs(q5[:, :, 0], q5[:, :, 1], kv_len, causal, scale)
         ctx.f8a = None
         if lean:  # e4m3 output projection; keep the e4m3 operands for the backward
-            s, o8 = rt.fp8.out_proj(o.view(B * L, d), wo, bo)
+            s, o8 = rt.fp8.out_proj(o.view(B * L, d), wo, bo, o8e[0] if o8e else None)
             ctx.f8a = (kx[0], kx[1], o8)
             y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
         elif s is None:
@@ -704,6 +709,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
         ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * T, wq, wo, d)
         kx = [] if lean else None
         if x.is_cuda:
+            o8e = None
             f8 = (rt.fp8 is not None and rt.fp8.kv8 is not None and K.attn_fwd_fp8_ok(T, S, hd))
             r = rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx) if rt.fp8 is not None else None
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
@@ -716,8 +722,10 @@ class CrossAttnBlockFn(torch.autograd.Function):
                                        f"{tuple(kv_all.shape)}")
                 kv85 = kv8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
                 skv = rt.fp8.meta.s(kvs)
+                o8e = rt.fp8.o8_for(wo, (B, T, heads, hd), x.device) if lean else None
                 o, aux = K.attn_fwd_fp8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],
-                                        rt.fp8.meta.s(r[2]), skv, skv, kv_len, scale, False)
+                                        rt.fp8.meta.s(r[2]), skv, skv, kv_len, scale, False,
+                                        *(o8e or ()))
             else:
                 o, aux = K.attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len,
                                     scale, False)
@@ -731,7 +739,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             rt.attn_maps[site] = attention_probs(q.view(B, T, heads, hd), kv5[:, :, 0], kv_len, False, scale)
         ctx.f8a = None
         if lean:  # e4m3 output projection; keep the e4m3 operands for the backward
-            s, o8 = rt.fp8.out_proj(o.view(B * T, d), wo, bo)
+            s, o8 = rt.fp8.out_proj(o.view(B * T, d), wo, bo, o8e[0] if o8e else None)
             ctx.f8a = (kx[0], kx[1], o8)
             y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
         elif s is None:
@@ -867,7 +875,7 @@ class FFNBlockFn(torch.autograd.Function):
             if not f8w:
                 _wgrad(rt, ds2, h, d, w2)
             if bw is not None:
-                # fp8 backward: e5m2 gradients x e4m3 transposed weights on the
+                # fp8 backward: e5m2 gradients x e4m3 weights on the
                 # block-scaled MFMA; the ReLU-backward dgrad also emits the e5m2
                 # copy of its output for the next dgrad, which accumulates the
                 # residual gradient already in dh
@@ -875,8 +883,9 @@ class FFNBlockFn(torch.autograd.Function):
                 gs, gh = bw
                 M = B * L
                 ds8 = ds2 if f8w else fp8.quantize(ds2, st.gmeta, gs)
-                w2t8, s2t = st.weights.get(w2, transposed=True)
-                w1t8, s1t = st.weights.get(w1, transposed=True)
+                wp = fp8.DGRAD_PLAIN_W  # plain e4m3 weights read N-contiguous
+                w2t8, s2t = st.weights.get(w2, transposed=not wp)
+                w1t8, s1t = st.weights.get(w1, transposed=not wp)
                 if f8w:
                     # lean fp8 backward: the ReLU-backward dgrad writes only
                     # the e5m2 dpre8 and, from its epilogue, b1's gradient
@@ -887,7 +896,7 @@ class FFNBlockFn(torch.autograd.Function):
                     xs, hs = st.ffn_slots[id(w1)]
                     dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, None,
                                                relu_aux8=h8.view(M, ff), out8_slot=gh,
-                                               colsum_out=b1.grad, colsum_beta=bt)
+                                               colsum_out=b1.grad, colsum_beta=bt, w_plain=wp)
                     _ready(rt, b1)
                     q = rt.wgrad
                     q.add_fp8(ds8.view(M, d), st.gmeta.s(gs), h8.view(M, ff), st.meta.s(hs), w2, bt, rt)
@@ -895,9 +904,10 @@ class FFNBlockFn(torch.autograd.Function):
                 else:
                     dpre = torch.empty(M, ff, dtype=ds2.dtype, device=ds2.device)
                     dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, dpre, relu_aux=h,
-                                               out8_slot=gh)
+                                               out8_slot=gh, w_plain=wp)
                     _wgrad(rt, dpre, x2, ff, w1, b1)
-                fp8.gemm_bf8_dgrad(dpre8, st.gmeta, gh, w1t8, st.meta, s1t, dh.view(M, d), beta=1.0)
+                fp8.gemm_bf8_dgrad(dpre8, st.gmeta, gh, w1t8, st.meta, s1t, dh.view(M, d), beta=1.0,
+                                   w_plain=wp)
                 return (dh.view(B, L, d),) + (None,) * 8
             if w2.compute_t is not None:  # NT layout against W2^T (ParamStore.add_transposed)
                 dpre = K.linear_dgrad_t(ds2, w2.compute_t, relu_aux=h)

@@ -45,6 +45,10 @@ WGRAD_FP8 = True
 ATTN_PROJ_FP8 = True
 # tile config of the e5m2 x e4m3 backward GEMMs (0: 128x128 / 4 waves; 9: 256x256 at one wave per SIMD)
 BWD_CFG = 0
+# fp8 dgrads read the forward's e4m3 weight copy N-contiguous (transposing LDS
+# reads, 128x128 tiles) instead of a transposed copy: no fp8_quant_t pass
+# over every weight per step
+DGRAD_PLAIN_W = True
 _TUNED: Dict[tuple, int] = {}
 
 
@@ -147,33 +151,38 @@ def gemm_fp8(a8, b8, bias, meta: Fp8Meta, ia: int, ib: int, relu: bool = False,
     return y, y8
 
 
-def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8t, wmeta: Fp8Meta, iw: int,
+def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
                    out: Optional[torch.Tensor], relu_aux: Optional[torch.Tensor] = None,
                    beta: float = 0.0, out8_slot: Optional[int] = None, cfg: Optional[int] = None,
                    relu_aux8: Optional[torch.Tensor] = None, colsum_out: Optional[torch.Tensor] = None,
-                   colsum_beta: float = 0.0) -> Optional[torch.Tensor]:
+                   colsum_beta: float = 0.0, w_plain: bool = False) -> Optional[torch.Tensor]:
     """Backward GEMM on the block-scaled MFMA: out[M,N] (=|+= beta) dequant(
-    g8[M,K] (e5m2 gradient) @ w8t[N,K]^T (e4m3 transposed weight)), bf16;
-    relu_aux: zero where relu_aux <= 0 (ReLU backward), or relu_aux8: zero
-    where the e4m3 ReLU output is 0; out8_slot: also the e5m2 copy of out in
-    gmeta's slot (returned, amax recorded); colsum_out[N] (=|+= colsum_beta):
-    the column sums of the (bf16-rounded) output -- a bias gradient -- from
-    the epilogue (128x128 tiles). out may be None (nothing but the e5m2 copy
-    and the sums is written)."""
+    g8[M,K] (e5m2 gradient) @ W), bf16, where W[K,N] is the e4m3 weight:
+    w_plain: w8 IS that weight ([out=K][in=N], the forward's copy; the kernel
+    reads it N-contiguous through the transposing LDS path, 128x128 tiles),
+    else w8 is its transposed copy [N,K]. relu_aux: zero where relu_aux <= 0
+    (ReLU backward), or relu_aux8: zero where the e4m3 ReLU output is 0;
+    out8_slot: also the e5m2 copy of out in gmeta's slot (returned, amax
+    recorded); colsum_out[N] (=|+= colsum_beta): the column sums of the
+    (bf16-rounded) output -- a bias gradient -- from the epilogue (128x128
+    tiles). out may be None (nothing but the e5m2 copy and the sums is
+    written)."""
     M, Kd = g8.shape
-    N = w8t.shape[0]
+    N = w8.shape[1] if w_plain else w8.shape[0]
     o8 = torch.empty(M, N, dtype=BF8, device=g8.device) if out8_slot is not None else None
     aux = relu_aux if relu_aux is not None else relu_aux8
     c = BWD_CFG if cfg is None else cfg
     ws = None
-    if colsum_out is not None:
+    if colsum_out is not None or w_plain:
         c = 0
+    if colsum_out is not None:
         ws = K.workspace("fp8_colsum", math.ceil(M / 128) * 2 * N, g8.device)
-    C().gemm_fp8(g8, w8t, out, None, gmeta.s(ig), wmeta.s(iw), o8,
+    epi = (3 if aux is not None else 0) | (32 if w_plain else 0)
+    C().gemm_fp8(g8, w8, out, None, gmeta.s(ig), wmeta.s(iw), o8,
                  gmeta.s(out8_slot) if o8 is not None else None,
                  gmeta.a(out8_slot) if o8 is not None else None,
-                 M, N, Kd, g8.stride(0), w8t.stride(0), out.stride(0) if out is not None else N, N,
-                 3 if aux is not None else 0, c, 1, 1, relu_aux,
+                 M, N, Kd, g8.stride(0), w8.stride(0), out.stride(0) if out is not None else N, N,
+                 epi, c, 1, 1, relu_aux,
                  aux.stride(0) if aux is not None else 0, beta, aux8=relu_aux8,
                  colsum_out=colsum_out, colsum_beta=colsum_beta, ws=ws)
     return o8
@@ -343,8 +352,9 @@ class Fp8State:
             feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
             self.ln_slots[id(feeder.gamma)] = xs
             if backward:
-                self.weights.add(layer.ff1.w, transposed=True)
-                self.weights.add(layer.ff2.w, transposed=True)
+                if not DGRAD_PLAIN_W:
+                    self.weights.add(layer.ff1.w, transposed=True)
+                    self.weights.add(layer.ff2.w, transposed=True)
                 self.ffn_bwd_slots[id(layer.ff1.w)] = (self.gmeta.slot(f"gs:{id(layer)}"),
                                                        self.gmeta.slot(f"gh:{id(layer)}"))
 
@@ -370,19 +380,22 @@ class Fp8State:
         # of its output gradient ds)) and its dgrad / weight gradient on the
         # e5m2 ds the LayerNorm backward emits; the input projections' dgrad
         # and weight gradient run on the e5m2 copy of the attention backward's
-        # dQ|dK|dV (`proj_bwd`: weight -> e5m2 slot) against transposed e4m3
-        # weights and the forward's e4m3 input
+        # dQ|dK|dV (`proj_bwd`: weight -> e5m2 slot) against the e4m3 weights
+        # (DGRAD_PLAIN_W: the forward's copies, read N-contiguous) and the
+        # forward's e4m3 input
         self.attn_out: Dict[int, Tuple[int, int]] = {}
         self.proj_bwd: Dict[int, int] = {}
         if backward and ATTN_PROJ_FP8:
             outs = [l.o.w for l in enc] + [w for l in dec for w in (l.o1.w, l.o2.w)]
             for w in outs:
                 self.weights.add(w)
-                self.weights.add(w, transposed=True)
+                if not DGRAD_PLAIN_W:
+                    self.weights.add(w, transposed=True)
                 self.attn_out[id(w)] = (self.meta.slot("o:" + w.name), self.gmeta.slot("go:" + w.name))
             ins = [l.qkv.w for l in enc] + [w for l in dec for w in (l.qkv1.w, l.q2.w)] + [model.cross_kv.w]
             for w in ins:
-                self.weights.add(w, transposed=True)
+                if not DGRAD_PLAIN_W:
+                    self.weights.add(w, transposed=True)
                 self.proj_bwd[id(w)] = self.gmeta.slot("gp:" + w.name)
         self.weights.calibrate()
 
@@ -408,14 +421,27 @@ class Fp8State:
         y, y8 = gemm_fp8(x8, w8, b.master, self.meta, xs, ws, out8_slot=ys, c_deq=want8)
         return (y, y8, ys) if want8 else y
 
-    def out_proj(self, o2: torch.Tensor, w, b):
-        """Attention output projection in e4m3 (ATTN_PROJ_FP8): o2 quantised
-        once (its e4m3 copy also feeds the weight gradient). Returns (s, o8)
-        or None when w is not covered."""
+    def o8_for(self, w, shape, device):
+        """(o8, scale, amax) for the e4m3 attention forward to emit the e4m3
+        copy of its output straight into (the input of output projection w),
+        or None when w's projection is not e4m3."""
         sl = self.attn_out.get(id(w))
         if sl is None:
             return None
-        o8 = quantize(o2.contiguous(), self.meta, sl[0]).view(o2.shape)
+        return (torch.empty(shape, dtype=FP8, device=device), self.meta.s(sl[0]), self.meta.a(sl[0]))
+
+    def out_proj(self, o2: torch.Tensor, w, b, o8: Optional[torch.Tensor] = None):
+        """Attention output projection in e4m3 (ATTN_PROJ_FP8): o2 quantised
+        once (its e4m3 copy also feeds the weight gradient) unless the
+        attention forward already emitted it (o8, see o8_for). Returns
+        (s, o8) or None when w is not covered."""
+        sl = self.attn_out.get(id(w))
+        if sl is None:
+            return None
+        if o8 is None:
+            o8 = quantize(o2.contiguous(), self.meta, sl[0]).view(o2.shape)
+        else:
+            o8 = o8.view(o2.shape)
         w8, ws = self.weights.get(w)
         s, _ = gemm_fp8(o8, w8, b.master, self.meta, sl[0], ws)
         return s, o8

@@ -74,10 +74,13 @@ def test_quantize_matches_torch_e5m2():
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128), (600, 520, 1024)])
 @pytest.mark.parametrize("relu,beta", [(True, 0.0), (False, 1.0)])
-@pytest.mark.parametrize("cfg", [0, 9])
+@pytest.mark.parametrize("cfg", [0, 9, "plain"])
 def test_gemm_bf8_dgrad(M, N, K, relu, beta, cfg):
     """out (=|+= beta) dequant(g8 e5m2 @ w8t e4m3^T), ReLU-backward mask, and
-    the e5m2 copy of the output, against an fp32 reference."""
+    the e5m2 copy of the output, against an fp32 reference. "plain": the
+    weight given untransposed ([K][N], read N-contiguous by the kernel)."""
+    if cfg == "plain" and N % 16:
+        pytest.skip("the N-contiguous weight path needs N % 16 == 0")
     torch.manual_seed(1)
     wm, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
     iw, ig, io = wm.slot("w"), gm.slot("g"), gm.slot("o")
@@ -91,8 +94,12 @@ def test_gemm_bf8_dgrad(M, N, K, relu, beta, cfg):
     if relu:
         ref = ref * (aux.float() > 0)
     ref = ref + beta * out.float()
-    o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux=aux, beta=beta,
-                          out8_slot=io if relu else None, cfg=cfg)
+    if cfg == "plain":
+        o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8.t().contiguous(), wm, iw, out, relu_aux=aux, beta=beta,
+                              out8_slot=io if relu else None, w_plain=True)
+    else:
+        o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux=aux, beta=beta,
+                              out8_slot=io if relu else None, cfg=cfg)
     err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
     assert err < 1e-2, err
     if relu:
@@ -182,6 +189,17 @@ def test_attention_fwd_fp8(causal, Lq, Lk):
     # and close to the bf16 kernel on the unquantised inputs
     ob, _ = kk.attn_fwd(q, k, v, kv_len, scale, causal)
     assert (out.float() - ob.float()).abs().max().item() < 0.15 * ob.float().abs().max().item()
+    # the epilogue's e4m3 copy of O equals quantising the bf16 O; amax recorded
+    meta = F.Fp8Meta(DEV)
+    io = meta.slot("o")
+    meta.scale[io] = 64.0
+    o8 = torch.empty(out.shape, dtype=torch.float8_e4m3fn, device=DEV)
+    out2, _ = kk.attn_fwd_fp8(q8, k8, v8, sc[0], sc[1], sc[2], kv_len, scale, causal, o8, meta.s(io),
+                              meta.a(io))
+    assert torch.equal(out2, out)
+    want = (out.float() * 64.0).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(o8.view(torch.uint8), want.view(torch.uint8))
+    assert meta.amax_values()[io].item() == out.float().abs().max().item()
 
 
 def test_fp8_attention_training_tracks_bf16(monkeypatch):
@@ -360,11 +378,14 @@ def test_fp8_ffn_wgrad_matches_bf16_path(monkeypatch):
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (1024, 4096, 1024)])
 @pytest.mark.parametrize("with_c", [True, False])
-def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c):
+@pytest.mark.parametrize("plain", [False, True])
+def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c, plain):
     """The lean fp8 FFN backward's ReLU-backward dgrad: mask from the e4m3
     hidden (h8 != 0), optional bf16 output, e5m2 copy, and the bias gradient
     (column sums of the bf16-rounded output, accumulated with beta) from the
     epilogue partials."""
+    if plain and N % 16:
+        pytest.skip("the N-contiguous weight path needs N % 16 == 0")
     torch.manual_seed(4)
     wm, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
     iw, ig, io, ih = wm.slot("w"), gm.slot("g"), gm.slot("o"), wm.slot("h")
@@ -378,8 +399,8 @@ def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c):
     out = torch.empty(M, N, device=DEV).bfloat16() if with_c else None
     bsum = torch.randn(N, device=DEV)
     bref = bsum + ref.bfloat16().float().sum(0)
-    o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux8=h8, out8_slot=io,
-                          colsum_out=bsum, colsum_beta=1.0)
+    o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8.t().contiguous() if plain else w8, wm, iw, out,
+                          relu_aux8=h8, out8_slot=io, colsum_out=bsum, colsum_beta=1.0, w_plain=plain)
     # (the kernel quantises the bf16-rounded value; compare values: masked
     # elements are +0 from the kernel, -0 in ref * 0)
     o8ref = (ref.bfloat16().float() * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
