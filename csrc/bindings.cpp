@@ -322,10 +322,11 @@ void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Te
   check_err(tdg_attn_fwd_fp8(&a, 64, stream_of(q8)), "tdg attn_fwd_fp8");
 }
 
-void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
-              const Tensor& dout, const Tensor& lse, const Tensor& delta, const Tensor& dq,
-              const Tensor& dk, const Tensor& dv, const optional<Tensor>& kv_len, double scale,
-              bool causal) {
+static tdg::AttnArgs attn_bwd_args(const Tensor& q, const Tensor& k, const Tensor& v,
+                                   const Tensor& o, const Tensor& dout, const Tensor& lse,
+                                   const Tensor& delta, const Tensor& dq, const Tensor& dk,
+                                   const Tensor& dv, const optional<Tensor>& kv_len, double scale,
+                                   bool causal) {
   tdg::AttnArgs a{};
   fill_qkv(a, q, k, v);
   check_like(o, a, a.Lq, "o");
@@ -359,8 +360,68 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   }
   a.scale = (float)scale;
   a.causal = causal;
+  return a;
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+              const Tensor& dout, const Tensor& lse, const Tensor& delta, const Tensor& dq,
+              const Tensor& dk, const Tensor& dv, const optional<Tensor>& kv_len, double scale,
+              bool causal) {
+  tdg::AttnArgs a = attn_bwd_args(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal);
   c10::DeviceGuard g(q.device());
   check_err(tdg_attn_bwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_bwd");
+}
+
+// attn_bwd that also emits e5m2 copies of dQ (and of dK / dV when given),
+// their amax, and the bias-gradient column-sum partials (tdg_attn.h); the
+// hd-64 pipelined kernels (Lq or Lk > 128) only.
+void attn_bwd_g8(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                 const Tensor& dout, const Tensor& lse, const Tensor& delta, const Tensor& dq,
+                 const Tensor& dk, const Tensor& dv, const optional<Tensor>& kv_len, double scale,
+                 bool causal, const Tensor& dq8, const optional<Tensor>& dk8,
+                 const optional<Tensor>& dv8, const Tensor& sg8, const optional<Tensor>& amax8,
+                 const optional<Tensor>& cs_part, int64_t cs_np, int64_t cs_ld, int64_t cs_q,
+                 int64_t cs_k, int64_t cs_v, bool skip_bf16) {
+  tdg::AttnArgs a = attn_bwd_args(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal);
+  TORCH_CHECK(q.size(3) == 64 && (a.Lq > 128 || a.Lk > 128),
+              "attn_bwd_g8: the pipelined hd-64 kernels (Lq or Lk > 128) only");
+  TORCH_CHECK(dk8.has_value() == dv8.has_value(), "attn_bwd_g8: dk8 and dv8 together");
+  auto same = [](const Tensor& x8, const Tensor& x, const char* n) {
+    check_f8_fmt(x8, 1, n);
+    TORCH_CHECK(x8.sizes() == x.sizes() && x8.strides() == x.strides(), n,
+                " must have the bf16 gradient's shape and strides");
+  };
+  same(dq8, dq, "dq8");
+  a.dq8 = (uint8_t*)dq8.data_ptr();
+  if (dk8.has_value()) {
+    same(*dk8, dk, "dk8");
+    same(*dv8, dv, "dv8");
+    a.dk8 = (uint8_t*)dk8->data_ptr();
+    a.dv8 = (uint8_t*)dv8->data_ptr();
+  }
+  check_f32(sg8, "sg8");
+  a.sg8 = sg8.data_ptr<float>();
+  a.amaxg8 = amax_ptr(amax8);
+  TORCH_CHECK(a.amaxg8 != nullptr, "attn_bwd_g8: amax8 slot");
+  if (cs_part.has_value()) {
+    check_f32(*cs_part, "cs_part");
+    const int64_t nqb = (a.Lq + 127) / 128, nkb = (a.Lk + 127) / 128;
+    TORCH_CHECK(cs_np == nqb && (!dk8.has_value() || nkb == nqb),
+                "attn_bwd_g8: cs_np must equal the query (and key) 128-row block count");
+    TORCH_CHECK(cs_part->numel() >= (int64_t)a.B * cs_np * cs_ld &&
+                    cs_q + a.H * 64 <= cs_ld && (!dk8.has_value() || (cs_k + a.H * 64 <= cs_ld &&
+                                                                       cs_v + a.H * 64 <= cs_ld)),
+                "attn_bwd_g8: column-sum partial extent");
+    a.cs_part = cs_part->data_ptr<float>();
+    a.cs_np = (int)cs_np;
+    a.cs_ld = (int)cs_ld;
+    a.cs_q = (int)cs_q;
+    a.cs_k = (int)cs_k;
+    a.cs_v = (int)cs_v;
+  }
+  a.skip_bf16 = skip_bf16 ? 1 : 0;
+  c10::DeviceGuard g(q.device());
+  check_err(tdg_attn_bwd(&a, 64, stream_of(q)), "tdg attn_bwd_g8");
 }
 
 void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
@@ -1119,6 +1180,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_fwd_fp8", &attn_fwd_fp8);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd_g8", &attn_bwd_g8);
   m.def("attn_probs", &attn_probs);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

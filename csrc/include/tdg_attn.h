@@ -32,5 +32,19 @@ struct AttnArgs {
   uint8_t* out8;
   const float* so8;
   unsigned* amax8;
+  // optional e5m2 copies of dQ / dK / dV (attention backward, hd-64 pipelined
+  // kernels; same element strides as dq / dk / dv): x8 = e5m2(bf16(x) * sg8[0]),
+  // amax into the slot amaxg8, and the column sums of the bf16-rounded values
+  // (the fused projection's bias gradient) as partial rows
+  // cs_part[(b * cs_np + block) * cs_ld + cs_{q,k,v} + h * 64 + col].
+  // skip_bf16: the bf16 dq / dk / dv are not written (strides still used).
+  uint8_t* dq8;
+  uint8_t* dk8;
+  uint8_t* dv8;
+  const float* sg8;
+  unsigned* amaxg8;
+  float* cs_part;
+  int cs_np, cs_ld, cs_q, cs_k, cs_v;
+  int skip_bf16;
 };
 }  // namespace tdg

@@ -1004,6 +1004,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 // the tile's lse / delta (one 4-byte-per-lane DMA per wave: wave 0 lse, wave 1
 // delta, the others a scratch copy so every wave's DMA count is the same),
 // dQ streams K and V.
+// e5m2 copy of a 4-wave workgroup's gradient tile (the hd-64 pipelined
+// backward kernels): lane (g, cl) of wave w holds rows rows[u] (u < U),
+// columns 16 dt + 4 g .. +3 of one head. Writes the e5m2 values of the
+// bf16-rounded x * sc, records their |max| (one atomic per wave) and, when
+// part != null, the columns' sums over the workgroup's valid rows into
+// part[0..63] (shuffles over the 16 rows of a lane group, then the 4 waves
+// through `red`, 1 KiB of LDS). Every thread of the workgroup must call it.
+template <int U>
+__device__ __forceinline__ void attn_emit_g8(const f32x4 (&x)[U][4], float sc, const int (&rows)[U],
+                                             int nrows, uint8_t* base8, long long sl, float s8,
+                                             unsigned* amax, float* part, float* red, int lane,
+                                             int w) {
+  const int g = lane >> 4;
+  float cs[4][4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[dt][r] = 0.f;
+  float am = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool ok = rows[u] < nrows;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ok ? bf2f(f2bf(x[u][dt][r] * sc)) : 0.f;
+        cs[dt][r] += v[r];
+        am = fmaxf(am, fabsf(v[r]));
+      }
+      int w8 = pack2_e5m2c<false>(v[0] * s8, v[1] * s8, 0);
+      w8 = pack2_e5m2c<true>(v[2] * s8, v[3] * s8, w8);
+      if (ok) *reinterpret_cast<int*>(base8 + (long long)rows[u] * sl + 16 * dt + 4 * g) = w8;
+    }
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 64));
+  if (lane == 0) atomic_amax(amax_word(amax, blockIdx.x + 5 * blockIdx.y + 11 * blockIdx.z + w), am);
+  if (!part) return;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int sh = 1; sh < 16; sh <<= 1) cs[dt][r] += __shfl_xor(cs[dt][r], sh, 64);
+  __syncthreads();  // (the caller's LDS reads are done)
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w * 64 + 16 * dt + 4 * g + r] = cs[dt][r];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64)
+    part[threadIdx.x] = red[threadIdx.x] + red[64 + threadIdx.x] + red[128 + threadIdx.x] +
+                        red[192 + threadIdx.x];
+  __syncthreads();
+}
+
 template <int U, int NS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_pipe_kernel(AttnArgs a) {
   constexpr int HD = 64;
@@ -1175,6 +1235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
   }
   wait_vmcnt<0>();
+  if (!a.skip_bf16) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (key[u] >= a.Lk) continue;
@@ -1190,6 +1251,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
       *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
     }
+  }
+  }
+  if (a.dk8) {  // e5m2 dK / dV (+ amax, + bias-gradient partials)
+    const float s8 = a.sg8[0];
+    float* red = reinterpret_cast<float*>(smem);
+    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + blockIdx.x) * a.cs_ld + h * 64 : nullptr;
+    attn_emit_g8<U>(dk, a.scale, key, a.Lk, a.dk8 + b * a.dk_sb + h * a.dk_sh, a.dk_sl, s8, a.amaxg8,
+                    prow ? prow + a.cs_k : nullptr, red, lane, w);
+    attn_emit_g8<U>(dv, 1.f, key, a.Lk, a.dv8 + b * a.dv_sb + h * a.dv_sh, a.dv_sl, s8, a.amaxg8,
+                    prow ? prow + a.cs_v : nullptr, red, lane, w);
   }
 }
 
@@ -1354,6 +1425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
   }
   wait_vmcnt<0>();
+  if (!a.skip_bf16) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (qrow[u] >= a.Lq) continue;
@@ -1365,6 +1437,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
       *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
     }
+  }
+  }
+  if (a.dq8) {  // e5m2 dQ (+ amax, + bias-gradient partials)
+    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + blockIdx.x) * a.cs_ld + h * 64 + a.cs_q
+                            : nullptr;
+    attn_emit_g8<U>(dq, a.scale, qrow, a.Lq, a.dq8 + b * a.dq_sb + h * a.dq_sh, a.dq_sl, a.sg8[0],
+                    a.amaxg8, prow, reinterpret_cast<float*>(smem), lane, w);
   }
 }
 

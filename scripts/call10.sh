@@ -2,7 +2,7 @@ set -uo pipefail
 O=gpurun_out/c10; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 export TDG_NO_AUTOBUILD=1
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fp8.py tests/test_gpu_graph.py tests/test_gpu_dp.py > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fp8.py tests/test_gpu_graph.py tests/test_gpu_dp.py tests/test_gpu_kernels.py > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log
 [ $rc -eq 0 ] || { grep -B5 -A30 "Error\|assert" $O/pytest.log | head -80; exit $rc; }
 for i in 1 2; do

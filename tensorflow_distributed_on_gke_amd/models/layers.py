@@ -343,6 +343,14 @@ def _fp8_grad_bias(g: torch.Tensor, g_slot: int, b: Param, rt: RunCtx, key: str)
     return g8
 
 
+def _fold_bias_later(rt: RunCtx, part: torch.Tensor, nparts: int, N: int, b: Param) -> None:
+    """b's gradient = column sums of the [nparts, N] partials, folded with the
+    queue's other deferred column reductions at the next flush."""
+    q = rt.wgrad
+    q.reductions.append((part, b.grad, nparts, N, _beta(rt)))
+    q.reduced_params.append((rt, b))
+
+
 def _fp8_dgrad_into(g8, g_slot: int, w: Param, out: torch.Tensor, rt: RunCtx, beta: float) -> None:
     """out (=|+= beta) dequant(g8 (e5m2) @ w) against w's e4m3 copy (read
     N-contiguous by the kernel, fp8.DGRAD_PLAIN_W; else its transposed copy)."""
@@ -603,10 +611,22 @@ class SelfAttnBlockFn(torch.autograd.Function):
         q5 = qkv.view(B, L, 3, heads, hd)
         dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
         g5 = dqkv.view(B, L, 3, heads, hd)
-        K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
-                   g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
         gq = st.proj_bwd[id(wqkv)]
-        dqkv8 = _fp8_grad_bias(dqkv, gq, bqkv, rt, f"qkv{site}")
+        if fp8.ATTN_BWD_G8 and K.attn_bwd_g8_ok(L, L, hd):
+            # the attention backward emits e5m2 dQ|dK|dV, their amax and the
+            # bias-gradient partials itself (no bf16 dQ|dK|dV pass)
+            dqkv8 = torch.empty(M, 3 * d, dtype=st.gmeta.dtype, device=dy.device)
+            g85 = dqkv8.view(B, L, 3, heads, hd)
+            part = K.workspace(f"qcs_qkv{site}", B * -(-L // 128) * 3 * d, dy.device)
+            nparts = K.attn_bwd_g8(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd),
+                                   aux, g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal,
+                                   g85[:, :, 0], g85[:, :, 1], g85[:, :, 2], st.gmeta.s(gq),
+                                   st.gmeta.a(gq), part, 3 * d, 0, d, 2 * d)
+            _fold_bias_later(rt, part[: nparts * 3 * d], nparts, 3 * d, bqkv)
+        else:
+            K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
+                       g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
+            dqkv8 = _fp8_grad_bias(dqkv, gq, bqkv, rt, f"qkv{site}")
         _fp8_dgrad_into(dqkv8, gq, wqkv, dh.view(M, d), rt, 1.0)
         q = rt.wgrad
         q.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
@@ -773,11 +793,24 @@ class CrossAttnBlockFn(torch.autograd.Function):
             do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
             _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
             dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
-            K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
-                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
-                       g5[:, :, 1], kv_len, scale, False)
             gq = st.proj_bwd[id(wq)]
-            dq8 = _fp8_grad_bias(dq, gq, bq, rt, f"q{site}")
+            if fp8.ATTN_BWD_G8 and K.attn_bwd_g8_ok(T, S, hd):
+                # e5m2 dQ (+ amax, bias partials) from the attention backward;
+                # dK / dV stay bf16 (summed over the layers into the batched
+                # cross K|V gradient)
+                dq8 = torch.empty(M, d, dtype=st.gmeta.dtype, device=dy.device)
+                part = K.workspace(f"qcs_q{site}", B * -(-T // 128) * d, dy.device)
+                nparts = K.attn_bwd_g8(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
+                                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd),
+                                       g5[:, :, 0], g5[:, :, 1], kv_len, scale, False,
+                                       dq8.view(B, T, heads, hd), None, None, st.gmeta.s(gq),
+                                       st.gmeta.a(gq), part, d, 0, 0, 0, skip_bf16=False)
+                _fold_bias_later(rt, part[: nparts * d], nparts, d, bq)
+            else:
+                K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
+                           do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
+                           g5[:, :, 1], kv_len, scale, False)
+                dq8 = _fp8_grad_bias(dq, gq, bq, rt, f"q{site}")
             _fp8_dgrad_into(dq8, gq, wq, dh.view(M, d), rt, 1.0)
             rt.wgrad.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
             rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)

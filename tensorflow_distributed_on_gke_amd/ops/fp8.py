@@ -49,6 +49,10 @@ BWD_CFG = 0
 # reads, 128x128 tiles) instead of a transposed copy: no fp8_quant_t pass
 # over every weight per step
 DGRAD_PLAIN_W = True
+# the attention backward emits the e5m2 dQ|dK|dV (and the projection bias
+# gradient partials) of the fp8 projection backward itself, instead of a
+# quantise + column-sum pass over the bf16 gradient (long sequences)
+ATTN_BWD_G8 = True
 _TUNED: Dict[tuple, int] = {}
 
 

@@ -379,6 +379,28 @@ def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bo
     C().attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal)
 
 
+def attn_bwd_g8_ok(Lq: int, Lk: int, hd: int) -> bool:
+    """Shapes whose attention backward can emit e5m2 gradients (the hd-64
+    pipelined kernels, attention.hip attn_emit_g8)."""
+    return hd == 64 and (Lq > 128 or Lk > 128)
+
+
+def attn_bwd_g8(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bool, dq8,
+                dk8, dv8, sg8, amax8, cs_part, cs_ld: int, cs_q: int, cs_k: int, cs_v: int,
+                skip_bf16: bool = True) -> int:
+    """attn_bwd that also writes e5m2 copies dq8 (dk8 / dv8 optional, same
+    layout as dq / dk / dv) = e5m2(bf16(grad) * sg8), their amax into the
+    slot amax8, and the bias-gradient column-sum partials cs_part[B *
+    nblocks, cs_ld] (columns cs_q / cs_k / cs_v + head * 64 + j). skip_bf16:
+    the bf16 dq / dk / dv are not written. Returns the partial row count."""
+    B, Lq = q.shape[0], q.shape[1]
+    np_ = -(-Lq // 128)
+    delta = workspace("attn_delta", lse.numel(), q.device)[: lse.numel()]
+    C().attn_bwd_g8(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal, dq8, dk8, dv8,
+                    sg8, amax8, cs_part, np_, cs_ld, cs_q, cs_k, cs_v, skip_bf16)
+    return B * np_
+
+
 def attn_probs(q, k, kv_len, scale: float, causal: bool) -> torch.Tensor:
     B, Lq, H, hd = q.shape
     Lk = k.shape[1]

@@ -525,3 +525,51 @@ def test_quant_colsum():
     ref = x.float().sum(0)
     assert torch.allclose(cs, ref, rtol=1e-4, atol=1e-4)
     assert gm.amax_values()[i].item() == x.float().abs().max().item()
+
+
+@pytest.mark.parametrize("causal,L,S,kv", [(True, 512, 512, True), (False, 300, 300, True),
+                                            (False, 384, 200, False)])
+def test_attn_bwd_emits_e5m2_grads(causal, L, S, kv):
+    """The pipelined attention backward's e5m2 dQ (and dK / dV) equal
+    quantising its bf16 gradients, amax recorded, bias-gradient partials sum
+    to the column sums; skip_bf16 leaves the bf16 gradients untouched."""
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+    torch.manual_seed(11)
+    B, H, hd = 2, 3, 64
+    q = torch.randn(B, L, H, hd, device=DEV).bfloat16()
+    k, v = (torch.randn(B, S, H, hd, device=DEV).bfloat16() for _ in range(2))
+    kv_len = torch.tensor([S, max(1, S - 37)], dtype=torch.int32, device=DEV)
+    scale = hd ** -0.5
+    o, lse = kk.attn_fwd(q, k, v, kv_len, scale, causal)
+    do = torch.randn(B, L, H, hd, device=DEV).bfloat16()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv_len, scale, causal)
+    gm = F.Fp8Meta(DEV, fmt=1)
+    i = gm.slot("g")
+    gm.scale[i] = 2.0 ** 12
+    d = H * hd
+    ncol = 3 * d if kv else d
+    dq2 = torch.full_like(q, 7.0)
+    dk2, dv2 = torch.full_like(k, 7.0), torch.full_like(v, 7.0)
+    dq8 = torch.empty(q.shape, dtype=torch.float8_e5m2, device=DEV)
+    dk8 = torch.empty(k.shape, dtype=torch.float8_e5m2, device=DEV) if kv else None
+    dv8 = torch.empty(v.shape, dtype=torch.float8_e5m2, device=DEV) if kv else None
+    part = torch.full((B * -(-L // 128) * ncol,), float("nan"), device=DEV)
+    np_ = kk.attn_bwd_g8(q, k, v, o, do, lse, dq2, dk2, dv2, kv_len, scale, causal, dq8, dk8, dv8,
+                         gm.s(i), gm.a(i), part, ncol, 0, d, 2 * d, skip_bf16=True)
+    assert bool((dq2 == 7.0).all()) and bool((dk2 == 7.0).all())  # bf16 outputs skipped
+
+    def e5(x):
+        return (x.float() * 2.0 ** 12).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+
+    assert torch.equal(dq8.view(torch.uint8), e5(dq))
+    cs = part[: np_ * ncol].view(np_, ncol).sum(0)
+    assert torch.allclose(cs[:d], dq.float().sum((0, 1)).reshape(d), rtol=1e-3, atol=1e-3)
+    am = dq.float().abs().max()
+    if kv:
+        assert torch.equal(dk8.view(torch.uint8), e5(dk))
+        assert torch.equal(dv8.view(torch.uint8), e5(dv))
+        assert torch.allclose(cs[d:2 * d], dk.float().sum((0, 1)).reshape(d), rtol=1e-3, atol=1e-3)
+        assert torch.allclose(cs[2 * d:], dv.float().sum((0, 1)).reshape(d), rtol=1e-3, atol=1e-3)
+        am = torch.maximum(am, torch.maximum(dk.float().abs().max(), dv.float().abs().max()))
+    assert gm.amax_values()[i].item() == am.item()

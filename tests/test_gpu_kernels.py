@@ -578,6 +578,26 @@ def test_dgrad_tile_configs(cfg):
     _close(out, ref, 1e-2, f"cfg{cfg} dgrad beta=1")
 
 
+@pytest.mark.parametrize("cfg", [20, 21, 22])
+@pytest.mark.parametrize("K", [32, 64, 96])
+def test_pipe_configs_short_k(cfg, K):
+    """The LDS-DMA ring configs (gemm_pipe.h) with fewer K tiles than ring
+    slots -- the one-K-tile case that faulted in the removed producer /
+    consumer kernel sharing this prologue (docs/KERNELS.md): forward and
+    beta = 1 dgrad vs fp32."""
+    M, N = 520, 776
+    x = _bf(_rand(M, K, seed=91)).to(DEV)
+    w = _bf(_rand(N, K, scale=1.0 / math.sqrt(K), seed=92)).to(DEV)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    kk.gemm(x, w, out, M, N, K, K, K, N, True, True, kk.EPI_NONE, cfg=(cfg, 1))
+    _close(out, x.float() @ w.float().t(), 1e-2, f"cfg{cfg} K={K} forward")
+    wd = _bf(_rand(K, N, scale=1.0 / math.sqrt(K), seed=93)).to(DEV)
+    c0 = _bf(_rand(M, N, seed=94)).to(DEV)
+    out = c0.clone()
+    kk.gemm(x, wd, out, M, N, K, K, N, N, True, False, kk.EPI_NONE, beta=1.0, cfg=(cfg, 1))
+    _close(out, x.float() @ wd.float() + c0.float(), 1e-2, f"cfg{cfg} K={K} dgrad")
+
+
 def test_no_library_gemm_in_training_step():
     """The training step runs only in-tree kernels: no hipBLASLt / rocBLAS
     (Cijk_* / rocblas_*) kernel in a profiled eager step of the base model,
