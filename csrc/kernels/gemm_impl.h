@@ -824,7 +824,10 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
 #undef TDG_PIPE
       if (ok) return;
     }
-    tile_cfg = 0;
+    // not applicable (K % 32, split-K, grouped): the deep-pipelined 8-wave
+    // 128x128 tile, which takes K tails -- cfg 0 ran the big vocab dgrad (K =
+    // 7010) at 0.6 PF/s
+    tile_cfg = 13;
   }
   if (tile_cfg == 12) {
     // 256x256 tiles (K % 64 == 0, no split-K; MN-contiguous operands need
@@ -839,7 +842,7 @@ void launch_tiles(int tile_cfg, const bf16_t* A, const bf16_t* B, void* C, const
       if (launch_256<AK, BKc, EPI, F32>(args, tiles, bias, aux, K, ldaux, alpha, beta, st) == 0)
         return;
     }
-    tile_cfg = 0;
+    tile_cfg = 13;
   }
 #define TDG_CFG(ID, BM_, BN_, WM_, WN_, ST_)                                                  \
   case ID:                                                                                    \

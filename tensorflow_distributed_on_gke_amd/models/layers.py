@@ -150,6 +150,7 @@ class WgradQueue:
         self.reductions = []
         self.reduced_params = []
         self.fp8_items = []
+        self.small_per_shape = False
 
     def boundary(self) -> None:
         if self.flush_at_boundary and not self._chunking() and (self.items or self.reductions or self.fp8_items):
@@ -215,7 +216,12 @@ class WgradQueue:
     def flush(self) -> None:
         self._flush_fp8()
         if self.items:
-            if RAGGED_WGRAD and all(self._ragged_ok(it) for it in self.items):
+            # (small_per_shape: a flush of under half a wave of 256x256 tiles
+            # -- the fp8 step's lone bf16 vocab projection -- runs per shape
+            # on 128x128 tiles)
+            if RAGGED_WGRAD and all(self._ragged_ok(it) for it in self.items) and (
+                    not self.small_per_shape or self._cursor
+                    or sum(self._tiles(it) for it in self.items) >= K.NUM_CU // 2):
                 self._launch_prefix(sum(self._tiles(it) for it in self.items) - self._cursor)
             else:  # (never partially launched: chunking needs the ragged path)
                 self._flush_grouped()

@@ -87,6 +87,9 @@ class TrainStep:
                                        wave_tiles=(WAVE_TILES or K.NUM_CU) if dp and CHUNKED_WGRAD else 0)
             # every encoder and decoder layer's backward ends with a layer_end()
             self.rt.wgrad.layers_per_step = 2 * model.cfg.layers
+            # fp8: the bf16 weight gradients left (the vocab projection) are
+            # too few tiles for the ragged 256x256 launch
+            self.rt.wgrad.small_per_shape = fp8_state is not None and not self.rt.wgrad._chunking()
         self.fp8 = fp8_state
         if dev.type == "cuda" and not self.rt.accumulate and ZERO_GRAD_FREE:
             opt.zero_grad = False  # every GPU gradient writer overwrites
