@@ -360,9 +360,9 @@ struct F8Epi {
         if (n + 8 <= N) {
           *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
         } else {
-          const uint8_t* b8 = reinterpret_cast<const uint8_t*>(&lo);
-          const uint8_t* c8 = reinterpret_cast<const uint8_t*>(&hi);
-          for (int e = 0; e < 8 && n + e < N; ++e) C8[(size_t)m * ldc8 + n + e] = e < 4 ? b8[e] : c8[e - 4];
+          // (bytes by shifts: taking &lo / &hi put them in scratch memory)
+          for (int e = 0; e < 8 && n + e < N; ++e)
+            C8[(size_t)m * ldc8 + n + e] = (uint8_t)((uint32_t)(e < 4 ? lo : hi) >> (8 * (e & 3)));
         }
       }
     }

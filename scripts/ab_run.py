@@ -10,6 +10,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("TDG_PKG_ROOT"):  # another copy of the package (and its built _C)
+    sys.path.insert(0, os.path.abspath(os.environ["TDG_PKG_ROOT"]))
+import tensorflow_distributed_on_gke_amd  # noqa: E402,F401  (cached: bench.py gets this copy)
+print(f"[ab_run] package {os.path.dirname(tensorflow_distributed_on_gke_amd.__file__)}", file=sys.stderr)
 i = sys.argv.index("--")
 for a in sys.argv[1:i]:
     name, val = a.split("=", 1)
