@@ -1085,6 +1085,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   bool causal;
   key_window(a, b, klim, scl, causal);
   const float c = scl * LOG2E;
+  const int kmaxw = k0 + 16 * U * (w + 1) - 1;  // the wave's last key
 
   f32x4 dk[U][T::DT], dv[U][T::DT];
 #pragma unroll
@@ -1185,15 +1186,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
             dpv[u] = mfma16(ofr[cb][ks], vf[u][ks], dpv[u]);
           }
         }
+        // the whole 16-query subtile valid for every key of the wave (a
+        // wave-uniform test): no per-element masking
+        const int qs0 = q0 + 16 * t;
+        const bool full = kmaxw < klim && qs0 + 15 < a.Lq && (!causal || kmaxw <= qs0);
+        if (full) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = q0 + 16 * t + 4 * g + r;
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
-            p[u][tt][r] = pv;
-            ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
+            for (int u = 0; u < U; ++u) {
+              const float pv = fast_exp2(sv[u][r] * c - l4[cb][r]);
+              p[u][tt][r] = pv;
+              ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
+            }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = qs0 + 4 * g + r;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
+              const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
+              p[u][tt][r] = pv;
+              ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
+            }
           }
         }
       }
@@ -1280,6 +1296,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   int qrow[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
+  const int qminw = q0 + 16 * U * w;  // the wave's first query
   int klim;
   float scl;
   bool causal;
@@ -1390,14 +1407,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
             dpv[u] = mfma16(vfr[cb][ks], of[u][ks], dpv[u]);
           }
         }
+        // the whole 16-key subtile valid for every query of the wave (a
+        // wave-uniform test): no per-element masking
+        const int ks0 = k0 + 16 * t;
+        const bool full = qminw + 16 * U <= a.Lq && ks0 + 15 < klim && (!causal || ks0 + 15 <= qminw);
+        if (full) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * t + 4 * g + r;
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
-            ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
+            for (int u = 0; u < U; ++u)
+              ds[u][tt][r] = fast_exp2(sv[u][r] * c - L[u]) * (dpv[u][r] - D[u]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = ks0 + 4 * g + r;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
+              const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+              ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
+            }
           }
         }
       }

@@ -6,6 +6,8 @@ us per call and PF/s (causal counts the unmasked half)."""
 import os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("TDG_PKG_ROOT"):  # A/B against another built copy of the package
+    sys.path.insert(0, os.path.abspath(os.environ["TDG_PKG_ROOT"]))
 from tensorflow_distributed_on_gke_amd.ops import kernels as kk
 
 def graph_time(fn, n=20):
