@@ -1613,16 +1613,28 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
       // lse / delta of queries 16t + 4g .. +3: one 16-byte LDS read each
       const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 16 * t + 4 * g);
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 16 * t + 4 * g);
+      // every (query, key) of this 16-query tile valid for the wave's keys
+      // (wave-uniform): no per-element masks
+      const int kmaxw = 16 * U * (__builtin_amdgcn_readfirstlane(w) + 1) - 1;
+      const bool full = live && kmaxw < klim && 16 * t + 15 < a.Lq && (!causal || kmaxw <= 16 * t);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         float pv[4], dv4[4];
         const bool kvalid = key[u] < klim;
+        if (full) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = 16 * t + 4 * g + r;
-          const bool ok = live && kvalid && q < a.Lq && (!causal || key[u] <= q);
-          pv[r] = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
-          dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
+          for (int r = 0; r < 4; ++r) {
+            pv[r] = fast_exp2(sv[u][r] * c - l4[r]);
+            dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = 16 * t + 4 * g + r;
+            const bool ok = live && kvalid && q < a.Lq && (!causal || key[u] <= q);
+            pv[r] = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
+            dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
+          }
         }
         pk[u][t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
         pk[u][t][1] = (uint32_t)f2bf(pv[2]) | ((uint32_t)f2bf(pv[3]) << 16);
