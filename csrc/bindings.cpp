@@ -85,6 +85,11 @@ int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, long long n, 
              float beta1, float beta2, float eps, float lr_const, float d_model, float warmup,
              float grad_scale, float weight_decay, int sched, int zero_grad, int inc_step,
              hipStream_t st);
+int tdg_adam_chunks(float* p, float* g, float* m, float* v, void* shadow, long long n,
+                    const void* chunks, int nchunks, long long* step, float beta1, float beta2,
+                    float eps, float lr_const, float d_model, float warmup, float grad_scale,
+                    float weight_decay, int sched, int zero_grad, int inc_step,
+                    const float* scale8, unsigned* amax8, hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
@@ -1117,6 +1122,38 @@ void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
             "tdg adam");
 }
 
+// Adam over the chunk table [nchunks, 4] int64 (start, n, fp8 slot or -1,
+// e4m3 address or 0) built by ops/fp8.py Fp8Weights.adam_chunks: the weights
+// with e4m3 copies get them refreshed in the same pass.
+void adam_chunks(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
+                 const Tensor& shadow, const Tensor& chunks, const Tensor& step, double beta1,
+                 double beta2, double eps, double lr_const, double d_model, double warmup,
+                 double grad_scale, double weight_decay, int64_t sched, bool zero_grad,
+                 bool inc_step, const Tensor& scale8, const Tensor& amax8) {
+  for (auto* t : {&p, &g, &m, &v}) {
+    check_f32(*t, "adam buffers");
+    check_contig(*t, "adam buffers");
+    TORCH_CHECK(t->numel() == p.numel(), "adam: buffer sizes differ");
+  }
+  check_bf16(shadow, "shadow");
+  TORCH_CHECK(shadow.numel() == p.numel() && p.numel() % 4 == 0 && p.numel() < (1LL << 28),
+              "adam_chunks: shadow size / flat size");
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.dim() == 2 &&
+                  chunks.size(1) == 4 && chunks.is_contiguous(),
+              "adam_chunks: chunk table [n, 4] int64 on the GPU");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.is_cuda(), "adam: step int64 GPU");
+  check_f32(scale8, "scale8");
+  c10::DeviceGuard gd(p.device());
+  check_err(tdg_adam_chunks(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                            v.data_ptr<float>(), shadow.data_ptr(), p.numel(), chunks.data_ptr(),
+                            (int)chunks.size(0), reinterpret_cast<long long*>(step.data_ptr<int64_t>()),
+                            (float)beta1, (float)beta2, (float)eps, (float)lr_const, (float)d_model,
+                            (float)warmup, (float)grad_scale, (float)weight_decay, (int)sched,
+                            zero_grad, inc_step, scale8.data_ptr<float>(),
+                            reinterpret_cast<unsigned*>(amax8.data_ptr()), stream_of(p)),
+            "tdg adam_chunks");
+}
+
 // dsts[g] [C, R] = srcs[g] [R, C]^T (bf16, same shape, <= 64 matrices, one launch)
 void transpose_grouped(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
   const size_t G = srcs.size();
@@ -1193,6 +1230,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent", &xent);
   m.def("xent_stats", &xent_stats);
   m.def("adam", &adam);
+  m.def("adam_chunks", &adam_chunks);
   m.def("reduce_partials_multi", &reduce_partials_multi);
   m.def("to_bf16", &to_bf16);
   m.attr("ARCH") = "gfx950";

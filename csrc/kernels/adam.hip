@@ -113,6 +113,79 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   }
 }
 
+// Adam over a table of chunks (<= 4096 parameters each, none crossing a
+// parameter that has an e4m3 copy): a chunk inside such a weight also writes
+// y8 = e4m3(bf16(p_new) * scale8[slot]) -- the refreshed e4m3 copy the next
+// forward reads -- and folds its |bf16(p_new)| max into the slot's amax
+// (one atomic per chunk). Replaces the separate re-quantisation pass over
+// the bf16 shadow (fp8_quant_multi) after the optimizer step.
+struct AdamChunk {
+  long long start;  // first parameter (multiple of 4)
+  long long n;      // parameter count (multiple of 4, <= 4096)
+  long long slot;   // fp8 scale / amax slot, or -1
+  long long y8;     // address of the e4m3 byte of parameter `start`, or 0
+};
+constexpr int ADAM_CHUNK = 4096, ADAM_PER_THREAD = ADAM_CHUNK / 4 / 256;
+
+__global__ __launch_bounds__(256) void adam_chunk_kernel(
+    float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    bf16_t* __restrict__ shadow, long long n, const AdamChunk* __restrict__ chunks,
+    const long long* __restrict__ step_ptr, AdamCfg c, const float* __restrict__ scale8,
+    unsigned* __restrict__ amax8) {
+  const AdamChunk ch = chunks[blockIdx.x];
+  const float step = (float)step_ptr[0];
+  const float t = step + 1.f;
+  const float lr = noam_lr(c, step);
+  const float lr_t = lr * sqrtf(1.f - powf(c.beta2, t)) / (1.f - powf(c.beta1, t));
+  const float ob1 = 1.f - c.beta1, ob2 = 1.f - c.beta2;
+  float4* P4 = reinterpret_cast<float4*>(p);
+  float4* G4 = reinterpret_cast<float4*>(g);
+  float4* M4 = reinterpret_cast<float4*>(m);
+  float4* V4 = reinterpret_cast<float4*>(v);
+  uint2* S2 = shadow ? reinterpret_cast<uint2*>(shadow) : nullptr;
+  const AdamOut o(p, m, v, shadow, n);
+  const long long i0 = ch.start / 4, n4 = ch.n / 4;
+  float4 pa[ADAM_PER_THREAD], ga[ADAM_PER_THREAD], ma[ADAM_PER_THREAD], va[ADAM_PER_THREAD];
+#pragma unroll
+  for (int k = 0; k < ADAM_PER_THREAD; ++k) {
+    const long long j = threadIdx.x + 256 * k;
+    if (j < n4) {
+      pa[k] = P4[i0 + j];
+      ga[k] = G4[i0 + j];
+      ma[k] = M4[i0 + j];
+      va[k] = V4[i0 + j];
+    }
+  }
+  uint8_t* y8 = reinterpret_cast<uint8_t*>(ch.y8);
+  const float s8 = y8 ? scale8[ch.slot] : 0.f;
+  float am = 0.f;
+#pragma unroll
+  for (int k = 0; k < ADAM_PER_THREAD; ++k) {
+    const long long j = threadIdx.x + 256 * k;
+    if (j >= n4) continue;
+    adam4(pa[k], ga[k], ma[k], va[k], c, lr, lr_t, ob1, ob2);
+    adam_store(o, P4, G4, M4, V4, S2, i0 + j, pa[k], ma[k], va[k], c.zero_grad);
+    if (y8) {
+      const float f0 = bf2f(f2bf(pa[k].x)), f1 = bf2f(f2bf(pa[k].y));
+      const float f2 = bf2f(f2bf(pa[k].z)), f3 = bf2f(f2bf(pa[k].w));
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
+      int w8 = pack2_e4m3<false>(f0 * s8, f1 * s8, 0);
+      w8 = pack2_e4m3<true>(f2 * s8, f3 * s8, w8);
+      *reinterpret_cast<int*>(y8 + 4 * j) = w8;
+    }
+  }
+  if (y8) {
+    __shared__ float red[4];
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomic_amax(amax_word(amax8 + ch.slot * AMAX_WORDS, blockIdx.x),
+                  fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
 __global__ void step_inc_kernel(long long* step) { step[0] += 1; }
 
 // p_bf16 = bf16(p_f32) for the whole flat buffer (init / checkpoint load).
@@ -205,6 +278,24 @@ extern "C" int tdg_adam(float* p, float* g, float* m, float* v, void* shadow, lo
                        m + o, v + o, shadow ? (bf16_t*)shadow + o : nullptr, cn, step, c);
   }
   // per-bucket updates (data parallel) share one step: only the last advances it
+  if (inc_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
+  return 0;
+}
+
+// The whole flat buffer through a chunk table built by the host (ops/fp8.py
+// Fp8Weights.adam_chunks); n < 2^28 (the write-through descriptors' 31-bit
+// offsets).
+extern "C" int tdg_adam_chunks(float* p, float* g, float* m, float* v, void* shadow, long long n,
+                               const void* chunks, int nchunks, long long* step, float beta1,
+                               float beta2, float eps, float lr_const, float d_model, float warmup,
+                               float grad_scale, float weight_decay, int sched, int zero_grad,
+                               int inc_step, const float* scale8, unsigned* amax8,
+                               hipStream_t st) {
+  if (n % 4 != 0 || n >= (1LL << 28) || nchunks <= 0) return -1;
+  AdamCfg c{beta1, beta2, eps, lr_const, d_model, warmup, grad_scale, weight_decay, sched,
+            zero_grad};
+  hipLaunchKernelGGL(adam_chunk_kernel, dim3(nchunks), dim3(256), 0, st, p, g, m, v,
+                     (bf16_t*)shadow, n, (const AdamChunk*)chunks, step, c, scale8, amax8);
   if (inc_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   return 0;
 }

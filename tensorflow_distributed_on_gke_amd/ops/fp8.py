@@ -304,6 +304,37 @@ class Fp8Weights:
                 C().fp8_quant_t([p.compute for p, _, _, _ in chunk], [w8 for _, w8, _, _ in chunk],
                                 [slot for _, _, slot, _ in chunk], self.meta.scale, self.meta.amax)
 
+    def adam_chunks(self, store) -> Optional[torch.Tensor]:
+        """Chunk table of the flat parameter buffer for the Adam kernel that
+        also refreshes these e4m3 copies (adam_chunk_kernel): int64 [n, 4]
+        rows (start, count <= 4096, slot or -1, e4m3 address or 0); chunks
+        never cross into or out of a weight with an e4m3 copy. None when some
+        copy is transposed or the buffer exceeds the kernel's 2^28 limit."""
+        if getattr(self, "_chunks", None) is not None:
+            return self._chunks
+        if any(it[3] for it in self.items) or store.total >= (1 << 28):
+            return None
+        CH = 4096
+        segs = sorted(((p.offset, p.numel, w8, slot) for p, w8, slot, _ in self.items),
+                      key=lambda t: t[0])
+        rows, pos = [], 0
+
+        def plain(a, b):
+            for c0 in range(a, b, CH):
+                rows.append((c0, min(CH, b - c0), -1, 0))
+
+        for off, n, w8, slot in segs:
+            if off % 4 or n % 4 or off < pos:
+                return None
+            plain(pos, off)
+            base = w8.data_ptr()
+            for c0 in range(0, n, CH):
+                rows.append((off + c0, min(CH, n - c0), slot, base + c0))
+            pos = off + n
+        plain(pos, store.total)
+        self._chunks = torch.tensor(rows, dtype=torch.int64, device=self.meta.device)
+        return self._chunks
+
     def calibrate(self) -> None:
         """Initial weight scales from their actual amax."""
         self.refresh()
@@ -454,3 +485,11 @@ class Fp8State:
         self.meta.update()
         self.gmeta.update()
         self.weights.refresh()
+
+    def before_fused_opt(self) -> None:
+        """Scale update ahead of an optimizer step that refreshes the e4m3
+        weight copies itself (Adam.apply(fp8w=...)): the same scales as
+        after_step(), which runs the update after the optimizer (neither
+        reads anything the optimizer writes)."""
+        self.meta.update()
+        self.gmeta.update()

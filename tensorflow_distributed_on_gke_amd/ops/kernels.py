@@ -563,6 +563,14 @@ def xent_stats(row_loss, row_correct, ntok, workers, step_out=None, accum=None):
     C().xent_stats(row_loss, row_correct, ntok, workers, step_out, accum)
 
 
+def adam_chunks(p, g, m, v, shadow, chunks, step, beta1, beta2, eps, lr_const, d_model, warmup,
+                grad_scale, weight_decay, sched, zero_grad, inc_step, scale8, amax8):
+    """Adam over a chunk table that also refreshes e4m3 weight copies
+    (adam.hip adam_chunk_kernel; table: ops.fp8.Fp8Weights.adam_chunks)."""
+    C().adam_chunks(p, g, m, v, shadow, chunks, step, beta1, beta2, eps, lr_const, d_model, warmup,
+                    grad_scale, weight_decay, sched, zero_grad, inc_step, scale8, amax8)
+
+
 def adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale=1.0,
          weight_decay=0.0, sched=1, zero_grad=True, inc_step=True):
     C().adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale,

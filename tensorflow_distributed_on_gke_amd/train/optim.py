@@ -49,8 +49,24 @@ class Adam:
             return self.lr_const
         return noam_lr(step, self.d_model, self.warmup)
 
-    def apply(self, grad_scale: float = 1.0) -> None:
+    def apply(self, grad_scale: float = 1.0, fp8w=None) -> bool:
+        """The whole step. fp8w (ops.fp8.Fp8Weights): also refresh its e4m3
+        weight copies from the updated weights in the same pass (GPU; returns
+        False -- nothing done -- when its chunk table is unavailable)."""
+        s = self.store
+        if fp8w is not None:
+            chunks = fp8w.adam_chunks(s) if s.flat.is_cuda and s.flat_compute is not None else None
+            if chunks is None:
+                return False
+            K.adam_chunks(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, chunks, self.step,
+                          self.beta1, self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model),
+                          float(self.warmup), 1.0 * grad_scale, self.weight_decay,
+                          0 if self.lr_const is not None else 1, self.zero_grad, True,
+                          fp8w.meta.scale, fp8w.meta.amax)
+            s.refresh_transposed(0, s.total)
+            return True
         self.apply_range(0, self.store.total, grad_scale, inc_step=True)
+        return True
 
     def apply_range(self, start: int, end: int, grad_scale: float = 1.0, inc_step: bool = True) -> None:
         """Update flat[start:end] only (one data-parallel bucket, as soon as its

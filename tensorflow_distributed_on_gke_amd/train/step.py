@@ -51,6 +51,9 @@ DP_AUTOSELECT = True
 # contended with the encoder backward for more than it hid (6.45 vs 6.34 ms).
 # "0": one Adam after finish.
 DP_OVERLAP_OPT = "tail"
+# fp8 (one optimizer pass over the whole buffer): the Adam kernel also
+# refreshes the e4m3 weight copies (no separate re-quantisation pass)
+FUSED_FP8_ADAM = True
 
 
 class TrainStep:
@@ -157,6 +160,12 @@ class TrainStep:
         if self.ddp is not None:
             self.ddp.finish()
         if self.ddp is None or self.ddp.opt is None:
+            if self.fp8 is not None and FUSED_FP8_ADAM and \
+                    self.fp8.weights.adam_chunks(self.model.store) is not None:
+                # new scales, then Adam refreshing the e4m3 weight copies
+                self.fp8.before_fused_opt()
+                self.opt.apply(fp8w=self.fp8.weights)
+                return self.last
             self.opt.apply()
         if self.fp8 is not None:
             self.fp8.after_step()  # new scales, then fp8 weight copies

@@ -573,3 +573,34 @@ def test_attn_bwd_emits_e5m2_grads(causal, L, S, kv):
         assert torch.allclose(cs[2 * d:], dv.float().sum((0, 1)).reshape(d), rtol=1e-3, atol=1e-3)
         am = torch.maximum(am, torch.maximum(dk.float().abs().max(), dv.float().abs().max()))
     assert gm.amax_values()[i].item() == am.item()
+
+
+def test_fused_fp8_adam_matches_separate_refresh(monkeypatch):
+    """The Adam kernel that refreshes the e4m3 weight copies itself (scale
+    update first, adam_chunk_kernel) trains bitwise like Adam followed by the
+    scale update and the separate re-quantisation pass."""
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.train import step as step_mod
+    from tensorflow_distributed_on_gke_amd.train.optim import Adam
+    from tensorflow_distributed_on_gke_amd.train.step import TrainStep
+
+    cfg = model_config("tiny", src_vocab=96, tgt_vocab=96, dropout=0.1)
+    data = SyntheticPairs(batch=16, src_len=16, tgt_len=17, src_vocab=96, tgt_vocab=96, seed=2)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(step_mod, "FUSED_FP8_ADAM", fused)
+        m = Transformer(cfg).build("cuda", seed=4)
+        opt = Adam(m.store, cfg.d_model)
+        st = F.Fp8State(m)
+        if fused:
+            assert st.weights.adam_chunks(m.store) is not None
+        step = TrainStep(m, opt, None, workers=1.0, seed=3, fp8_state=st)
+        for i in range(4):
+            src, tgt = data.batch(i)
+            step(src.cuda(), tgt.cuda())
+        torch.cuda.synchronize()
+        res[fused] = (m.store.flat.clone(), st.meta.scale.clone(),
+                      torch.cat([w8.view(torch.uint8).reshape(-1) for _, w8, _, _ in st.weights.items]))
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
