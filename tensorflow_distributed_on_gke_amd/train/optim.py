@@ -19,6 +19,11 @@ from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.train.schedule import noam_lr
 
 
+# whole-buffer steps through the contiguous-chunk kernel (adam_chunk_kernel:
+# one 4096-parameter chunk per workgroup) instead of the grid-strided one
+ADAM_CHUNKED = True
+
+
 class Adam:
     def __init__(self, store: ParamStore, d_model: int, warmup: float = 4000.0, beta1: float = 0.9,
                  beta2: float = 0.98, eps: float = 1e-9, lr: Optional[float] = None,
@@ -63,6 +68,18 @@ class Adam:
                           float(self.warmup), 1.0 * grad_scale, self.weight_decay,
                           0 if self.lr_const is not None else 1, self.zero_grad, True,
                           fp8w.meta.scale, fp8w.meta.amax)
+            s.refresh_transposed(0, s.total)
+            return True
+        if ADAM_CHUNKED and s.flat.is_cuda and s.flat_compute is not None and s.total < (1 << 28):
+            if getattr(self, "_chunks", None) is None:
+                rows = [(c0, min(4096, s.total - c0), -1, 0) for c0 in range(0, s.total, 4096)]
+                self._chunks = torch.tensor(rows, dtype=torch.int64, device=s.flat.device)
+                self._no8 = (torch.ones(1, device=s.flat.device), torch.zeros(2048, dtype=torch.int32,
+                                                                             device=s.flat.device))
+            K.adam_chunks(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, self._chunks, self.step,
+                          self.beta1, self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model),
+                          float(self.warmup), 1.0 * grad_scale, self.weight_decay,
+                          0 if self.lr_const is not None else 1, self.zero_grad, True, *self._no8)
             s.refresh_transposed(0, s.total)
             return True
         self.apply_range(0, self.store.total, grad_scale, inc_step=True)
