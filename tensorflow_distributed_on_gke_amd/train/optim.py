@@ -70,18 +70,6 @@ class Adam:
                           fp8w.meta.scale, fp8w.meta.amax)
             s.refresh_transposed(0, s.total)
             return True
-        if ADAM_CHUNKED and s.flat.is_cuda and s.flat_compute is not None and s.total < (1 << 28):
-            if getattr(self, "_chunks", None) is None:
-                rows = [(c0, min(4096, s.total - c0), -1, 0) for c0 in range(0, s.total, 4096)]
-                self._chunks = torch.tensor(rows, dtype=torch.int64, device=s.flat.device)
-                self._no8 = (torch.ones(1, device=s.flat.device), torch.zeros(2048, dtype=torch.int32,
-                                                                             device=s.flat.device))
-            K.adam_chunks(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, self._chunks, self.step,
-                          self.beta1, self.beta2, self.eps, self.lr_const or 0.0, float(self.d_model),
-                          float(self.warmup), 1.0 * grad_scale, self.weight_decay,
-                          0 if self.lr_const is not None else 1, self.zero_grad, True, *self._no8)
-            s.refresh_transposed(0, s.total)
-            return True
         self.apply_range(0, self.store.total, grad_scale, inc_step=True)
         return True
 
@@ -91,6 +79,26 @@ class Adam:
         counter; exactly one call per step (the last) passes inc_step."""
         s = self.store
         sl = slice(start, end)
+        if (s.flat.is_cuda and ADAM_CHUNKED and s.flat_compute is not None and s.total < (1 << 28)
+                and start % 4 == 0 and end % 4 == 0 and end > start):
+            tabs = self.__dict__.setdefault("_range_chunks", {})
+            if (start, end) not in tabs and torch.cuda.is_current_stream_capturing():
+                tabs = None  # (tables are built by the eager warm-up steps, not in a capture)
+        else:
+            tabs = None
+        if tabs is not None:
+            if (start, end) not in tabs:
+                rows = [(c0, min(4096, end - c0), -1, 0) for c0 in range(start, end, 4096)]
+                tabs[(start, end)] = torch.tensor(rows, dtype=torch.int64, device=s.flat.device)
+            if getattr(self, "_no8", None) is None:
+                self._no8 = (torch.ones(1, device=s.flat.device),
+                             torch.zeros(2048, dtype=torch.int32, device=s.flat.device))
+            K.adam_chunks(s.flat, s.flat_grad, self.m, self.v, s.flat_compute, tabs[(start, end)],
+                          self.step, self.beta1, self.beta2, self.eps, self.lr_const or 0.0,
+                          float(self.d_model), float(self.warmup), grad_scale, self.weight_decay,
+                          0 if self.lr_const is not None else 1, self.zero_grad, inc_step, *self._no8)
+            s.refresh_transposed(start, end)
+            return
         if s.flat.is_cuda:
             K.adam(s.flat[sl], s.flat_grad[sl], self.m[sl], self.v[sl],
                    s.flat_compute[sl] if s.flat_compute is not None else None, self.step,
