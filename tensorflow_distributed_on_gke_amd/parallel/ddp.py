@@ -45,13 +45,13 @@ from tensorflow_distributed_on_gke_amd.parallel.dist import PG_TIMEOUT_S
 
 
 # Issue GPU collectives from a host thread (CommThread) instead of making the
-# communication stream wait on the compute stream. Opt-in (TDG_DP_COMM_THREAD=1
-# on RCCL; "force": also over gloo with GPU tensors -- the multi-rank
-# rehearsals on one GPU, tests/test_gpu_dp.py). It measured 0.3 ms/step faster
-# on one rank (docs/PERF.md) but has not yet run on more than one GPU, so the
-# default is the process group's own stream handoff, the standard
-# torch.distributed issue path.
-COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "0")
+# communication stream wait on the compute stream. Default on RCCL
+# (TDG_DP_COMM_THREAD=0: the process group's own stream handoff; "force":
+# also over gloo with GPU tensors -- the multi-rank rehearsals on one GPU,
+# tests/test_gpu_dp.py). Round 4, one rank through the data-parallel step
+# (--force-dp 1, same box): 5.10-5.12 ms with the thread vs 5.33-5.35 without,
+# single graph 5.01 (profiles/r4/ab_dp_comm_thread.txt).
+COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1")
 # seconds the host waits for the comm thread to enqueue a collective before
 # the data-parallel state is poisoned and the step raises (a GPU that never
 # reaches the issue point would otherwise hang); default: the process-group

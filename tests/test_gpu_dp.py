@@ -87,7 +87,7 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1",
     (2, "0", "replica_mean", "", "0", False), (2, "tail", "replica_mean", "", "0", False),
     (2, "tail", "global_mean", "", "0", False), (2, "tail", "replica_mean", "seg", "0", False),
     (2, "0", "global_mean", "seg", "0", False),
-    # the opt-in host comm thread (TDG_DP_COMM_THREAD=1 on RCCL) driven over gloo
+    # the host comm thread (default on RCCL, TDG_DP_COMM_THREAD) driven over gloo
     (2, "tail", "replica_mean", "", "force", False), (2, "tail", "replica_mean", "seg", "force", False),
     (2, "tail", "global_mean", "seg", "force", False),
     # four ranks on the production path: segmented graph, bf16 gradient
