@@ -808,8 +808,8 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const optional<Tensor>& C, const
                   (bt ? B.numel() >= (K - 1) * ldb + N && ldb >= N && N % 16 == 0
                       : B.numel() >= (N - 1) * ldb + K),
               "gemm_fp8: A/B extent");
-  TORCH_CHECK(!bt || (cfg == 0 && afmt == 1 && cfmt == 1),
-              "gemm_fp8: N-contiguous B runs the e5m2 backward 128x128 config (cfg 0) only");
+  TORCH_CHECK(!bt || ((cfg == 0 || cfg == 10) && afmt == 1 && cfmt == 1),
+              "gemm_fp8: N-contiguous B runs the e5m2 backward 128x128 configs (cfg 0, 10) only");
   if (bias.has_value()) check_f32(*bias, "bias");
   const int64_t epi_id = epi & 15;  // (flag 16: C = dequant(C8))
   TORCH_CHECK((epi & ~int64_t(63)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
@@ -832,8 +832,8 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const optional<Tensor>& C, const
   }
   if (colsum_out.has_value()) {
     check_f32(*colsum_out, "colsum_out");
-    TORCH_CHECK(colsum_out->is_contiguous() && colsum_out->numel() == N && cfg == 0,
-                "gemm_fp8: colsum_out is [N] f32 (128x128 tile config)");
+    TORCH_CHECK(colsum_out->is_contiguous() && colsum_out->numel() == N && (cfg == 0 || cfg == 10),
+                "gemm_fp8: colsum_out is [N] f32 (128x128 tile configs 0, 10)");
     TORCH_CHECK(ws.has_value() && ws->scalar_type() == at::kFloat &&
                     ws->numel() >= ((M + 127) / 128) * 2 * N,
                 "gemm_fp8: colsum workspace [ceil(M/128)*2, N] f32");

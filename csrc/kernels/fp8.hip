@@ -217,6 +217,7 @@ struct F8Epi {
       }
     }
   }
+  // the 16x16 MFMA accumulators (acc[i][j] of the wave's WTM x WTN tile)
   static __device__ __forceinline__ void run(char* smem, const f32x4 (&acc)[TM][TN],
                                              bf16_t* __restrict__ C, const float* __restrict__ bias,
                                              const float* __restrict__ sa,
@@ -225,11 +226,69 @@ struct F8Epi {
                                              unsigned* __restrict__ amax_out, int M, int N, int ldc,
                                              int ldc8, int m0, int n0, int wid, int lane, int tid,
                                              const F8Extra& ex, const Pre& pre) {
+    const int g = lane >> 4, cl = lane & 15, wn = wid % WN;
+    run_w(
+        [&](char* wimg, float alpha) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WTN + 16 * j + cl;
+            float bn = 0.f;
+            if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float v = alpha * acc[i][j][r] + bn;
+                if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                *reinterpret_cast<bf16_t*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * 2) = f2bf(v);
+              }
+          }
+        },
+        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre);
+  }
+  // the 32x32 MFMA accumulators (acc[i][j]: rows 32 i .., columns 32 j .. of the wave's tile)
+  static __device__ __forceinline__ void run32(char* smem, const f32x16 (&acc)[WTM / 32][WTN / 32],
+                                               bf16_t* __restrict__ C, const float* __restrict__ bias,
+                                               const float* __restrict__ sa,
+                                               const float* __restrict__ sb, uint8_t* __restrict__ C8,
+                                               const float* __restrict__ sc8,
+                                               unsigned* __restrict__ amax_out, int M, int N, int ldc,
+                                               int ldc8, int m0, int n0, int wid, int lane, int tid,
+                                               const F8Extra& ex, const Pre& pre) {
+    const int h = lane >> 5, cl = lane & 31, wn = wid % WN;
+    run_w(
+        [&](char* wimg, float alpha) {
+#pragma unroll
+          for (int j = 0; j < WTN / 32; ++j) {
+            const int n = n0 + wn * WTN + 32 * j + cl;
+            float bn = 0.f;
+            if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
+#pragma unroll
+            for (int i = 0; i < WTM / 32; ++i)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                float v = alpha * acc[i][j][r] + bn;
+                if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                const int row = 32 * i + 8 * (r >> 2) + 4 * h + (r & 3);
+                *reinterpret_cast<bf16_t*>(wimg + row * SROW + (32 * j + cl) * 2) = f2bf(v);
+              }
+          }
+        },
+        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre);
+  }
+  // write_img(wimg, alpha): the wave's dequantised (bias, ReLU) bf16 tile into its image
+  template <class W>
+  static __device__ __forceinline__ void run_w(W&& write_img, char* smem, bf16_t* __restrict__ C,
+                                               const float* __restrict__ sa,
+                                               const float* __restrict__ sb, uint8_t* __restrict__ C8,
+                                               const float* __restrict__ sc8,
+                                               unsigned* __restrict__ amax_out, int M, int N, int ldc,
+                                               int ldc8, int m0, int n0, int wid, int lane, int tid,
+                                               const F8Extra& ex, const Pre& pre) {
     const int wm = wid / WN, wn = wid % WN;
     const float alpha = 1.f / (sa[0] * sb[0]);
     const float s8 = C8 ? sc8[0] : 0.f;
     char* wimg = smem + wid * (WTM * SROW);
-    const int g = lane >> 4, cl = lane & 15;
     static_assert(64 % CPR == 0, "a lane keeps its column chunk across iterations");
     short8_t pre_aux[PRE && !A8 ? ITER : 1];
     const bool vec_ok = F8Epi::vec_ok(ldc, ex);
@@ -250,20 +309,7 @@ struct F8Epi {
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WTN + 16 * j + cl;
-      float bn = 0.f;
-      if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = alpha * acc[i][j][r] + bn;
-          if constexpr (EPI == F8_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-          *reinterpret_cast<bf16_t*>(wimg + (16 * i + 4 * g + r) * SROW + (16 * j + cl) * 2) = f2bf(v);
-        }
-    }
+    write_img(wimg, alpha);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     float amax = 0.f;
 #pragma unroll
@@ -571,6 +617,198 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   f8::lds_barrier();
   Epi::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
            pre);
+}
+
+// ---------------------------------------------------------------------------
+// 128x128 tile on 4 waves (64x64 each) on the 32x32x64 block-scaled MFMA, so
+// one K step is 64 bytes: a ring of FIVE 16 KiB stages (an 8 KiB A image
+// [128 rows][64 B] + an 8 KiB B image) per workgroup, two workgroups per CU
+// (80 KiB each). Step j: wait for stage j, one barrier (stage j landed for
+// every wave; stage j - 1 read by every wave), issue stage j + 4 into stage
+// j - 1's slot, read the fragments, 4 MFMAs per wave. Every stage is issued
+// FOUR steps (two 128-byte K steps) before it is read: 64 KiB per workgroup
+// in flight across the load latency, against 32 KiB in gemm_fp8_kernel's
+// 2-stage 128-byte loop, whose stage is read one step after its issue. The
+// loop is bound by bytes in flight per CU (docs/PERF.md "Round 4").
+// K-contiguous stage image: row R, 16-byte chunk c at chunk c ^ ((R >> 2) & 3):
+// the four ds_read_b128 lane groups of a 32-row fragment read (rows R..R+31
+// by lane & 31, chunk pair 2 (lane >> 5)) hit 16 distinct 16-byte slots each.
+namespace f8r {
+constexpr int IMG = 128 * 64;  // bytes of one operand stage image
+constexpr int NS = 5;          // ring slots (each: A image + B image)
+constexpr int SLOT = 2 * IMG;
+__device__ __forceinline__ int off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// LDS-DMA of a [128 rows][64 B] K-slice of a K-contiguous operand: 8 pieces of
+// 16 rows; wave wid issues pieces 2 wid, 2 wid + 1 (lane: row 16 piece +
+// lane / 4, chunk position lane % 4 <- operand chunk (lane % 4) ^ ((row >> 2) & 3))
+struct StageK {
+  uint32_t off[2];
+  __device__ __forceinline__ void init(int wid, int lane, int mn0, int len, int ld) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wid * 2 + i) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      int mn = mn0 + row;
+      mn = mn < len ? mn : len - 1;
+      off[i] = (uint32_t)mn * (uint32_t)ld + (uint32_t)(c * 16);
+    }
+  }
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ X, int k0, char* lds, int wid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(X + off[i] + k0),
+                                       (__attribute__((address_space(3))) void*)(lds + (wid * 2 + i) * 1024),
+                                       16, 0, 0);
+  }
+};
+// N-contiguous stage image ([64 k-rows][128 n-bytes]): row t, 16-byte chunk c
+// at chunk c ^ (2 ((t >> 1) & 3)): a transposing fragment read's 32-lane half
+// (rows 8 j + q, q < 8; 32 columns: chunks c0, c0 + 1 with c0 even) lands
+// on 32 distinct 8-byte slots
+__device__ __forceinline__ int swn(int t) { return ((t >> 1) & 3) << 1; }
+__device__ __forceinline__ int offn(int t, int x) { return t * 128 + ((((x >> 4) ^ swn(t)) & 7) << 4) + (x & 15); }
+struct StageN {
+  uint32_t off[2];
+  __device__ __forceinline__ void init(int wid, int lane, int n0, int N, int ld) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wid * 2 + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swn(row);
+      int n = n0 + 16 * c;
+      n = n + 16 <= N ? n : 0;  // past the operand: never stored (N % 16 == 0)
+      off[i] = (uint32_t)row * (uint32_t)ld + (uint32_t)n;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ X, int ld, int k0, char* lds,
+                                        int wid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(X + (size_t)k0 * ld + off[i]),
+                                       (__attribute__((address_space(3))) void*)(lds + (wid * 2 + i) * 1024),
+                                       16, 0, 0);
+  }
+};
+// 32x32x64 operand fragment of a K-contiguous image: row base + (lane & 31),
+// K bytes 32 (lane >> 5) .. +31
+__device__ __forceinline__ i32x8 frag(const char* img, int base, int lane) {
+  const int row = base + (lane & 31), c = 2 * (lane >> 5);
+  const int4 lo = __builtin_bit_cast(int4, tdg::lds_read_b128_async(img + off(row, c)));
+  const int4 hi = __builtin_bit_cast(int4, tdg::lds_read_b128_async(img + off(row, c + 1)));
+  return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+// ... of an N-contiguous image: column base + (lane & 31), K rows
+// 32 (lane >> 5) .. +31 by four transposing reads of 8 rows (a 16-lane group
+// reads 8 rows x 16 columns; lane w of it gets column w)
+__device__ __forceinline__ i32x8 frag_t(const char* img, int base, int lane) {
+  const int h = lane >> 5, cb = base + 16 * ((lane >> 4) & 1), w = lane & 15, q = w >> 1, p = w & 1;
+  uint64_t r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = wf8::tr8(img + offn(32 * h + 8 * j + q, cb + 8 * p));
+  return i32x8{(int)r[0], (int)(r[0] >> 32), (int)r[1], (int)(r[1] >> 32),
+               (int)r[2], (int)(r[2] >> 32), (int)r[3], (int)(r[3] >> 32)};
+}
+}  // namespace f8r
+
+template <int EPI, int AF = 0, int CF = 0, bool BT = false>
+__global__ __launch_bounds__(256) void gemm_fp8_ring_kernel(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
+    uint8_t* __restrict__ C8, const float* __restrict__ sc8, unsigned* __restrict__ amax_out,
+    int M, int N, int K, int lda, int ldb, int ldc, int ldc8, F8Extra ex) {
+  constexpr int P = 4;  // LDS-DMA pieces per wave per stage (A 2 + B 2)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = cdiv(M, 128), tiles_n = cdiv(N, 128);
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  if (tiles_n <= tiles_m) {
+    tn = t % tiles_n;
+    tm = t / tiles_n;
+  } else {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+  }
+  const int m0 = tm * 128, n0 = tn * 128;
+  const int ns = K / 64;  // 64-byte K steps (host: K % 128 == 0, so ns >= 2)
+
+  using Epi = F8Epi<128, 128, 2, 2, EPI, CF>;
+  typename Epi::Pre pre;
+  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex);  // (older than every DMA)
+  f8r::StageK ga;
+  ga.init(wid, lane, m0, M, lda);
+  f8r::StageK gbk;
+  f8r::StageN gbn;
+  if constexpr (BT) gbn.init(wid, lane, n0, N, ldb);
+  else gbk.init(wid, lane, n0, N, ldb);
+  auto issue = [&](int j) {
+    char* slot = smem + (j % f8r::NS) * f8r::SLOT;
+    ga.issue(A, 64 * j, slot, wid);
+    if constexpr (BT) gbn.issue(B, ldb, 64 * j, slot + f8r::IMG, wid);
+    else gbk.issue(B, 64 * j, slot + f8r::IMG, wid);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int abase = wm * 64, bbase = wn * 64;
+
+  // prologue: stages 0..3 (ns >= 2); step j waits for stage j with the
+  // stages issued after it (up to j + 3) still in flight
+  issue(0);
+  issue(1);
+  if (ns > 2) issue(2);
+  if (ns > 3) issue(3);
+  // W: stages younger than j in flight at step j's wait; ISS: issue stage j + 4
+  auto kstep = [&](int j, auto wc, auto ic) {
+    constexpr int W = decltype(wc)::value;
+    constexpr bool ISS = decltype(ic)::value != 0;
+    f8::wait_vmcnt<W * P>();
+    f8::lds_barrier();
+    if constexpr (ISS) issue(j + 4);
+    const char* st = smem + (j % f8r::NS) * f8r::SLOT;
+    i32x8 fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = f8r::frag(st, abase + 32 * i, lane);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if constexpr (BT) fb[jj] = f8r::frag_t(st + f8r::IMG, bbase + 32 * jj, lane);
+      else fb[jj] = f8r::frag(st + f8r::IMG, bbase + 32 * jj, lane);
+    }
+    tdg::lgkm_wait<0>();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) tdg::tie(fa[i]);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) tdg::tie(fb[jj]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+        acc[i][jj] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[i], fb[jj], acc[i][jj], AF, 0,
+                                                                     0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  int j = 0;
+  for (; j + 4 < ns; ++j) kstep(j, I3{}, I1{});  // stages j+1..j+3 in flight; issue j + 4
+  // tail: no more issues; the stages younger than j in flight: ns - 1 - j
+  if (ns - j == 4) kstep(j++, I3{}, I0{});
+  if (ns - j == 3) kstep(j++, I2{}, I0{});
+  kstep(j++, I1{}, I0{});
+  kstep(j, I0{}, I0{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  f8::lds_barrier();
+  Epi::run32(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid,
+             ex, pre);
 }
 
 // ---------------------------------------------------------------------------
@@ -1324,6 +1562,27 @@ int launch_f8_w1(const void* A, const void* B, void* C, const float* bias, const
   return 0;
 }
 
+template <int EPI, int AF = 0, int CF = 0, bool BT = false>
+int launch_f8r(const void* A, const void* B, void* C, const float* bias, const float* sa,
+               const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
+               int lda, int ldb, int ldc, int ldc8, const F8Extra& ex, hipStream_t st) {
+  if ((long long)M * lda >= (1LL << 32) || (!BT && (long long)N * ldb >= (1LL << 32))) return -3;
+  constexpr int img = 4 * 64 * (64 * 2 + 16) + 64;
+  constexpr int lds = std::max(f8r::NS * f8r::SLOT, img);
+  static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_fp8_ring_kernel<EPI, AF, CF, BT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int tiles = cdiv(M, 128) * cdiv(N, 128);
+  hipLaunchKernelGGL((gemm_fp8_ring_kernel<EPI, AF, CF, BT>), dim3(tiles), dim3(256), lds, st,
+                     (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C, bias, sa, sb, (uint8_t*)C8,
+                     sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
+  return 0;
+}
+
 template <int EPI>
 int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, const float* sa,
              const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
@@ -1341,6 +1600,8 @@ int tiles_f8(int cfg, const void* A, const void* B, void* C, const float* bias, 
     case 9:  // 256x256, one wave per SIMD (gemm_fp8_w1_kernel)
       if ((long long)M * lda >= (1LL << 32) || (long long)N * ldb >= (1LL << 32)) return -3;
       return launch_f8_w1<EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    case 10:  // 128x128, ring of 64-byte K half-stages (gemm_fp8_ring_kernel)
+      return launch_f8r<EPI>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
     default:
       TDG_F8(5, 64, 128, 2, 2, 2)
   }
@@ -1372,10 +1633,10 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
   const int cdeq = (epi & F8_EPI_CDEQ) != 0;
   const bool bt = (epi & F8_B_NCONTIG) != 0;
   epi &= ~(F8_EPI_CDEQ | F8_B_NCONTIG);
-  if (bt && (cfg != 0 || N % 16 != 0 || ldb < N || afmt != 1 || cfmt != 1)) return -6;
+  if (bt && ((cfg != 0 && cfg != 10) || N % 16 != 0 || ldb < N || afmt != 1 || cfmt != 1)) return -6;
   if (cdeq && !C8) return -2;
   if (!C && (beta != 0.f || cdeq)) return -2;
-  if (colsum_out && (!ws || cfg != 0)) return -2;  // (partials: the 128x128 / 2x2 tile)
+  if (colsum_out && (!ws || (cfg != 0 && cfg != 10))) return -2;  // (partials: 128x128 / 2x2 tiles)
   const F8Extra ex{(const bf16_t*)aux, ldaux, beta, cdeq, (const uint8_t*)aux8,
                    colsum_out ? ws : nullptr};
   if (colsum_out) {
@@ -1394,7 +1655,16 @@ static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float*
                              unsigned* amax, int M, int N, int K, int lda, int ldb, int ldc,
                              int ldc8, int epi, int cfg, int afmt, int cfmt, const F8Extra& ex,
                              hipStream_t st, bool bt) {
-  if (bt) {  // e5m2 x N-contiguous e4m3 (validated by the caller: cfg 0)
+  if (bt && cfg == 10) {
+    if (epi == F8_EPI_DRELU && ex.aux8)
+      return launch_f8r<F8_EPI_DRELU8, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    if (epi == F8_EPI_DRELU)
+      return launch_f8r<F8_EPI_DRELU, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    if (epi == F8_EPI_NONE)
+      return launch_f8r<F8_EPI_NONE, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+    return -1;
+  }
+  if (bt) {  // e5m2 x N-contiguous e4m3 (validated by the caller: cfg 0 or 10)
     if (epi == F8_EPI_DRELU && ex.aux8)
       return launch_f8<128, 128, 2, 2, 2, F8_EPI_DRELU8, 1, 1, true>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
     if (epi == F8_EPI_DRELU)
@@ -1412,6 +1682,15 @@ static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float*
     }
   }
   if (afmt == 1 && cfmt == 1) {
+    if (cfg == 10) {
+      if (epi == F8_EPI_DRELU && ex.aux8)
+        return launch_f8r<F8_EPI_DRELU8, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      if (epi == F8_EPI_DRELU)
+        return launch_f8r<F8_EPI_DRELU, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      if (epi == F8_EPI_NONE)
+        return launch_f8r<F8_EPI_NONE, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
+      return -1;
+    }
     if (epi == F8_EPI_DRELU && ex.aux8) {
       if (cfg == 9 && (long long)M * lda < (1LL << 32) && (long long)N * ldb < (1LL << 32))
         return launch_f8_w1<F8_EPI_DRELU8, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);

@@ -37,14 +37,17 @@ BF8 = torch.float8_e5m2  # gradient format of the fp8 backward
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
 AMAX_WORDS = 64 * 32  # per slot (csrc/include/tdg_common.h AMAX_WORDS)
-_CANDS = (0, 1, 2, 3, 4, 5, 8, 9)
+_CANDS = (0, 1, 2, 3, 4, 5, 8, 9, 10)
 # FFN weight gradients in fp8 (wgrad_fp8) when the step runs the fp8 backward
 WGRAD_FP8 = True
 # attention projections in fp8 too (Fp8State(backward=True)): output
 # projection forward, every projection dgrad and weight gradient
 ATTN_PROJ_FP8 = True
-# tile config of the e5m2 x e4m3 backward GEMMs (0: 128x128 / 4 waves; 9: 256x256 at one wave per SIMD)
+# tile config of the e5m2 x e4m3 backward GEMMs (0: 128x128 / 4 waves; 9: 256x256 at one wave per SIMD;
+# 10: 128x128 / 4 waves on a ring of 64-byte K half-stages)
 BWD_CFG = 0
+# ... of those reading the weight N-contiguous or producing column sums (0 or 10)
+BWD_CFG_128 = 0
 # fp8 dgrads read the forward's e4m3 weight copy N-contiguous (transposing LDS
 # reads, 128x128 tiles) instead of a transposed copy: no fp8_quant_t pass
 # over every weight per step
@@ -177,8 +180,8 @@ def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
     aux = relu_aux if relu_aux is not None else relu_aux8
     c = BWD_CFG if cfg is None else cfg
     ws = None
-    if colsum_out is not None or w_plain:
-        c = 0
+    if (colsum_out is not None or w_plain) and c not in (0, 10):
+        c = BWD_CFG_128
     if colsum_out is not None:
         ws = K.workspace("fp8_colsum", math.ceil(M / 128) * 2 * N, g8.device)
     epi = (3 if aux is not None else 0) | (32 if w_plain else 0)

@@ -74,12 +74,13 @@ def test_quantize_matches_torch_e5m2():
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (64, 64, 128), (600, 520, 1024)])
 @pytest.mark.parametrize("relu,beta", [(True, 0.0), (False, 1.0)])
-@pytest.mark.parametrize("cfg", [0, 9, "plain"])
+@pytest.mark.parametrize("cfg", [0, 9, 10, "plain", "plain10"])
 def test_gemm_bf8_dgrad(M, N, K, relu, beta, cfg):
     """out (=|+= beta) dequant(g8 e5m2 @ w8t e4m3^T), ReLU-backward mask, and
     the e5m2 copy of the output, against an fp32 reference. "plain": the
-    weight given untransposed ([K][N], read N-contiguous by the kernel)."""
-    if cfg == "plain" and N % 16:
+    weight given untransposed ([K][N], read N-contiguous by the kernel);
+    10: the half-stage ring kernel."""
+    if str(cfg).startswith("plain") and N % 16:
         pytest.skip("the N-contiguous weight path needs N % 16 == 0")
     torch.manual_seed(1)
     wm, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
@@ -94,9 +95,10 @@ def test_gemm_bf8_dgrad(M, N, K, relu, beta, cfg):
     if relu:
         ref = ref * (aux.float() > 0)
     ref = ref + beta * out.float()
-    if cfg == "plain":
+    if str(cfg).startswith("plain"):
         o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8.t().contiguous(), wm, iw, out, relu_aux=aux, beta=beta,
-                              out8_slot=io if relu else None, w_plain=True)
+                              out8_slot=io if relu else None, w_plain=True,
+                              cfg=10 if cfg == "plain10" else 0)
     else:
         o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, wm, iw, out, relu_aux=aux, beta=beta,
                               out8_slot=io if relu else None, cfg=cfg)
@@ -379,7 +381,8 @@ def test_fp8_ffn_wgrad_matches_bf16_path(monkeypatch):
 @pytest.mark.parametrize("M,N,K", [(512, 384, 256), (333, 1000, 512), (1024, 4096, 1024)])
 @pytest.mark.parametrize("with_c", [True, False])
 @pytest.mark.parametrize("plain", [False, True])
-def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c, plain):
+@pytest.mark.parametrize("cfg", [0, 10])
+def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c, plain, cfg):
     """The lean fp8 FFN backward's ReLU-backward dgrad: mask from the e4m3
     hidden (h8 != 0), optional bf16 output, e5m2 copy, and the bias gradient
     (column sums of the bf16-rounded output, accumulated with beta) from the
@@ -400,7 +403,8 @@ def test_gemm_bf8_dgrad_mask8_colsum(M, N, K, with_c, plain):
     bsum = torch.randn(N, device=DEV)
     bref = bsum + ref.bfloat16().float().sum(0)
     o8 = F.gemm_bf8_dgrad(g8, gm, ig, w8.t().contiguous() if plain else w8, wm, iw, out,
-                          relu_aux8=h8, out8_slot=io, colsum_out=bsum, colsum_beta=1.0, w_plain=plain)
+                          relu_aux8=h8, out8_slot=io, colsum_out=bsum, colsum_beta=1.0, w_plain=plain,
+                          cfg=cfg)
     # (the kernel quantises the bf16-rounded value; compare values: masked
     # elements are +0 from the kernel, -0 in ref * 0)
     o8ref = (ref.bfloat16().float() * 2.0 ** 10).clamp(-57344, 57344).to(torch.float8_e5m2)
