@@ -236,9 +236,10 @@ void check_like(const Tensor& t, const tdg::AttnArgs& a, int L, const char* n) {
   TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.size(0) == a.B && t.size(1) == L &&
                   t.size(2) == a.H,
               n, ": bad shape/stride");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 8) == 0 && t.stride(1) % 4 == 0 &&
-                  t.stride(2) % 4 == 0,
-              n, ": rows must be 8-byte aligned");
+  // (16 bytes: the kernels store whole 16-byte row chunks, attention.hip store_row16)
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0 && t.stride(0) % 8 == 0 &&
+                  t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
+              n, ": rows must be 16-byte aligned");
 }
 
 void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out,

@@ -35,6 +35,38 @@ constexpr float LOG2E = 1.4426950408889634f;
 // flushed to zero change nothing at bf16 P.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Row-per-lane store of a 16x16-MFMA output row: lane (g, cl) holds columns
+// 16 dt + 4 g .. +3 (dt < DT) of its row as packed bf16 pairs lo[dt] / hi[dt].
+// For each dt pair, v_permlane16_swap exchanges the odd 16-lane groups' dt
+// half with the even groups' dt + 1 half, after which every lane holds 16
+// contiguous bytes -- columns 16 (dt + (g & 1)) + 8 (g >> 1) .. +7 -- and
+// writes them with one dwordx4: half the store instructions of the 8-byte
+// form, whose tail was store-issue-bound (the guide's T21). Every lane of
+// the wave must call it (the swaps); `store` masks the lane's row.
+template <int DT>
+__device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint32_t (&lo)[DT],
+                                            const uint32_t (&hi)[DT], int g, bool store) {
+  if constexpr (DT % 2 == 0) {
+#pragma unroll
+    for (int d = 0; d < DT; d += 2) {
+      const auto r0 = __builtin_amdgcn_permlane16_swap(lo[d], lo[d + 1], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(hi[d], hi[d + 1], false, false);
+      if (store)
+        *reinterpret_cast<uint4*>(row + 16 * (d + (g & 1)) + 8 * (g >> 1)) =
+            make_uint4(r0[0], r1[0], r0[1], r1[1]);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+      if (store) *reinterpret_cast<uint2*>(row + 16 * d + 4 * g) = make_uint2(lo[d], hi[d]);
+  }
+}
+// (the packing of an accumulator: 4 values, times sc)
+__device__ __forceinline__ void pack_acc(const f32x4& v, float sc, uint32_t& lo, uint32_t& hi) {
+  lo = (uint32_t)f2bf(v[0] * sc) | ((uint32_t)f2bf(v[1] * sc) << 16);
+  hi = (uint32_t)f2bf(v[2] * sc) | ((uint32_t)f2bf(v[3] * sc) << 16);
+}
+
 // Key window and logit scale of batch row b. A row with NO valid key
 // (kv_len == 0: an all-PAD sequence) gets the reference's numerics: its
 // padding mask adds -1e9 to every logit, which in fp32 leaves them all equal
@@ -359,17 +391,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
     float lu = l[u];
     lu += __shfl_xor(lu, 16, 64);
     lu += __shfl_xor(lu, 32, 64);
-    if (qrow[u] >= a.Lq) continue;
+    const bool ok = qrow[u] < a.Lq;
     const float inv = lu > 0.f ? 1.f / lu : 0.f;
     bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      // rows d = 16dt + 4g + r
-      uint32_t lo = (uint32_t)f2bf(oacc[u][dt][0] * inv) | ((uint32_t)f2bf(oacc[u][dt][1] * inv) << 16);
-      uint32_t hi = (uint32_t)f2bf(oacc[u][dt][2] * inv) | ((uint32_t)f2bf(oacc[u][dt][3] * inv) << 16);
-      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
-    if (g == 0)
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(oacc[u][dt], inv, lo[dt], hi[dt]);  // columns 16dt + 4g + r
+    store_row16<T::DT>(op, lo, hi, g, ok);
+    if (ok && g == 0)
       a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + log2f(lu) : INFINITY;
   }
 #ifdef TDG_STAMPS
@@ -510,16 +539,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
     float lu = l[u];
     lu += __shfl_xor(lu, 16, 64);
     lu += __shfl_xor(lu, 32, 64);
-    if (qrow[u] >= a.Lq) continue;
+    const bool ok = qrow[u] < a.Lq;
     const float inv = lu > 0.f ? 1.f / lu : 0.f;
     bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      uint32_t lo = (uint32_t)f2bf(oacc[u][dt][0] * inv) | ((uint32_t)f2bf(oacc[u][dt][1] * inv) << 16);
-      uint32_t hi = (uint32_t)f2bf(oacc[u][dt][2] * inv) | ((uint32_t)f2bf(oacc[u][dt][3] * inv) << 16);
-      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
-    if (g == 0)
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(oacc[u][dt], inv, lo[dt], hi[dt]);
+    store_row16<T::DT>(op, lo, hi, g, ok);
+    if (ok && g == 0)
       a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + log2f(lu) : INFINITY;
   }
 }
@@ -685,16 +712,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   // values (what quantising the bf16 O gives), wave amax -> one atomic
   const float so = a.out8 ? a.so8[0] : 0.f;
   float am = 0.f;
+  uint32_t olo[DT], ohi[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) pack_acc(oacc[dt], inv, olo[dt], ohi[dt]);
+  store_row16<DT>(op, olo, ohi, g, valid);
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
-    bf16_t e[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) e[r] = f2bf(oacc[dt][r] * inv);
-    if (valid) {
-      const uint32_t lo = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
-      const uint32_t hi = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
-      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    const bf16_t e[4] = {(bf16_t)(olo[dt] & 0xffff), (bf16_t)(olo[dt] >> 16), (bf16_t)(ohi[dt] & 0xffff),
+                         (bf16_t)(ohi[dt] >> 16)};
     if (a.out8) {
       float v[4];
 #pragma unroll
@@ -846,19 +871,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (key[u] >= a.Lk) continue;
+    const bool ok = key[u] < a.Lk;
     bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
     bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
-    const float sc = a.scale;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
-      uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-      lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
-      hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
-      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dk[u][dt], a.scale, lo[dt], hi[dt]);
+    store_row16<T::DT>(dkp, lo, hi, g, ok);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dv[u][dt], 1.f, lo[dt], hi[dt]);
+    store_row16<T::DT>(dvp, lo, hi, g, ok);
   }
 }
 
@@ -986,15 +1008,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (qrow[u] >= a.Lq) continue;
     bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow[u] * a.dq_sl + h * a.dq_sh;
-    const float sc = a.scale;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
-      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dq[u][dt], a.scale, lo[dt], hi[dt]);
+    store_row16<T::DT>(dqp, lo, hi, g, qrow[u] < a.Lq);
   }
 }
 
@@ -1254,19 +1272,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   if (!a.skip_bf16) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (key[u] >= a.Lk) continue;
+    const bool ok = key[u] < a.Lk;
     bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
     bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
-    const float sc = a.scale;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
-      uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-      lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
-      hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
-      *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dk[u][dt], a.scale, lo[dt], hi[dt]);
+    store_row16<T::DT>(dkp, lo, hi, g, ok);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dv[u][dt], 1.f, lo[dt], hi[dt]);
+    store_row16<T::DT>(dvp, lo, hi, g, ok);
   }
   }
   if (a.dk8) {  // e5m2 dK / dV (+ amax, + bias-gradient partials)
@@ -1457,15 +1472,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   if (!a.skip_bf16) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (qrow[u] >= a.Lq) continue;
     bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow[u] * a.dq_sl + h * a.dq_sh;
-    const float sc = a.scale;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
-      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dq[u][dt], a.scale, lo[dt], hi[dt]);
+    store_row16<T::DT>(dqp, lo, hi, g, qrow[u] < a.Lq);
   }
   }
   if (a.dq8) {  // e5m2 dQ (+ amax, + bias-gradient partials)
@@ -1682,19 +1693,16 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
   const float sc = a.scale;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (key[u] < a.Lk) {
-      bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
-      bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
+    const bool ok = key[u] < a.Lk;
+    bf16_t* dkp = a.dk + b * a.dk_sb + (long long)key[u] * a.dk_sl + h * a.dk_sh;
+    bf16_t* dvp = a.dv + b * a.dv_sb + (long long)key[u] * a.dv_sl + h * a.dv_sh;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-      for (int dt = 0; dt < T::DT; ++dt) {
-        uint32_t lo = (uint32_t)f2bf(dk[u][dt][0] * sc) | ((uint32_t)f2bf(dk[u][dt][1] * sc) << 16);
-        uint32_t hi = (uint32_t)f2bf(dk[u][dt][2] * sc) | ((uint32_t)f2bf(dk[u][dt][3] * sc) << 16);
-        *reinterpret_cast<uint2*>(dkp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-        lo = (uint32_t)f2bf(dv[u][dt][0]) | ((uint32_t)f2bf(dv[u][dt][1]) << 16);
-        hi = (uint32_t)f2bf(dv[u][dt][2]) | ((uint32_t)f2bf(dv[u][dt][3]) << 16);
-        *reinterpret_cast<uint2*>(dvp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-      }
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dk[u][dt], sc, lo[dt], hi[dt]);
+    store_row16<T::DT>(dkp, lo, hi, g, ok);
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dv[u][dt], 1.f, lo[dt], hi[dt]);
+    store_row16<T::DT>(dvp, lo, hi, g, ok);
   }
   __syncthreads();
 
@@ -1721,14 +1729,11 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int qrow = 16 * (U * w + u) + cl;
-    if (qrow >= a.Lq) continue;
     bf16_t* dqp = a.dq + b * a.dq_sb + (long long)qrow * a.dq_sl + h * a.dq_sh;
+    uint32_t lo[T::DT], hi[T::DT];
 #pragma unroll
-    for (int dt = 0; dt < T::DT; ++dt) {
-      const uint32_t lo = (uint32_t)f2bf(dq[u][dt][0] * sc) | ((uint32_t)f2bf(dq[u][dt][1] * sc) << 16);
-      const uint32_t hi = (uint32_t)f2bf(dq[u][dt][2] * sc) | ((uint32_t)f2bf(dq[u][dt][3] * sc) << 16);
-      *reinterpret_cast<uint2*>(dqp + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(dq[u][dt], sc, lo[dt], hi[dt]);
+    store_row16<T::DT>(dqp, lo, hi, g, qrow < a.Lq);
   }
 #ifdef TDG_STAMPS
   TDG_STAMP(3);
