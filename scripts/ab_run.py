@@ -20,7 +20,10 @@ for a in sys.argv[1:i]:
     mod, attr = name.rsplit(".", 1)
     m = importlib.import_module("tensorflow_distributed_on_gke_amd." + mod)
     old = getattr(m, attr)
-    setattr(m, attr, type(old)(int(val)) if isinstance(old, (bool, int)) else type(old)(val))
+    if isinstance(old, tuple):
+        setattr(m, attr, tuple(int(x) for x in val.split(",")))
+    else:
+        setattr(m, attr, type(old)(int(val)) if isinstance(old, (bool, int)) else type(old)(val))
     print(f"[ab_run] {name} = {getattr(m, attr)!r}", file=sys.stderr)
 sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[i + 1:]
 runpy.run_path(sys.argv[0], run_name="__main__")

@@ -8,9 +8,12 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 sys.path.insert(0, ROOT)
+if os.environ.get("TDG_PKG_ROOT"):  # A/B against another built copy of the package
+    sys.path.insert(0, os.path.abspath(os.environ["TDG_PKG_ROOT"]))
 from tensorflow_distributed_on_gke_amd.ops import fp8 as F  # noqa: E402
 from gemm_ceiling import graph_time  # noqa: E402
 
+print("package:", os.path.dirname(F.__file__), flush=True)
 torch.manual_seed(0)
 meta, gm = F.Fp8Meta("cuda"), F.Fp8Meta("cuda", fmt=1)
 ia, ib, io = meta.slot("a"), meta.slot("b"), meta.slot("o")
