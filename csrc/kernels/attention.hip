@@ -29,6 +29,7 @@
 namespace tdg {
 
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LOG2_448 = 8.807354922057604f;  // log2(448): the e4m3 P scale
 
 // v_exp_f32 as is: libm's exp2f wraps it in a denormal-range fix-up (compare,
 // select, ldexp: 4 more VALU per element); softmax weights below 2^-126
@@ -667,26 +668,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         const int ch = (2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1);
         vfr[s2][dt] = lds_read_tr8_async(ldsV + row * RB + 8 * ch);
       }
-    // P = exp2(c S - m) (f32 row sum), then e4m3(P * 448) in PV operand order
+    // P448 = 448 exp2(c S - m) = exp2(c S - m + log2 448) (f32 row sum l of
+    // P448), then e4m3(P448) in PV operand order: P <= 1 against the running
+    // max, so P448 <= 448 needs no clamp and the 448 costs no multiply
     const float cs = msk ? 1.f : c;
-    const float nm = m == -INFINITY ? 0.f : -m;
+    const float nm = (m == -INFINITY ? 0.f : -m) + LOG2_448;
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = fast_exp2(fmaf(s[t][r], cs, nm));
-        s[t][r] = p * 448.f;
-        rs += p;
+        s[t][r] = fast_exp2(fmaf(s[t][r], cs, nm));
+        rs += s[t][r];
       }
     l += rs;
     long pf[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      int lo = pack2_e4m3<false>(s[2 * s2][0], s[2 * s2][1], 0);
-      lo = pack2_e4m3<true>(s[2 * s2][2], s[2 * s2][3], lo);
-      int hi = pack2_e4m3<false>(s[2 * s2 + 1][0], s[2 * s2 + 1][1], 0);
-      hi = pack2_e4m3<true>(s[2 * s2 + 1][2], s[2 * s2 + 1][3], hi);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2][0], s[2 * s2][1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2][2], s[2 * s2][3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2 + 1][0], s[2 * s2 + 1][1], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2 + 1][2], s[2 * s2 + 1][3], hi, true);
       pf[s2] = (long)(uint32_t)lo | ((long)hi << 32);
     }
 #pragma unroll
@@ -705,7 +707,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   lu += __shfl_xor(lu, 16, 64);
   lu += __shfl_xor(lu, 32, 64);
   const bool valid = qrow < a.Lq;
-  const float inv = lu > 0.f ? 1.f / (lu * 448.f * a.sv8[0]) : 0.f;
+  const float inv = lu > 0.f ? 1.f / (lu * a.sv8[0]) : 0.f;  // (lu: the row sum of P448)
   const long long ooff = b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
   bf16_t* op = a.out + ooff;
   // e4m3 copy of O for the e4m3 output projection: from the bf16-rounded
@@ -741,7 +743,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int sh = 32; sh >= 1; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 64));
     if (lane == 0) atomic_amax(amax_word(a.amax8, blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z), am);
   }
-  if (valid && g == 0) a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + log2f(lu) : INFINITY;
+  if (valid && g == 0)
+    a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + (log2f(lu) - LOG2_448) : INFINITY;
 }
 
 // ============================================================================ dK, dV

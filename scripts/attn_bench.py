@@ -37,6 +37,11 @@ for causal in (False, True):
     tf = graph_time(lambda: kk.attn_fwd(q, k, v, kv, 0.125, causal))
     tb = graph_time(lambda: kk.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, kv, 0.125, causal))
     fl = 4.0 * B * H * L * L * hd * (0.5 if causal else 1.0)
+    if os.environ.get("ATTN_FP8") and kk.attn_fwd_fp8_ok(L, L, hd):
+        sc = torch.full((1,), 8.0, device="cuda")
+        q8, k8, v8 = ((x.float() * 8.0).to(torch.float8_e4m3fn) for x in (q, k, v))
+        t8 = graph_time(lambda: kk.attn_fwd_fp8(q8, k8, v8, sc, sc, sc, kv, 0.125, causal))
+        print(f"B={B} H={H} L={L} causal={causal}: e4m3 fwd {t8:.2f} us ({fl / t8 / 1e9:.3f} PF/s)", flush=True)
     print(f"B={B} H={H} L={L} causal={causal}: "
           f"fwd {tf:.2f} us ({fl / tf / 1e9:.3f} PF/s)  bwd {tb:.2f} us ({2.5 * fl / tb / 1e9:.3f} PF/s)",
           flush=True)
