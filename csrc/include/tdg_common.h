@@ -4,6 +4,7 @@
 // cores and the 64-bank LDS of gfx950. No portability layer: this is CDNA4 code.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <utility>
 #include <stdint.h>
 
 namespace tdg {
@@ -188,6 +189,33 @@ __device__ __forceinline__ long lds_read_b64_async(const void* p) {
   const uint32_t a = (uint32_t)(uintptr_t)p;
   asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(a) : "memory");
   return r;
+}
+// ... at a compile-time byte offset from a 32-bit LDS address (the DS
+// instruction's 16-bit offset field: no v_add per read for the constant part
+// of a fragment address)
+template <int OFF>
+__device__ __forceinline__ long lds_read_b64_at(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset field");
+  long r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ long lds_read_tr8_at(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset field");
+  long r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+// f(std::integral_constant<int, I>{}) for I = 0 .. N-1 (compile-time indices
+// for the offset-immediate reads)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 __device__ __forceinline__ long lds_read_tr8_async(const void* p) {
   long r;

@@ -616,6 +616,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   for (int s = 0; s < NS - 1; ++s) issue(s);
   wait_vmcnt_known<NS - 1>();
 
+  // lane parts of the fragment addresses (the swizzle term (row >> 2) & 3 is
+  // the same for every 16-row K tile t and both 32-row V halves s2)
+  uint32_t koff[2], voff[DT];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) koff[ks] = cl * RB + 8 * ((4 * ks + g) ^ (((cl >> 2) & 3) << 1));
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int row = 8 * g + (cl >> 1);
+    voff[dt] = row * RB + 8 * ((2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1));
+  }
   const float inv_qk = 1.f / (a.sq8[0] * a.sk8[0]);
   const float c = scl * LOG2E * inv_qk;
   const int wq0 = q0 + 16 * w;
@@ -627,19 +637,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     wait_tiles<1, NS - 2>(min(NS - 2, nkt - 1 - kt));
     lds_barrier();
     if (kt + NS - 1 < nkt) issue(kt + NS - 1);
-    const char* ldsK = smem + (kt % NS) * SLOT;
-    const char* ldsV = ldsK + TB;
+    const uint32_t slot = (uint32_t)(uintptr_t)smem + (uint32_t)((kt % NS) * SLOT);
     const int k0 = 64 * kt;
-    // S^T: K rows 16 t + cl, hd bytes 32 ks + 8 g (8-byte chunk 4 ks + g)
+    // S^T: K rows 16 t + cl, hd bytes 32 ks + 8 g (8-byte chunk 4 ks + g);
+    // lane part of the address koff[ks], the 16 t rows an immediate offset
     long kfr[NT16][2];
-#pragma unroll
-    for (int t = 0; t < NT16; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int row = 16 * t + cl;
-        const int ch = (4 * ks + g) ^ (((row >> 2) & 3) << 1);
-        kfr[t][ks] = lds_read_b64_async(ldsK + row * RB + 8 * ch);
-      }
+    const uint32_t ka0 = slot + koff[0], ka1 = slot + koff[1];
+    static_for<NT16>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      kfr[t][0] = lds_read_b64_at<16 * t * RB>(ka0);
+      kfr[t][1] = lds_read_b64_at<16 * t * RB>(ka1);
+    });
     f32x4 s[NT16];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -660,14 +668,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     // V^T fragments: lane pair (2 r8 + hh) of group g passes V row 32 s2 + 8 g + r8,
     // 8-byte chunk 2 dt + hh; lane i receives hd column 16 dt + i, keys 8 g .. +7
     long vfr[2][DT];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int row = 32 * s2 + 8 * g + (cl >> 1);
-        const int ch = (2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1);
-        vfr[s2][dt] = lds_read_tr8_async(ldsV + row * RB + 8 * ch);
-      }
+    static_for<DT>([&](auto dc) {
+      constexpr int dt = decltype(dc)::value;
+      const uint32_t va = slot + TB + voff[dt];
+      vfr[0][dt] = lds_read_tr8_at<0>(va);
+      vfr[1][dt] = lds_read_tr8_at<32 * RB>(va);
+    });
     // P448 = 448 exp2(c S - m) = exp2(c S - m + log2 448) (f32 row sum l of
     // P448), then e4m3(P448) in PV operand order: P <= 1 against the running
     // max, so P448 <= 448 needs no clamp and the 448 costs no multiply
