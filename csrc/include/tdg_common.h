@@ -207,6 +207,20 @@ __device__ __forceinline__ long lds_read_tr8_at(uint32_t a) {
   asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
   return r;
 }
+template <int OFF>
+__device__ __forceinline__ short8_t lds_read_b128_at(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset field");
+  short8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ short4_t lds_read_tr16_at(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset field");
+  short4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
 // f(std::integral_constant<int, I>{}) for I = 0 .. N-1 (compile-time indices
 // for the offset-immediate reads)
 template <class F, int... I>

@@ -171,6 +171,30 @@ struct ATile {
     const int c = 4 * s + (lane >> 4);
     return lds_read_b128_async(lds + off(row, c * 16));
   }
+  // Offset-immediate forms (tdg_common.h lds_read_*_at): the lane part of
+  // the address once per tile, the row base in the DS offset field.
+  // row_off: frag_row_async's lane part for row bases that are multiples of
+  // 8 (the swizzle term is then the lane's own); frag_row_at<RBASE>(tile
+  // address + row_off(s, lane)) == frag_row_async(tile, RBASE, s, lane).
+  __device__ static __forceinline__ uint32_t row_off(int s, int lane) {
+    return (uint32_t)off(lane & 15, (4 * s + (lane >> 4)) * 16);
+  }
+  template <int RBASE>
+  __device__ static __forceinline__ short8_t frag_row_at(uint32_t a) {
+    static_assert(RBASE % 8 == 0, "row base: multiple of 8");
+    return lds_read_b128_at<RBASE * RB>(a);
+  }
+  // tr_off: frag_tr_async's lane part (rows 4 g + q of k-step 0: the swizzle
+  // term is the same at + 16 and + 32 s2 rows)
+  __device__ static __forceinline__ uint32_t tr_off(int dt, int lane) {
+    const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+    return (uint32_t)off(4 * g + q, (16 * dt + 4 * p) * 2);
+  }
+  template <int S2>
+  __device__ static __forceinline__ void frag_tr_at(uint32_t a, short4_t& lo, short4_t& hi) {
+    lo = lds_read_tr16_at<32 * S2 * RB>(a);
+    hi = lds_read_tr16_at<(32 * S2 + 16) * RB>(a);
+  }
   // Transposed fragment, untracked, as its two 8-byte halves (tie both
   // after the wait, then cat4)
   __device__ static __forceinline__ void frag_tr_async(const char* lds, int s2, int dt, int lane,
@@ -1158,112 +1182,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   for (int s = 0; s < NS - 1; ++s) issue(s);
   wait_vmcnt_known<(NS - 1) * PT>();
 
+  uint32_t roff[T::KS], troff[T::DT];  // lane parts of the fragment addresses
+#pragma unroll
+  for (int ks = 0; ks < T::KS; ++ks) roff[ks] = T::row_off(ks, lane);
+#pragma unroll
+  for (int dt = 0; dt < T::DT; ++dt) troff[dt] = T::tr_off(dt, lane);
   for (int it = 0; it < nqt; ++it) {
     wait_tiles<PT, NS - 2>(min(NS - 2, nqt - 1 - it));
     lds_barrier();
     if (it + NS - 1 < nqt) issue(it + NS - 1);
-    const char* ldsQ = smem + (it % NS) * SLOT;
-    const char* ldsO = ldsQ + T::BYTES;
-    const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * T::BYTES);
-    const float* ldsD = ldsL + 64;
+    const uint32_t slotQ = (uint32_t)(uintptr_t)smem + (uint32_t)((it % NS) * SLOT);
+    const uint32_t slotO = slotQ + T::BYTES;
+    const char* ldsL = smem + (it % NS) * SLOT + 2 * T::BYTES;  // lse, then delta (64 floats each)
     const int q0 = qstart + 64 * it;
     // untracked LDS reads with counted waits (a tracked read would get a
     // vmcnt(0) for the DMA in flight); the next 16-query tile's Q / dO
-    // fragments and lse / delta are requested before this one is used
+    // fragments and lse / delta are requested before this one is used; row
+    // bases in the DS offset field
+    uint32_t qra[T::KS], ora[T::KS];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      qra[ks] = slotQ + roff[ks];
+      ora[ks] = slotO + roff[ks];
+    }
+    const uint32_t lda4 = (uint32_t)(uintptr_t)ldsL + 16 * g;
     short8_t pf[U][2], dsf[U][2];
     short8_t qfr[2][T::KS], ofr[2][T::KS];
     f32x4 l4[2], d4[2];
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) {
-      qfr[0][ks] = T::frag_row_async(ldsQ, 0, ks, lane);
-      ofr[0][ks] = T::frag_row_async(ldsO, 0, ks, lane);
+      qfr[0][ks] = T::template frag_row_at<0>(qra[ks]);
+      ofr[0][ks] = T::template frag_row_at<0>(ora[ks]);
     }
-    l4[0] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsL + 4 * g));
-    d4[0] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsD + 4 * g));
+    l4[0] = __builtin_bit_cast(f32x4, lds_read_b128_at<0>(lda4));
+    d4[0] = __builtin_bit_cast(f32x4, lds_read_b128_at<256>(lda4));
     constexpr int RPT = 2 * T::KS + 2;  // LDS reads per 16-query tile
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      f32x4 p[U][2], ds[U][2];
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * s2 + tt, cb = t & 1, nb = cb ^ 1;
-        if (t < 3) {
-#pragma unroll
-          for (int ks = 0; ks < T::KS; ++ks) {
-            qfr[nb][ks] = T::frag_row_async(ldsQ, 16 * (t + 1), ks, lane);
-            ofr[nb][ks] = T::frag_row_async(ldsO, 16 * (t + 1), ks, lane);
-          }
-          l4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsL + 16 * (t + 1) + 4 * g));
-          d4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_async(ldsD + 16 * (t + 1) + 4 * g));
-          lgkm_wait<RPT>();
-        } else {
-          lgkm_wait<0>();
-        }
+    f32x4 p[U][2], ds[U][2];
+    static_for<4>([&](auto tc) {
+      constexpr int t = decltype(tc)::value, tt = t & 1, s2 = t >> 1, cb = t & 1, nb = cb ^ 1;
+      if constexpr (t < 3) {
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
-          tie(qfr[cb][ks]);
-          tie(ofr[cb][ks]);
+          qfr[nb][ks] = T::template frag_row_at<16 * (t + 1)>(qra[ks]);
+          ofr[nb][ks] = T::template frag_row_at<16 * (t + 1)>(ora[ks]);
         }
-        tie(l4[cb]);
-        tie(d4[cb]);
-        f32x4 sv[U], dpv[U];
+        l4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_at<64 * (t + 1)>(lda4));
+        d4[nb] = __builtin_bit_cast(f32x4, lds_read_b128_at<256 + 64 * (t + 1)>(lda4));
+        lgkm_wait<RPT>();
+      } else {
+        lgkm_wait<0>();
+      }
 #pragma unroll
-        for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < T::KS; ++ks) {
+        tie(qfr[cb][ks]);
+        tie(ofr[cb][ks]);
+      }
+      tie(l4[cb]);
+      tie(d4[cb]);
+      f32x4 sv[U], dpv[U];
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) {
+      for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          sv[u] = mfma16(qfr[cb][ks], kf[u][ks], sv[u]);
+          dpv[u] = mfma16(ofr[cb][ks], vf[u][ks], dpv[u]);
+        }
+      }
+      // the whole 16-query subtile valid for every key of the wave (a
+      // wave-uniform test): no per-element masking
+      const int qs0 = q0 + 16 * t;
+      const bool full = kmaxw < klim && qs0 + 15 < a.Lq && (!causal || kmaxw <= qs0);
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            sv[u] = mfma16(qfr[cb][ks], kf[u][ks], sv[u]);
-            dpv[u] = mfma16(ofr[cb][ks], vf[u][ks], dpv[u]);
+            const float pv = fast_exp2(sv[u][r] * c - l4[cb][r]);
+            p[u][tt][r] = pv;
+            ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
           }
-        }
-        // the whole 16-query subtile valid for every key of the wave (a
-        // wave-uniform test): no per-element masking
-        const int qs0 = q0 + 16 * t;
-        const bool full = kmaxw < klim && qs0 + 15 < a.Lq && (!causal || kmaxw <= qs0);
-        if (full) {
+      } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 4; ++r) {
+          const int q = qs0 + 4 * g + r;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const float pv = fast_exp2(sv[u][r] * c - l4[cb][r]);
-              p[u][tt][r] = pv;
-              ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
-            }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = qs0 + 4 * g + r;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
-              const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
-              p[u][tt][r] = pv;
-              ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
-            }
+          for (int u = 0; u < U; ++u) {
+            const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
+            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
+            p[u][tt][r] = pv;
+            ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
           }
         }
       }
+      if constexpr (tt == 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        pf[u][s2] = pack8(p[u][0][0], p[u][0][1], p[u][0][2], p[u][0][3], p[u][1][0], p[u][1][1],
-                          p[u][1][2], p[u][1][3]);
-        dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
-                           ds[u][1][1], ds[u][1][2], ds[u][1][3]);
+        for (int u = 0; u < U; ++u) {
+          pf[u][s2] = pack8(p[u][0][0], p[u][0][1], p[u][0][2], p[u][0][3], p[u][1][0], p[u][1][1],
+                            p[u][1][2], p[u][1][3]);
+          dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                             ds[u][1][1], ds[u][1][2], ds[u][1][3]);
+        }
       }
-    }
+    });
     // dV^T += dO^T P, dK^T += Q^T dS: transposed fragments, next requested
     // before this one is used
-    short4_t olo[2], ohi[2], qlo[2], qhi[2];
-    T::frag_tr_async(ldsO, 0, 0, lane, olo[0], ohi[0]);
-    T::frag_tr_async(ldsQ, 0, 0, lane, qlo[0], qhi[0]);
+    uint32_t otra[T::DT], qtra[T::DT];
 #pragma unroll
-    for (int i = 0; i < 2 * T::DT; ++i) {
-      const int s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
-      if (i + 1 < 2 * T::DT) {
-        const int s2n = (i + 1) / T::DT, dtn = (i + 1) % T::DT;
-        T::frag_tr_async(ldsO, s2n, dtn, lane, olo[nb], ohi[nb]);
-        T::frag_tr_async(ldsQ, s2n, dtn, lane, qlo[nb], qhi[nb]);
+    for (int dt = 0; dt < T::DT; ++dt) {
+      otra[dt] = slotO + troff[dt];
+      qtra[dt] = slotQ + troff[dt];
+    }
+    short4_t olo[2], ohi[2], qlo[2], qhi[2];
+    T::template frag_tr_at<0>(otra[0], olo[0], ohi[0]);
+    T::template frag_tr_at<0>(qtra[0], qlo[0], qhi[0]);
+    static_for<2 * T::DT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
+      if constexpr (i + 1 < 2 * T::DT) {
+        T::template frag_tr_at<(i + 1) / T::DT>(otra[(i + 1) % T::DT], olo[nb], ohi[nb]);
+        T::template frag_tr_at<(i + 1) / T::DT>(qtra[(i + 1) % T::DT], qlo[nb], qhi[nb]);
         lgkm_wait<4>();
       } else {
         lgkm_wait<0>();
@@ -1279,7 +1317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         dv[u][dt] = mfma16(ot, pf[u][s2], dv[u][dt]);
         dk[u][dt] = mfma16(qt, dsf[u][s2], dk[u][dt]);
       }
-    }
+    });
   }
   wait_vmcnt<0>();
   if (!a.skip_bf16) {
@@ -1385,91 +1423,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int i = 0; i < T::DT; ++i) dq[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t roff[T::KS], troff[T::DT];  // lane parts of the fragment addresses
+#pragma unroll
+  for (int ks = 0; ks < T::KS; ++ks) roff[ks] = T::row_off(ks, lane);
+#pragma unroll
+  for (int dt = 0; dt < T::DT; ++dt) troff[dt] = T::tr_off(dt, lane);
 
   for (int kt = 0; kt < nkt; ++kt) {
     wait_tiles<PT, NS - 2>(min(NS - 2, nkt - 1 - kt));
     lds_barrier();
     if (kt + NS - 1 < nkt) issue(kt + NS - 1);
-    const char* ldsK = smem + (kt % NS) * SLOT;
-    const char* ldsV = ldsK + T::BYTES;
+    const uint32_t slotK = (uint32_t)(uintptr_t)smem + (uint32_t)((kt % NS) * SLOT);
+    const uint32_t slotV = slotK + T::BYTES;
     const int k0 = 64 * kt;
     // untracked LDS reads with counted waits, next 16-key tile requested
-    // before this one is used
+    // before this one is used; row bases in the DS offset field
+    uint32_t kra[T::KS], vra[T::KS];
+#pragma unroll
+    for (int ks = 0; ks < T::KS; ++ks) {
+      kra[ks] = slotK + roff[ks];
+      vra[ks] = slotV + roff[ks];
+    }
     short8_t dsf[U][2];
     short8_t kfr[2][T::KS], vfr[2][T::KS];
 #pragma unroll
     for (int ks = 0; ks < T::KS; ++ks) {
-      kfr[0][ks] = T::frag_row_async(ldsK, 0, ks, lane);
-      vfr[0][ks] = T::frag_row_async(ldsV, 0, ks, lane);
+      kfr[0][ks] = T::template frag_row_at<0>(kra[ks]);
+      vfr[0][ks] = T::template frag_row_at<0>(vra[ks]);
     }
     constexpr int RPT = 2 * T::KS;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      f32x4 ds[U][2];
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * s2 + tt, cb = t & 1, nb = cb ^ 1;
-        if (t < 3) {
-#pragma unroll
-          for (int ks = 0; ks < T::KS; ++ks) {
-            kfr[nb][ks] = T::frag_row_async(ldsK, 16 * (t + 1), ks, lane);
-            vfr[nb][ks] = T::frag_row_async(ldsV, 16 * (t + 1), ks, lane);
-          }
-          lgkm_wait<RPT>();
-        } else {
-          lgkm_wait<0>();
-        }
+    f32x4 ds[U][2];
+    static_for<4>([&](auto tc) {
+      constexpr int t = decltype(tc)::value, tt = t & 1, s2 = t >> 1, cb = t & 1, nb = cb ^ 1;
+      if constexpr (t < 3) {
 #pragma unroll
         for (int ks = 0; ks < T::KS; ++ks) {
-          tie(kfr[cb][ks]);
-          tie(vfr[cb][ks]);
+          kfr[nb][ks] = T::template frag_row_at<16 * (t + 1)>(kra[ks]);
+          vfr[nb][ks] = T::template frag_row_at<16 * (t + 1)>(vra[ks]);
         }
-        f32x4 sv[U], dpv[U];
+        lgkm_wait<RPT>();
+      } else {
+        lgkm_wait<0>();
+      }
 #pragma unroll
-        for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < T::KS; ++ks) {
+        tie(kfr[cb][ks]);
+        tie(vfr[cb][ks]);
+      }
+      f32x4 sv[U], dpv[U];
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) {
+      for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          sv[u] = mfma16(kfr[cb][ks], qf[u][ks], sv[u]);
+          dpv[u] = mfma16(vfr[cb][ks], of[u][ks], dpv[u]);
+        }
+      }
+      // the whole 16-key subtile valid for every query of the wave (a
+      // wave-uniform test): no per-element masking
+      const int ks0 = k0 + 16 * t;
+      const bool full = qminw + 16 * U <= a.Lq && ks0 + 15 < klim && (!causal || ks0 + 15 <= qminw);
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            ds[u][tt][r] = fast_exp2(sv[u][r] * c - L[u]) * (dpv[u][r] - D[u]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = ks0 + 4 * g + r;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            sv[u] = mfma16(kfr[cb][ks], qf[u][ks], sv[u]);
-            dpv[u] = mfma16(vfr[cb][ks], of[u][ks], dpv[u]);
-          }
-        }
-        // the whole 16-key subtile valid for every query of the wave (a
-        // wave-uniform test): no per-element masking
-        const int ks0 = k0 + 16 * t;
-        const bool full = qminw + 16 * U <= a.Lq && ks0 + 15 < klim && (!causal || ks0 + 15 <= qminw);
-        if (full) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-              ds[u][tt][r] = fast_exp2(sv[u][r] * c - L[u]) * (dpv[u][r] - D[u]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = ks0 + 4 * g + r;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
-              const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
-              ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
-            }
+            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
+            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+            ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
           }
         }
       }
+      if constexpr (tt == 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
-                           ds[u][1][1], ds[u][1][2], ds[u][1][3]);
-    }
+        for (int u = 0; u < U; ++u)
+          dsf[u][s2] = pack8(ds[u][0][0], ds[u][0][1], ds[u][0][2], ds[u][0][3], ds[u][1][0],
+                             ds[u][1][1], ds[u][1][2], ds[u][1][3]);
+      }
+    });
+    uint32_t ktra[T::DT];
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) ktra[dt] = slotK + troff[dt];
     short4_t klo[2], khi[2];
-    T::frag_tr_async(ldsK, 0, 0, lane, klo[0], khi[0]);
-#pragma unroll
-    for (int i = 0; i < 2 * T::DT; ++i) {
-      const int s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
-      if (i + 1 < 2 * T::DT) {
-        T::frag_tr_async(ldsK, (i + 1) / T::DT, (i + 1) % T::DT, lane, klo[nb], khi[nb]);
+    T::template frag_tr_at<0>(ktra[0], klo[0], khi[0]);
+    static_for<2 * T::DT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, s2 = i / T::DT, dt = i % T::DT, cb = i & 1, nb = cb ^ 1;
+      if constexpr (i + 1 < 2 * T::DT) {
+        T::template frag_tr_at<(i + 1) / T::DT>(ktra[(i + 1) % T::DT], klo[nb], khi[nb]);
         lgkm_wait<2>();
       } else {
         lgkm_wait<0>();
@@ -1479,7 +1528,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       const short8_t kt2 = cat4(klo[cb], khi[cb]);
 #pragma unroll
       for (int u = 0; u < U; ++u) dq[u][dt] = mfma16(kt2, dsf[u][s2], dq[u][dt]);
-    }
+    });
   }
   wait_vmcnt<0>();
   if (!a.skip_bf16) {
