@@ -35,6 +35,15 @@ constexpr float LOG2_448 = 8.807354922057604f;  // log2(448): the e4m3 P scale
 // select, ldexp: 4 more VALU per element); softmax weights below 2^-126
 // flushed to zero change nothing at bf16 P.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// ok ? exp2(x) : 0 as a select: exp2 computed for every lane (x is finite or
+// -inf on the masked side, never NaN). Written as the conditional expression,
+// the compiler branched around each element's exp (exec-mask save / restore,
+// ~10 instructions per element on every masked tile).
+__device__ __forceinline__ float masked_exp2(float x, bool ok) {
+  float e = fast_exp2(x);
+  asm volatile("" : "+v"(e));
+  return ok ? e : 0.f;
+}
 
 // Row-per-lane store of a 16x16-MFMA output row: lane (g, cl) holds columns
 // 16 dt + 4 g .. +3 (dt < DT) of its row as packed bf16 pairs lo[dt] / hi[dt].
@@ -789,7 +798,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   char* ldsO = smem + T::BYTES;  // dO tile
   float* ldsL = reinterpret_cast<float*>(smem + 2 * T::BYTES);
   float* ldsD = ldsL + QB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KBW;
   int key[U];
 #pragma unroll
@@ -875,8 +885,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
             const float lq = ldsL[ql], dq = ldsD[ql];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
-              const float pv = ok ? fast_exp2(sv[u][r] * c - lq) : 0.f;
+              const bool ok = (key[u] < klim) & (q < a.Lq) & (!causal | (key[u] <= q));  // (no short circuit: no branches)
+              const float pv = masked_exp2(sv[u][r] * c - lq, ok);
               p[u][tt][r] = pv;
               ds[u][tt][r] = pv * (dpv[u][r] - dq);
             }
@@ -931,7 +941,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
   char* ldsV = smem + T::BYTES;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
   int qrow[U];
 #pragma unroll
@@ -1021,8 +1032,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           const int key = k0 + 16 * t + 4 * g + r;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+            const bool ok = (qrow[u] < a.Lq) & (key < klim) & (!causal | (key <= qrow[u]));  // (no short circuit)
+            const float pv = masked_exp2(sv[u][r] * c - L[u], ok);
             ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
           }
         }
@@ -1269,8 +1280,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           const int q = qs0 + 4 * g + r;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const bool ok = key[u] < klim && q < a.Lq && (!causal || key[u] <= q);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - l4[cb][r]) : 0.f;
+            const bool ok = (key[u] < klim) & (q < a.Lq) & (!causal | (key[u] <= q));  // (no short circuit: no branches)
+            const float pv = masked_exp2(sv[u][r] * c - l4[cb][r], ok);
             p[u][tt][r] = pv;
             ds[u][tt][r] = pv * (dpv[u][r] - d4[cb][r]);
           }
@@ -1497,8 +1508,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           const int key = ks0 + 4 * g + r;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const bool ok = qrow[u] < a.Lq && key < klim && (!causal || key <= qrow[u]);
-            const float pv = ok ? fast_exp2(sv[u][r] * c - L[u]) : 0.f;
+            const bool ok = (qrow[u] < a.Lq) & (key < klim) & (!causal | (key <= qrow[u]));  // (no short circuit)
+            const float pv = masked_exp2(sv[u][r] * c - L[u], ok);
             ds[u][tt][r] = pv * (dpv[u][r] - D[u]);
           }
         }
@@ -1580,7 +1591,8 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
   char* ldsS = ALIAS ? smem : smem + 3 * TB;
   float* ldsL = reinterpret_cast<float*>(smem + (ALIAS ? 3 * TB : 3 * TB + SB));
   float* ldsD = ldsL + R;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh % a.H;
   int klim;
@@ -1667,20 +1679,23 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
   if (active) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
+      const bool live = 16 * t < a.Lq && (!causal || 16 * t + 15 >= 16 * U * w);  // uniform
+      if (!live) {  // (no query of the tile attends to the wave's keys: P = dS = 0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) pk[u][t][0] = pk[u][t][1] = dk2[u][t][0] = dk2[u][t][1] = 0u;
+        continue;
+      }
       f32x4 sv[U], dpv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) sv[u] = dpv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool live = 16 * t < a.Lq && (!causal || 16 * t + 15 >= 16 * U * w);  // uniform
-      if (live) {
 #pragma unroll
-        for (int ks = 0; ks < T::KS; ++ks) {
-          const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
-          const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
+      for (int ks = 0; ks < T::KS; ++ks) {
+        const short8_t qfr = T::frag_row(ldsQ, 16 * t, ks, lane);
+        const short8_t ofr = T::frag_row(ldsO, 16 * t, ks, lane);
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
-            dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
-          }
+        for (int u = 0; u < U; ++u) {
+          sv[u] = mfma16(qfr, kf[u][ks], sv[u]);
+          dpv[u] = mfma16(ofr, vf[u][ks], dpv[u]);
         }
       }
       // lse / delta of queries 16t + 4g .. +3: one 16-byte LDS read each
@@ -1688,8 +1703,8 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 16 * t + 4 * g);
       // every (query, key) of this 16-query tile valid for the wave's keys
       // (wave-uniform): no per-element masks
-      const int kmaxw = 16 * U * (__builtin_amdgcn_readfirstlane(w) + 1) - 1;
-      const bool full = live && kmaxw < klim && 16 * t + 15 < a.Lq && (!causal || kmaxw <= 16 * t);
+      const int kmaxw = 16 * U * (w + 1) - 1;
+      const bool full = kmaxw < klim && 16 * t + 15 < a.Lq && (!causal || kmaxw <= 16 * t);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         float pv[4], dv4[4];
@@ -1704,8 +1719,8 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = 16 * t + 4 * g + r;
-            const bool ok = live && kvalid && q < a.Lq && (!causal || key[u] <= q);
-            pv[r] = ok ? fast_exp2(sv[u][r] * c - l4[r]) : 0.f;
+            const bool ok = kvalid & (q < a.Lq) & (!causal | (key[u] <= q));  // (no short circuit: no branches)
+            pv[r] = masked_exp2(sv[u][r] * c - l4[r], ok);
             dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
           }
         }
