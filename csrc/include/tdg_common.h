@@ -50,6 +50,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
+// Two floats -> one packed bf16 pair (lo = a) in ONE v_cvt_pk_bf16_f32; the
+// `f2bf(a) | f2bf(b) << 16` form converts each alone and then shifts and ors
+// (4 instructions per pair).
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------- reductions

@@ -49,7 +49,7 @@ struct RowVec {
   __device__ __forceinline__ void store_row(bf16_t* row, int lane, const WtBuf& wt) const {
     bf16_t* p = row + lane * Map::W;
     if constexpr (VEC == 2) {
-      wt.st4(p, (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16));
+      wt.st4(p, pack2bf(v[0], v[1]));
     } else if constexpr (VEC == 4) {
       short4_t w;
 #pragma unroll
@@ -68,7 +68,7 @@ struct RowVec {
   __device__ __forceinline__ void store_row(bf16_t* row, int lane) const {
     bf16_t* p = row + lane * Map::W;
     if constexpr (VEC == 2) {
-      *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      *reinterpret_cast<uint32_t*>(p) = pack2bf(v[0], v[1]);
     } else if constexpr (VEC == 4) {
       short4_t w;
 #pragma unroll

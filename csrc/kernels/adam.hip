@@ -69,8 +69,8 @@ __device__ __forceinline__ void adam_store(const AdamOut& o, float4* P4, float4*
   o.v.st16(V4 + i, vv);
   if (zero_grad) G4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (S2) {
-    const uint32_t lo = (uint32_t)f2bf(pp.x) | ((uint32_t)f2bf(pp.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(pp.z) | ((uint32_t)f2bf(pp.w) << 16);
+    const uint32_t lo = pack2bf(pp.x, pp.y);
+    const uint32_t hi = pack2bf(pp.z, pp.w);
     o.s.st8(S2 + i, make_uint2(lo, hi));
   }
 }

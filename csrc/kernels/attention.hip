@@ -73,8 +73,8 @@ __device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint
 }
 // (the packing of an accumulator: 4 values, times sc)
 __device__ __forceinline__ void pack_acc(const f32x4& v, float sc, uint32_t& lo, uint32_t& hi) {
-  lo = (uint32_t)f2bf(v[0] * sc) | ((uint32_t)f2bf(v[1] * sc) << 16);
-  hi = (uint32_t)f2bf(v[2] * sc) | ((uint32_t)f2bf(v[3] * sc) << 16);
+  lo = pack2bf(v[0] * sc, v[1] * sc);
+  hi = pack2bf(v[2] * sc, v[3] * sc);
 }
 
 // Key window and logit scale of batch row b. A row with NO valid key
@@ -1724,10 +1724,10 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
             dv4[r] = pv[r] * (dpv[u][r] - d4[r]);
           }
         }
-        pk[u][t][0] = (uint32_t)f2bf(pv[0]) | ((uint32_t)f2bf(pv[1]) << 16);
-        pk[u][t][1] = (uint32_t)f2bf(pv[2]) | ((uint32_t)f2bf(pv[3]) << 16);
-        dk2[u][t][0] = (uint32_t)f2bf(dv4[0]) | ((uint32_t)f2bf(dv4[1]) << 16);
-        dk2[u][t][1] = (uint32_t)f2bf(dv4[2]) | ((uint32_t)f2bf(dv4[3]) << 16);
+        pk[u][t][0] = pack2bf(pv[0], pv[1]);
+        pk[u][t][1] = pack2bf(pv[2], pv[3]);
+        dk2[u][t][0] = pack2bf(dv4[0], dv4[1]);
+        dk2[u][t][1] = pack2bf(dv4[2], dv4[3]);
       }
     }
 #pragma unroll

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void xent_kernel(bf16_t* __restrict__ logits, 
       }
     }
     if (c + 1 < ldl) {
-      *reinterpret_cast<uint32_t*>(x + c) = (uint32_t)f2bf(g0) | ((uint32_t)f2bf(g1) << 16);
+      *reinterpret_cast<uint32_t*>(x + c) = pack2bf(g0, g1);
     } else {
       x[c] = f2bf(g0);
     }
