@@ -421,13 +421,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
   };
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue_half(0, h);
-  for (int kt = 0; kt < nk; ++kt) {
+  // MORE: K-tile kt + 1 exists (steady state, branch-free); the last tile is
+  // its own instantiation (tail branches inside one loop body invite the
+  // compiler to move MFMAs out of their phases: docs/PERF.md "Round 4")
+  auto kstep = [&](int kt, auto morec) {
+    constexpr bool more = decltype(morec)::value;
     const char* st = smem + (kt & 1) * SB;
-    const bool more = kt + 1 < nk;
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
       if (ph < 3) {
-        if (more) wait_vmcnt<4>();
+        if constexpr (more) wait_vmcnt<4>();
         else wait_vmcnt<0>();
         lds_barrier();
         if (kt == 0 && ph == 0) TDG_STAMP(1);
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
       }
-      if (more) issue_half(kt + 1, ph);
+      if constexpr (more) issue_half(kt + 1, ph);
       // this phase's fragment reads (untracked transposing reads included)
       if (ph < 3) {
         lgkm_wait<0>();
@@ -485,7 +488,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
       // to scratch
       if (do_bsum && (ph == 0 || ph == 2)) bias_sum(ph);
     }
-  }
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; ++kt) kstep(kt, std::true_type{});
+  kstep(kt, std::false_type{});
   if (do_bsum) {  // lanes l, l+16, l+32, l+48 hold disjoint K subsets of row l&15
     bsum0 += __shfl_xor(bsum0, 16, 64);
     bsum0 += __shfl_xor(bsum0, 32, 64);
