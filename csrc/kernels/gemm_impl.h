@@ -175,7 +175,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 
   // LDS instructions of one k-step's fragment reads (for the counted waits)
   constexpr int STEP_OPS = TM * frag_ops<A_KC>() + TN * frag_ops<B_KC>();
-  for (int kt = 0; kt < nk; ++kt) {
+  // MODE 3: steady state (tile kt + STAGES exists: refill, counted wait);
+  // 2: tile kt + STAGES - 1 is the last one (counted wait, no refill);
+  // 1: drain (wait for everything); 0: the last tile. Branch-free steady
+  // state, the tail steps their own instantiations (docs/PERF.md "Round 4").
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
     const char* st = smem + (kt % STAGES) * SB;
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa1[i] = frag<A_KC, BM>(st, abase + 16 * i, 1, lane);
@@ -191,21 +196,21 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb0[j], fa0[i], acc[i][j]);
     prio_lo();
-    if (kt + 1 < nk) {
+    if constexpr (MODE >= 1) {
       // tile kt+1 landed (this wave's DMA), then everyone's; everyone is done
       // reading tile kt (its fragments are in registers)
-      if (kt + STAGES - 1 < nk)
-        wait_vmcnt<(STAGES - 2) * PT>();
-      else
-        wait_vmcnt<0>();
+      if constexpr (MODE >= 2) wait_vmcnt<(STAGES - 2) * PT>();
+      else wait_vmcnt<0>();
       lds_barrier();
       const char* nx = smem + ((kt + 1) % STAGES) * SB;
-      if (ktail && kt + 1 == nk - 1) {
-        GA::zero_ktail(const_cast<char*>(nx), kb + (kt + 1) * BK, ke, tid, NT);
-        GB::zero_ktail(const_cast<char*>(nx) + A_BYTES, kb + (kt + 1) * BK, ke, tid, NT);
-        lds_barrier();
+      if constexpr (MODE <= 2) {  // (a K tail is only ever the last tile)
+        if (ktail && kt + 1 == nk - 1) {
+          GA::zero_ktail(const_cast<char*>(nx), kb + (kt + 1) * BK, ke, tid, NT);
+          GB::zero_ktail(const_cast<char*>(nx) + A_BYTES, kb + (kt + 1) * BK, ke, tid, NT);
+          lds_barrier();
+        }
       }
-      if (kt + STAGES < nk) {
+      if constexpr (MODE == 3) {
         char* ns = smem + (kt % STAGES) * SB;
         ga.issue(A, lda, M, ke, m0, kb + (kt + STAGES) * BK, ns, wid);
         gb.issue(B, ldb, N, ke, n0, kb + (kt + STAGES) * BK, ns + A_BYTES, wid);
@@ -226,6 +231,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
     prio_lo();
+  };
+  {
+    int kt = 0;
+    for (; kt + STAGES < nk; ++kt) kstep(kt, std::integral_constant<int, 3>{});
+    if (kt + STAGES - 1 < nk && kt + 1 < nk) kstep(kt++, std::integral_constant<int, 2>{});
+    for (; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<int, 1>{});
+    if (kt < nk) kstep(kt, std::integral_constant<int, 0>{});
   }
 
   TDG_STAMP(2);
