@@ -201,27 +201,40 @@ struct Pipe {
     float none[TM];
     ktile_bs<false>(kt, nk, FB, FN, fa, acc, sa, sb, smem, lane, wid, abase, bbase, none, false);
   }
+  // steady-state tile (1 <= kt <= nk - NS: the next tile exists, a tile is
+  // refilled, NS - 3 tiles stay in flight): no runtime tail tests in the
+  // body (docs/PERF.md "Round 4": tail branches inside the loop body)
+  static __device__ __forceinline__ void ktile_s(int kt, int nk, FBt (&FB)[TN],
+                                                 FBt (&FN)[TN], FA (&fa)[TM],
+                                                 f32x4 (&acc)[TM][TN], const SA& sa, const SBt& sb,
+                                                 char* smem, int lane, int wid, int abase,
+                                                 int bbase) {
+    float none[TM];
+    ktile_bs<false, true>(kt, nk, FB, FN, fa, acc, sa, sb, smem, lane, wid, abase, bbase, none,
+                          false);
+  }
   // BS: also accumulate the sums over k of the A fragments (bs[i]: row
   // abase + 16 i + (lane & 15), this lane's k subset) when do_bs -- the fused
   // bias gradient of a weight-gradient tile (A = dY^T), from registers the
   // MFMAs already hold
-  template <bool BS>
+  template <bool BS, bool STEADY = false>
   static __device__ __forceinline__ void ktile_bs(int kt, int nk, FBt (&FB)[TN],
                                                   FBt (&FN)[TN], FA (&fa)[TM],
                                                   f32x4 (&acc)[TM][TN], const SA& sa,
                                                   const SBt& sb, char* smem, int lane, int wid,
                                                   int abase, int bbase, float (&bs)[TM],
                                                   bool do_bs) {
-    if (kt + 1 < nk) {
+    if (STEADY || kt + 1 < nk) {
       // tile kt+1 landed (this wave's pieces), then everyone's; every wave
       // also finished reading tile kt-1, whose slot is refilled below.
       // In flight after kt+1: tiles up to kt+NS-2 (kt = 0: NS-1)
-      wait_tiles<PT, NS - 2>(kt == 0 ? min(NS - 2, nk - 2) : min(NS - 3, nk - 2 - kt));
+      if constexpr (STEADY) wait_vmcnt<(NS - 3) * PT>();
+      else wait_tiles<PT, NS - 2>(kt == 0 ? min(NS - 2, nk - 2) : min(NS - 3, nk - 2 - kt));
       __builtin_amdgcn_s_barrier();
     }
     const char* nx = smem + ((kt + 1) % NS) * SB;
     const int rt = kt - 1 + NS;  // tile refilled into tile kt-1's slot
-    const bool refill = rt < nk && kt >= 1;
+    const bool refill = STEADY || (rt < nk && kt >= 1);
     // (the next tile's fragments are read unconditionally -- after the last
     // tile from a stale slot, never used -- so the compiler's lgkmcnt
     // bookkeeping stays exact: no branch around an LDS read)
@@ -324,12 +337,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pipe_kernel(
 
   // kt = 0 refills nothing (tile NS-1's slot was never used): issue it now
   if (NS - 1 < nk) P::stage(sa, sb, smem, NS - 1, wid);
+  // tile 0, then steady-state pairs (odd kt: B fragments in fbn), then the
+  // tail tiles with their runtime tests
   int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    P::ktile(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
-    P::ktile(kt + 1, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+  if (nk > 0) P::ktile(kt++, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+  for (; kt + 1 <= nk - NS; kt += 2) {
+    P::ktile_s(kt, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+    P::ktile_s(kt + 1, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
   }
-  if (kt < nk) P::ktile(kt, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+  for (; kt + 1 < nk; kt += 2) {
+    P::ktile(kt, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+    P::ktile(kt + 1, nk, fb, fbn, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
+  }
+  if (kt < nk) P::ktile(kt, nk, fbn, fb, fa, acc, sa, sb, smem, lane, wid, abase, bbase);
 
   // ---------------- epilogue: per-wave LDS image over the pipeline stages
   // (the last tile's next-fragment reads, from a stale slot, are drained here)
