@@ -77,6 +77,14 @@ __device__ __forceinline__ void pack_acc(const f32x4& v, float sc, uint32_t& lo,
   hi = pack2bf(v[2] * sc, v[3] * sc);
 }
 
+// 16-byte global load from an always-valid (clamped) address, zero where
+// !ok: a select instead of an exec-mask branch around every prologue load
+__device__ __forceinline__ short8_t ld8_or0(const bf16_t* p, bool ok) {
+  const short8_t v = *reinterpret_cast<const short8_t*>(p);
+  const short8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return ok ? v : z;
+}
+
 // Key window and logit scale of batch row b. A row with NO valid key
 // (kv_len == 0: an all-PAD sequence) gets the reference's numerics: its
 // padding mask adds -1e9 to every logit, which in fp32 leaves them all equal
@@ -135,9 +143,14 @@ struct ATile {
     for (int i = 0; i < C::NI; ++i) {
       const int id = tid + i * NT;
       const int row = id / C::CPR, cc = id % C::CPR;
-      c.v[i] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      if ((C::TOTAL % NT == 0 || id < C::TOTAL) && row0 + row < nrows)
-        c.v[i] = *reinterpret_cast<const short8_t*>(base + (long long)(row0 + row) * sl + cc * 8);
+      if constexpr (C::TOTAL % NT == 0) {  // (rows past nrows: clamped load, zeroed)
+        const int r = min(row0 + row, nrows - 1);
+        c.v[i] = ld8_or0(base + (long long)r * sl + cc * 8, row0 + row < nrows);
+      } else {
+        c.v[i] = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        if (id < C::TOTAL && row0 + row < nrows)
+          c.v[i] = *reinterpret_cast<const short8_t*>(base + (long long)(row0 + row) * sl + cc * 8);
+      }
     }
   }
   template <int NT = 256>
@@ -231,9 +244,13 @@ template <int HD>
 __device__ __forceinline__ short8_t gfrag(const bf16_t* __restrict__ rowp, bool valid, int s,
                                           int lane) {
   const int c = 4 * s + (lane >> 4);
-  short8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (valid && c < HD / 8) v = *reinterpret_cast<const short8_t*>(rowp + c * 8);
-  return v;
+  if constexpr (HD >= 64) {  // (c < HD / 8 always; rowp is a clamped, valid row)
+    return ld8_or0(rowp + c * 8, valid);
+  } else {
+    short8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid && c < HD / 8) v = *reinterpret_cast<const short8_t*>(rowp + c * 8);
+    return v;
+  }
 }
 
 
@@ -1635,13 +1652,21 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
       const int id = tid + i * NT;
       const int row = id / CPR, cc = id % CPR;
       vq[i] = vo[i] = vk[i] = vx[i] = z;
-      if (id < TOTAL && row < a.Lq) {
-        vq[i] = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
-        vo[i] = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
-        vx[i] = *reinterpret_cast<const short8_t*>(obo + (long long)row * a.o_sl + cc * 8);
+      if constexpr (TOTAL % NT == 0) {  // (clamped rows, zeroed: no branch per load)
+        const int rq = min(row, a.Lq - 1), rk = min(row, a.Lk - 1);
+        vq[i] = ld8_or0(qb + (long long)rq * a.q_sl + cc * 8, row < a.Lq);
+        vo[i] = ld8_or0(ob + (long long)rq * a.do_sl + cc * 8, row < a.Lq);
+        vx[i] = ld8_or0(obo + (long long)rq * a.o_sl + cc * 8, row < a.Lq);
+        vk[i] = ld8_or0(kbp + (long long)rk * a.k_sl + cc * 8, row < a.Lk);
+      } else {
+        if (id < TOTAL && row < a.Lq) {
+          vq[i] = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
+          vo[i] = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
+          vx[i] = *reinterpret_cast<const short8_t*>(obo + (long long)row * a.o_sl + cc * 8);
+        }
+        if (id < TOTAL && row < a.Lk)
+          vk[i] = *reinterpret_cast<const short8_t*>(kbp + (long long)row * a.k_sl + cc * 8);
       }
-      if (id < TOTAL && row < a.Lk)
-        vk[i] = *reinterpret_cast<const short8_t*>(kbp + (long long)row * a.k_sl + cc * 8);
     }
     const float lse_v = (tid < R && tid < a.Lq) ? a.lse[((long long)b * a.H + h) * a.Lq + tid] : INFINITY;
 #pragma unroll
