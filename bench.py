@@ -39,6 +39,33 @@ METRIC = "tokens/sec (whole node), Transformer-base en-pt at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
 
 
+def visible_gpus() -> int:
+    """GPUs this process could use, counted WITHOUT initialising HIP (the
+    launcher parent must not touch the GPU): the visible-devices lists if set,
+    else the GPU nodes of the KFD topology (nodes with SIMDs)."""
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() and x.strip() != "-1"])
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return 0
+    for node in nodes:
+        try:
+            with open(os.path.join(base, node, "properties")) as f:
+                for line in f:
+                    k, _, val = line.partition(" ")
+                    if k == "simd_count" and int(val) > 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
 def self_launch(n: int) -> int:
     """Spawn `n` ranks of this script (one per GPU) and return their exit code.
 
@@ -53,7 +80,7 @@ def self_launch(n: int) -> int:
 
     from tensorflow_distributed_on_gke_amd.cluster import launch, rendezvous
 
-    ngpu = torch.cuda.device_count()
+    ngpu = visible_gpus()
     if 0 < ngpu < n and os.environ.get("TDG_DIST_BACKEND") != "gloo":
         print(f"bench.py: --gpus {n} requested but only {ngpu} GPU(s) are visible; refusing to "
               f"measure fewer ranks (set TDG_DIST_BACKEND=gloo for a shared-GPU rehearsal)",
@@ -63,7 +90,15 @@ def self_launch(n: int) -> int:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     spec = rendezvous.ClusterSpec(0, 1, ["127.0.0.1"], "127.0.0.1", port)
+    # the parent never initialises HIP: the ranks are fresh child processes
+    # that each bind their own GPU
+    assert not torch.cuda.is_initialized(), "bench.py launcher must not initialise HIP"
     return launch.launch([os.path.abspath(__file__)] + sys.argv[1:], n, spec)
+
+
+def _fp8_precision() -> str:
+    from tensorflow_distributed_on_gke_amd.ops.fp8 import precision_string
+    return precision_string()
 
 
 def main() -> None:
@@ -83,9 +118,10 @@ def main() -> None:
     ap.add_argument("--defer-wgrad", type=int, default=-1,
                     help="1: group weight gradients at the end of backward (default: on for 1 GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: FFN + attention-input forward GEMMs and the attention forward in "
-                         "e4m3, FFN dgrads e5m2 x e4m3, delayed scaling "
-                         "(BASELINE config 5)")
+                    help="fp8 (BASELINE config 5): every encoder/decoder projection GEMM in fp8 "
+                         "(forward e4m3 x e4m3; dgrads and weight gradients e5m2 x e4m3), the "
+                         "attention forward in e4m3, delayed per-tensor scaling; the per-op map "
+                         "(ops/fp8.py precision_map) is printed in the record's dtype field")
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     ap.add_argument("--force-dp", type=int, default=0,
                     help="1: run the RCCL data-parallel path even with one rank (testing)")
@@ -162,7 +198,7 @@ def main() -> None:
     if ddp is not None:
         # every rank reports its own decision and spans (they must agree)
         spans = [round((b.end - b.start) * 4 / 2 ** 20, 1) for b in ddp.last_buckets]
-        print(f"[rank {info.rank}/{world}] dp_mode_select={dp_select} comm_thread={ddp._thread is not None} "
+        print(f"[rank {info.rank}/{world}] dp_mode_select={dp_select} comm_issue={ddp.comm_choice} "
               f"all-reduce spans per step (MB, launch order): {spans}", file=sys.stderr, flush=True)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -186,8 +222,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": ("fp32 (CPU reference ops)" if dev.type != "cuda" else "bf16") if args.dtype == "bf16" else
-                     "fp8 (e4m3 forward GEMMs of the FFNs and attention input projections, e4m3 "
-                     "attention forward, e5m2 x e4m3 FFN dgrads; bf16 elsewhere)",
+                     _fp8_precision(),
             "data": f"synthetic (random-init weights, synthetic pt/en token pairs, full-length {S})",
             "config": {
                 "model": f"transformer-{args.preset} ({cfg.layers}L, d_model={cfg.d_model}, "
@@ -199,6 +234,7 @@ def main() -> None:
                 "hip_graph": (("segmented" if step.segments is not None else "single")
                               if use_graph else False),
                 **({"dp_mode_select": dp_select} if dp_select else {}),
+                **({"comm_issue": ddp.comm_choice} if ddp is not None else {}),
                 "grad_comm": args.grad_comm,
                 "defer_wgrad": step.rt.wgrad is not None,
                 "bucket_mb": args.bucket_mb,

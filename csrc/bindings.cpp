@@ -392,6 +392,9 @@ void attn_bwd_g8(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor
   TORCH_CHECK(q.size(3) == 64 && (a.Lq > 128 || a.Lk > 128),
               "attn_bwd_g8: the pipelined hd-64 kernels (Lq or Lk > 128) only");
   TORCH_CHECK(dk8.has_value() == dv8.has_value(), "attn_bwd_g8: dk8 and dv8 together");
+  // skip_bf16 leaves the bf16 dK / dV unwritten: only legal when their e5m2
+  // copies are the output (else the gradients would stay uninitialised)
+  TORCH_CHECK(!skip_bf16 || dk8.has_value(), "attn_bwd_g8: skip_bf16 needs dk8/dv8");
   auto same = [](const Tensor& x8, const Tensor& x, const char* n) {
     check_f8_fmt(x8, 1, n);
     TORCH_CHECK(x8.sizes() == x.sizes() && x8.strides() == x.strides(), n,
@@ -1143,7 +1146,15 @@ void adam_chunks(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor
                   chunks.size(1) == 4 && chunks.is_contiguous(),
               "adam_chunks: chunk table [n, 4] int64 on the GPU");
   TORCH_CHECK(step.scalar_type() == at::kLong && step.is_cuda(), "adam: step int64 GPU");
+  // The table's CONTENTS (start + n <= numel, n <= 4096, n % 4 == 0, slot <
+  // scale8.numel(), live e4m3 addresses) are validated on the host where it
+  // is built (ops/fp8.py validate_chunk_table: Fp8Weights.adam_chunks and
+  // Adam.apply_range) -- reading it back here would be a device sync inside
+  // the captured step. Here: its size against the buffer.
+  TORCH_CHECK(chunks.size(0) >= 1 && chunks.size(0) <= (p.numel() + 3) / 4,
+              "adam_chunks: chunk count out of range for the flat buffer");
   check_f32(scale8, "scale8");
+  TORCH_CHECK(amax8.numel() >= 2048, "adam_chunks: amax slot table");
   c10::DeviceGuard gd(p.device());
   check_err(tdg_adam_chunks(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                             v.data_ptr<float>(), shadow.data_ptr(), p.numel(), chunks.data_ptr(),

@@ -1,26 +1,22 @@
-"""FP8 (OCP e4m3) forward GEMMs with delayed per-tensor scaling.
+"""FP8 training path (BASELINE config 5: "Transformer-big seq_len=512 fp8 MFMA
+attention+FFN"): e4m3 / e5m2 operands on gfx950's block-scaled MFMA
+(`v_mfma_scale_f32_*_f8f6f4`, csrc/kernels/fp8.hip) with delayed
+per-tensor scaling.
 
-BASELINE config 5 ("Transformer-big seq_len=512 fp8 MFMA attention+FFN").
-Every fp8 operand has a slot in one device-resident `Fp8Meta`: `scale[i]`
-(x8 = e4m3(x * scale)) and `amax[i]` (max |x| recorded by whoever quantised
-slot i this step). Once per step, after the optimizer,
-`Fp8Meta.update()` turns the recorded amax into the next step's scale
-(448 / (amax * 2^margin)) and clears amax -- all on device, so the step stays
-one HIP graph. Weights are re-quantised right after that update, with the
-scale the next forward will dequantise with.
+Every fp8 operand has a slot in a device-resident `Fp8Meta` (e4m3 for
+activations and weights, a second e5m2 one for gradients): `scale[i]`
+(x8 = fp8(x * scale)) and `amax[i]` (max |x| recorded by whoever quantised
+slot i this step). Once per step `Fp8Meta.update()` turns the recorded amax
+into the next step's power-of-two scale and clears amax -- on device, so the
+step stays one HIP graph; the e4m3 weight copies are refreshed by the Adam
+kernel itself (adam_chunk_kernel) with the scale the next forward uses.
 
-Forward: activation -> e4m3 (fp8_quant, or fused into the producing GEMM's
-epilogue), e4m3 x e4m3 GEMM on the block-scaled MFMA (csrc/kernels/fp8.hip),
-bf16 out. Backward (`Fp8State(backward=True)`): the two FFN dgrads run as
-e5m2-gradient x e4m3-transposed-weight GEMMs (the ReLU-backward one emits the
-e5m2 copy of its output for the other, which accumulates the residual
-gradient); gradient scales live in a second, e5m2 `Fp8Meta`. The FFN weight
-gradients run in fp8 too (`wgrad_fp8`: e5m2 gradient x the forward's e4m3
-activation copy, both token-major, through the transposing LDS reads); the
-attention backward, the other weight gradients and the optimizer stay bf16 /
-fp32.
-Measured on Transformer-big seq 512: 14.77-14.83 vs 14.85-14.99 ms/step with
-the FFN backward in bf16 (profiles/r3s2/fp8_backward_ab.txt).
+What runs in which format is `precision_map()` (bench.py prints it in its
+record for `--dtype fp8`): every projection GEMM of the encoder / decoder
+layers -- forward, dgrad and weight gradient -- and the attention forward
+are fp8; the attention backward, the vocabulary projection, LayerNorm,
+embeddings, cross-entropy and the fp32 Adam are not. Measured (docs/PERF.md):
+Transformer-big seq 512 fp8 11.78 vs 13.59 ms/step bf16 on one box (round 4).
 """
 from __future__ import annotations
 
@@ -57,6 +53,65 @@ DGRAD_PLAIN_W = True
 # quantise + column-sum pass over the bf16 gradient (long sequences)
 ATTN_BWD_G8 = True
 _TUNED: Dict[tuple, int] = {}
+
+
+def precision_map() -> Dict[str, str]:
+    """Per-op number formats of the `--dtype fp8` training step with the
+    module flags as they are (the truthful record bench.py prints)."""
+    proj_bwd = "e5m2 x e4m3" if ATTN_PROJ_FP8 else "bf16"
+    return {
+        "ffn_forward": "e4m3 x e4m3 (FFN1 bias+ReLU, FFN2)",
+        "attention_input_projections_forward": "e4m3 x e4m3 (self Q|K|V, cross Q, batched cross K|V)",
+        "attention_output_projection_forward": "e4m3 x e4m3" if ATTN_PROJ_FP8 else "bf16",
+        "attention_forward": "e4m3 Q/K/V and P, fp32 softmax (hd 64, seq > 128; else bf16)",
+        "attention_backward": ATTN_BWD_PRECISION,
+        "ffn_dgrads": "e5m2 x e4m3 (ReLU-backward epilogue)",
+        "attention_projection_dgrads": proj_bwd,
+        "ffn_weight_gradients": "e5m2 x e4m3" if WGRAD_FP8 else "bf16",
+        "attention_projection_weight_gradients": proj_bwd if WGRAD_FP8 else "bf16",
+        "vocab_projection": "bf16 (forward, dgrad, weight gradient)",
+        "layernorm": "fp32 math on bf16 I/O (emits the e4m3 / e5m2 copies its fp8 consumers read)",
+        "embedding": "bf16 gather, fp32 fixed-point gradient",
+        "cross_entropy": "fp32 on bf16 logits",
+        "optimizer": "fp32 Keras Adam (refreshes the bf16 and e4m3 weight copies)",
+    }
+
+
+# the attention backward's format (precision_map): its MFMAs read the
+# dequantised e4m3 Q/K/V of the forward and bf16 dO
+ATTN_BWD_PRECISION = "bf16 MFMA on the dequantised e4m3 Q/K/V, bf16 dO (e5m2 dQ|dK|dV out)"
+
+
+def precision_string() -> str:
+    return "fp8: " + "; ".join(f"{k}={v}" for k, v in precision_map().items())
+
+
+ADAM_CHUNK = 4096  # parameters per adam_chunk_kernel workgroup
+
+
+def validate_chunk_table(rows, total: int, nslots: int, w8_extents=()) -> None:
+    """Host-side check of an adam_chunk_kernel table (rows of (start, n,
+    slot, e4m3 address)) before it is uploaded: every chunk inside the flat
+    buffer, n in (0, 4096] and a multiple of 4, starts 4-aligned, chunks
+    disjoint and in order, slots in range, and every e4m3 address inside one
+    of the live copies w8_extents = [(address, bytes)] at the chunk's offset
+    within it. The kernel trusts the table (it silently skips parameters past
+    4096 in a chunk), so a malformed one must never reach it."""
+    pos = 0
+    ext = sorted(w8_extents)
+    for start, n, slot, addr in rows:
+        if not (0 < n <= ADAM_CHUNK and n % 4 == 0 and start % 4 == 0):
+            raise ValueError(f"adam chunk ({start}, {n}): n must be in (0, {ADAM_CHUNK}] and 4-aligned")
+        if start < pos or start + n > total:
+            raise ValueError(f"adam chunk ({start}, {n}) overlaps or leaves the flat buffer [0, {total})")
+        pos = start + n
+        if slot >= 0:
+            if slot >= nslots or not addr:
+                raise ValueError(f"adam chunk ({start}, {n}): slot {slot} / address {addr:#x} invalid")
+            if not any(a <= addr and addr + n <= a + nb for a, nb in ext):
+                raise ValueError(f"adam chunk ({start}, {n}): e4m3 address {addr:#x} outside every copy")
+        elif addr:
+            raise ValueError(f"adam chunk ({start}, {n}): address without a slot")
 
 
 class Fp8Meta:
@@ -313,11 +368,14 @@ class Fp8Weights:
         rows (start, count <= 4096, slot or -1, e4m3 address or 0); chunks
         never cross into or out of a weight with an e4m3 copy. None when some
         copy is transposed or the buffer exceeds the kernel's 2^28 limit."""
-        if getattr(self, "_chunks", None) is not None:
+        # the table bakes in the e4m3 copies' addresses and the buffer size:
+        # rebuilt if either changed since it was built
+        sig = (store.total, tuple((w8.data_ptr(), w8.numel()) for _, w8, _, _ in self.items))
+        if getattr(self, "_chunks", None) is not None and self._chunk_sig == sig:
             return self._chunks
         if any(it[3] for it in self.items) or store.total >= (1 << 28):
             return None
-        CH = 4096
+        CH = ADAM_CHUNK
         segs = sorted(((p.offset, p.numel, w8, slot) for p, w8, slot, _ in self.items),
                       key=lambda t: t[0])
         rows, pos = [], 0
@@ -335,7 +393,10 @@ class Fp8Weights:
                 rows.append((off + c0, min(CH, n - c0), slot, base + c0))
             pos = off + n
         plain(pos, store.total)
+        validate_chunk_table(rows, store.total, self.meta.scale.numel(),
+                             [(w8.data_ptr(), w8.numel()) for _, w8, _, _ in self.items])
         self._chunks = torch.tensor(rows, dtype=torch.int64, device=self.meta.device)
+        self._chunk_sig = sig
         return self._chunks
 
     def calibrate(self) -> None:

@@ -44,22 +44,29 @@ from tensorflow_distributed_on_gke_amd.models.params import Param, ParamStore
 from tensorflow_distributed_on_gke_amd.parallel.dist import PG_TIMEOUT_S
 
 
-# Issue GPU collectives from a host thread (CommThread) instead of making the
-# communication stream wait on the compute stream. Default on RCCL
-# (TDG_DP_COMM_THREAD=0: the process group's own stream handoff; "force":
-# also over gloo with GPU tensors -- the multi-rank rehearsals on one GPU,
-# tests/test_gpu_dp.py). Round 4, one rank through the data-parallel step
-# (--force-dp 1, same box): 5.10-5.12 ms with the thread vs 5.33-5.35 without,
-# single graph 5.01 (profiles/r4/ab_dp_comm_thread.txt).
-COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "1")
+# Issue the gradient collectives from a host thread (CommThread) instead of
+# making the communication stream wait on the compute stream.
+#   "auto" (default): both issue paths are kept ready; TrainStep.choose_dp_mode
+#          times them on the node the job runs on (segmented HIP graph with the
+#          thread vs with the process group's own stream handoff), checks that
+#          the replicas stay bitwise equal after each (verify_replicas) and keeps
+#          the faster verified one. Without that start-up measurement the
+#          process group's handoff is used -- the thread is never the default
+#          on evidence from another machine (round-4 one-rank A/B: 5.10-5.12 ms
+#          with the thread vs 5.33-5.35 without, profiles/r4/ab_dp_comm_thread.txt).
+#   "1":   thread on RCCL (no measurement);  "0": never;
+#   "force": thread also over gloo (GPU tensors: the multi-rank rehearsals on
+#          one GPU, tests/test_gpu_dp.py; CPU tensors: tests/test_parallel_cpu.py).
+COMM_THREAD = os.environ.get("TDG_DP_COMM_THREAD", "auto")
+# tests: each thread-issued collective first sleeps a random 0..N ms (per-rank
+# jitter in issue timing; replicas must stay bitwise equal and nothing hangs)
+ISSUE_JITTER_MS = float(os.environ.get("TDG_DP_ISSUE_JITTER_MS", "0") or 0)
 # seconds the host waits for the comm thread to enqueue a collective before
 # the data-parallel state is poisoned and the step raises (a GPU that never
 # reaches the issue point would otherwise hang); default: the process-group
 # timeout (parallel/dist.py). A stall is reported every ISSUE_REPORT_S.
 COMM_ISSUE_TIMEOUT_S = PG_TIMEOUT_S
 ISSUE_REPORT_S = 60.0
-
-
 class CommThread:
     """Issues the data-parallel collectives from one host thread, each once the
     compute-stream event recorded at its issue point has completed, on a
@@ -71,17 +78,20 @@ class CommThread:
     reverse wait (compute waits for the finished all-reduce) and a plain event
     record are cheap (scripts/seg_comm_probe.py, docs/ROADMAP.md). One thread
     issues everything, so every rank issues its collectives in the same
-    order, as ProcessGroupNCCL requires."""
+    order, as ProcessGroupNCCL requires. CPU tensors (gloo rehearsals): no
+    streams; the job issues the collective and waits for it on the thread."""
 
     def __init__(self, device: torch.device):
         self.device = device
-        self.stream = torch.cuda.Stream(device)
+        self.cuda = device.type == "cuda"
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
         self._q: "queue.Queue[Optional[Callable[[], None]]]" = queue.Queue()
         self._t = threading.Thread(target=self._run, name="tdg-comm", daemon=True)
         self._t.start()
 
     def _run(self) -> None:
-        torch.cuda.set_device(self.device)
+        if self.cuda:
+            torch.cuda.set_device(self.device)
         while True:
             job = self._q.get()
             if job is None:
@@ -185,11 +195,19 @@ class DataParallel:
         # a train/graphs.SegmentedGraph while the step is being captured: the
         # collectives become host calls between graph segments
         self.recorder = None
-        # GPU collectives issued from a host thread (CommThread)
+        # collectives issued from a host thread (CommThread): `_comm` is the
+        # thread when this configuration may use one, `_thread` the issue
+        # path in use (None: the process group's own stream handoff)
+        self._comm: Optional[CommThread] = None
         self._thread: Optional[CommThread] = None
-        if self.active and COMM_THREAD != "0" and store.flat.is_cuda and \
-                (dist.get_backend(group) == "nccl" or COMM_THREAD == "force"):
-            self._thread = CommThread(store.flat.device)
+        if self.active and COMM_THREAD != "0":
+            nccl = store.flat.is_cuda and dist.get_backend(group) == "nccl"
+            if nccl or COMM_THREAD == "force":
+                self._comm = CommThread(store.flat.device)
+                if COMM_THREAD in ("1", "force"):
+                    self._thread = self._comm
+        # how the issue path was chosen (introspection / the bench record)
+        self.comm_choice = "thread" if self._thread is not None else "pg"
         # collectives issued but not yet waited for (any issue path): a
         # main-thread collective issued meanwhile could interleave differently
         # on different ranks, so those check this is zero (check_quiescent)
@@ -284,19 +302,32 @@ class DataParallel:
             if th is None:
                 h.work = dist.all_reduce(t, group=grp, async_op=True)
                 return
-            ready = torch.cuda.Event()
-            ready.record()  # the current (compute) stream: t is final here
+            cuda = th.cuda
+            ready = None
+            if cuda:
+                ready = torch.cuda.Event()
+                ready.record()  # the current (compute) stream: t is final here
             h.issued = threading.Event()
             h.error = None
+            jitter = ISSUE_JITTER_MS
 
             def job():
                 try:
-                    ready.synchronize()
-                    with torch.cuda.stream(th.stream):
+                    if jitter > 0:
+                        import random
+                        import time
+                        time.sleep(random.uniform(0.0, jitter) / 1e3)
+                    if cuda:
+                        ready.synchronize()
+                        with torch.cuda.stream(th.stream):
+                            w = dist.all_reduce(t, group=grp, async_op=True)
+                            w.wait()  # comm stream after the collective
+                            done = torch.cuda.Event()
+                            done.record(th.stream)
+                    else:  # CPU (gloo): complete before `issued` is set
                         w = dist.all_reduce(t, group=grp, async_op=True)
-                        w.wait()  # comm stream after the collective
-                        done = torch.cuda.Event()
-                        done.record(th.stream)
+                        w.wait()
+                        done = None
                     h.work, h.done = w, done
                 except BaseException as e:  # surfaced by the waiter
                     h.error = e
@@ -318,9 +349,9 @@ class DataParallel:
 
     def _poison(self, reason: str) -> None:
         self.poisoned = reason
-        if self._thread is not None:
+        if self._comm is not None:
             # a stuck job keeps later ones queued behind it: drop them all
-            self._thread.abandon()
+            self._comm.abandon()
 
     def check_quiescent(self, what: str) -> None:
         """Every collective this object issued has been waited for: `what` (a
@@ -330,6 +361,21 @@ class DataParallel:
         if self._outstanding:
             raise RuntimeError(f"{what}: {self._outstanding} data-parallel collective(s) issued but not "
                                "waited for (call finish() first)")
+
+    @property
+    def can_thread(self) -> bool:
+        """A comm thread exists, so the issue path can be switched."""
+        return self._comm is not None
+
+    def use_thread(self, on: bool) -> None:
+        """Select the issue path for collectives issued from now on (a
+        segmented graph captured earlier keeps the path it was captured
+        with). Only between steps: nothing may be in flight."""
+        self.check_quiescent("use_thread")
+        if on and self._comm is None:
+            raise RuntimeError("no comm thread in this configuration (TDG_DP_COMM_THREAD)")
+        self._thread = self._comm if on else None
+        self.comm_choice = "thread" if on else "pg"
 
     def _wait_now(self, h: Pending) -> None:
         """Current stream waits for the collective (device-side; the host only
@@ -352,7 +398,8 @@ class DataParallel:
         if h.error is not None:
             self._poison(f"collective failed on the comm thread: {h.error!r}")
             raise RuntimeError("data-parallel collective failed on the comm thread") from h.error
-        torch.cuda.current_stream().wait_event(h.done)
+        if h.done is not None:
+            torch.cuda.current_stream().wait_event(h.done)
         self._outstanding -= 1
 
     def _wait(self, h: Pending) -> None:
@@ -462,9 +509,9 @@ class DataParallel:
         """Stop the comm thread (all its collectives have been waited for).
         Raises if it is stuck, so the process exits non-zero instead of
         tearing the process group down under a collective."""
-        if self._thread is not None:
-            ok = self._thread.close()
-            self._thread = None
+        if self._comm is not None:
+            ok = self._comm.close()
+            self._comm = self._thread = None
             if not ok:
                 raise RuntimeError("data-parallel comm thread did not stop (a collective is stuck)")
 

@@ -89,6 +89,8 @@ class Adam:
         if tabs is not None:
             if (start, end) not in tabs:
                 rows = [(c0, min(4096, end - c0), -1, 0) for c0 in range(start, end, 4096)]
+                from tensorflow_distributed_on_gke_amd.ops.fp8 import validate_chunk_table
+                validate_chunk_table(rows, s.total, 1)
                 tabs[(start, end)] = torch.tensor(rows, dtype=torch.int64, device=s.flat.device)
             if getattr(self, "_no8", None) is None:
                 self._no8 = (torch.ones(1, device=s.flat.device),

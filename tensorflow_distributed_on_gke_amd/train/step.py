@@ -21,6 +21,7 @@ import torch.distributed as dist
 
 from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
 from tensorflow_distributed_on_gke_amd.models.transformer import Transformer
+from tensorflow_distributed_on_gke_amd.parallel import ddp as _ddp_mod
 from tensorflow_distributed_on_gke_amd.parallel.ddp import DataParallel
 from tensorflow_distributed_on_gke_amd.ops import kernels as K
 from tensorflow_distributed_on_gke_amd.train.graphs import SegmentedGraph, prepare_capture
@@ -186,7 +187,14 @@ class TrainStep:
         mode = self.capture_mode()
         if mode == "0":
             return False
-        self._static = (src.clone(), tgt.clone())
+        if (self._static is not None and self._static[0].shape == src.shape
+                and self._static[1].shape == tgt.shape):
+            # (choose_dp_mode captures more than one arm: every captured graph
+            # reads the same static input buffers)
+            self._static[0].copy_(src)
+            self._static[1].copy_(tgt)
+        else:
+            self._static = (src.clone(), tgt.clone())
         saved = self.snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -230,59 +238,98 @@ class TrainStep:
 
     def choose_dp_mode(self, src: torch.Tensor, tgt: torch.Tensor, steps: int = 8,
                        rounds: int = 3, margin: float = 0.03) -> Dict[str, object]:
-        """Data parallel: capture the segmented graph, then time it against the
-        eager step on this batch (interleaved rounds, median per mode, MAX over
-        ranks so every rank takes the same decision) and keep the faster. The
+        """Data parallel: pick how the step runs on THIS node, by measurement.
+
+        Arms: the segmented graph (collectives issued between graph segments)
+        and the eager step; and, where a comm thread exists
+        (ddp.COMM_THREAD "auto"), the segmented graph once more with the
+        collectives issued by the host comm thread instead of the process
+        group's own stream handoff. Each arm is timed in interleaved rounds
+        (median per arm, MAX over ranks, so every rank takes the same
+        decision) and, after its timed steps, the replicas must be bitwise
+        equal (DataParallel.verify_replicas raises otherwise: an issue path
+        that breaks synchronous DP is an error, not a slower option). The
         segmented graph wins when the host is the bottleneck (eight ranks
-        sharing a node's CPUs: the eager step's enqueue costs about its GPU
-        time); the eager step wins when the host keeps ahead (on one MI355X
-        with a fast host the graph cuts cost ~0.3 ms/step, docs/PERF.md). The
-        training state is restored afterwards, so this trains nothing. Returns
-        {"mode": "seg" | "0", "seg_ms": .., "eager_ms": ..}."""
+        sharing a node's CPUs); the eager step when the host keeps ahead. The
+        training state is restored afterwards, so this trains nothing.
+        Returns {"mode": "seg" | "0", "comm_thread": bool, "<arm>_ms": ..}."""
+        ddp = self.ddp
+        auto_thread = (ddp is not None and ddp.active and ddp.can_thread
+                       and _ddp_mod.COMM_THREAD == "auto")
+        if auto_thread:
+            ddp.use_thread(False)
         if not self.capture(src, tgt):
-            return {"mode": self.capture_mode()}
-        if not (self.ddp is not None and self.ddp.active and self.segments is not None) \
-                or not DP_AUTOSELECT:
-            return {"mode": "seg" if self.segments is not None else self.capture_mode()}
+            return {"mode": self.capture_mode(), "comm_thread": ddp is not None and ddp._thread is not None}
+        if not (ddp is not None and ddp.active and self.segments is not None) or not DP_AUTOSELECT:
+            return {"mode": "seg" if self.segments is not None else self.capture_mode(),
+                    "comm_thread": ddp is not None and ddp._thread is not None}
+        arms = {"seg": (self.segments, ddp._thread is not None)}
+        if auto_thread:
+            self.segments = None
+            ddp.use_thread(True)
+            if self.capture(src, tgt):
+                arms["seg_thread"] = (self.segments, True)
+            ddp.use_thread(False)
         saved = self.snapshot()
         dev = self.model.device
-        seg = self.segments
 
         def timed(run) -> float:
             for _ in range(2):
                 run()
             torch.cuda.synchronize()
-            self.ddp.check_quiescent("choose_dp_mode")
-            dist.barrier(group=self.ddp.group)
+            ddp.check_quiescent("choose_dp_mode")
+            dist.barrier(group=ddp.group)
             t0 = time.perf_counter()
             for _ in range(steps):
                 run()
             torch.cuda.synchronize()
-            return (time.perf_counter() - t0) / steps
+            dt = (time.perf_counter() - t0) / steps
+            ddp.verify_replicas()  # the arm kept synchronous DP exact
+            return dt
 
-        runs = {"seg": [], "0": []}
+        def seg_run(name):
+            segs, th = arms[name]
+
+            def run():
+                self.segments = segs
+                self(src, tgt)
+            return run, th
+
+        names = list(arms) + ["0"]
+        runs = {k: [] for k in names}
         for _ in range(rounds):
-            self.segments = seg
-            runs["seg"].append(timed(lambda: self(src, tgt)))
-            self.segments = None
-            runs["0"].append(timed(lambda: self.eager(src, tgt)))
-        # median per mode: one noisy round (box clock, host contention) does
+            for k in names:
+                if k == "0":
+                    self.segments = None
+                    ddp.use_thread(False)
+                    runs[k].append(timed(lambda: self.eager(src, tgt)))
+                else:
+                    run, th = seg_run(k)
+                    ddp.use_thread(th)  # (a captured graph keeps its own path)
+                    runs[k].append(timed(run))
+        # median per arm: one noisy round (box clock, host contention) does
         # not decide the mode for the whole run
         med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
-        t = torch.tensor([med["seg"], med["0"]], dtype=torch.float64, device=dev)
-        self.ddp.check_quiescent("choose_dp_mode")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ddp.group)
-        seg_s, eager_s = float(t[0]), float(t[1])
+        t = torch.tensor([med[k] for k in names], dtype=torch.float64, device=dev)
+        ddp.check_quiescent("choose_dp_mode")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ddp.group)
+        ms = {k: float(v) for k, v in zip(names, t.tolist())}
         self.restore(saved)
-        if eager_s < seg_s * (1.0 - margin):
+        best_seg = min((k for k in names if k != "0"), key=lambda k: ms[k])
+        if ms["0"] < ms[best_seg] * (1.0 - margin):
             self.segments = None
             self._static = None
-            mode = "0"
+            ddp.use_thread(False)
+            mode, th = "0", False
         else:
-            self.segments = seg
+            self.segments, th = arms[best_seg]
+            ddp.use_thread(th)
             mode = "seg"
+        arms.clear()  # the other captures' graphs and pools are released
         torch.cuda.synchronize()
-        return {"mode": mode, "seg_ms": round(seg_s * 1e3, 3), "eager_ms": round(eager_s * 1e3, 3)}
+        out = {"mode": mode, "comm_thread": th}
+        out.update({f"{'eager' if k == '0' else k}_ms": round(v * 1e3, 3) for k, v in ms.items()})
+        return out
 
     def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         if not self.captured:

@@ -62,3 +62,64 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_self_launches_eight_ranks():
+    """`python bench.py --gpus 8` -- the driver's largest case -- starting its
+    own eight ranks (gloo on CPU, tiny preset), with the host comm-thread
+    issue path forced and random per-rank issue jitter: one dp8 line from
+    rank 0, global batch 8 x local."""
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1",
+           "--preset", "tiny", "--local-batch", "2", "--seq-len", "8"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "MASTER_ADDR", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", TDG_DP_COMM_THREAD="force", TDG_DP_ISSUE_JITTER_MS="10")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8"
+    assert d["config"]["global_batch"] == 16
+    assert d["config"]["comm_issue"] == "thread"
+    assert r.stderr.count("comm_issue=thread") == 8  # every rank on the thread path
+
+
+def test_visible_gpus_does_not_initialise_hip(monkeypatch):
+    """The self-launching parent counts GPUs from the visible-devices lists
+    or the KFD topology, never through a HIP call."""
+    import importlib.util
+
+    import torch
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    assert bench.visible_gpus() == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus() == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert bench.visible_gpus() >= 0  # KFD topology (0 without a GPU)
+    assert not torch.cuda.is_initialized()
+
+
+def test_fp8_precision_record_lists_every_op():
+    """bench.py's dtype field for --dtype fp8 says exactly what runs in which
+    format (the output projection and the weight gradients are fp8, the
+    attention backward is not)."""
+    from tensorflow_distributed_on_gke_amd.ops import fp8
+
+    m = fp8.precision_map()
+    s = fp8.precision_string()
+    assert m["attention_output_projection_forward"].startswith("e4m3")
+    assert m["ffn_weight_gradients"].startswith("e5m2")
+    assert m["attention_projection_weight_gradients"].startswith("e5m2")
+    assert m["attention_projection_dgrads"].startswith("e5m2")
+    assert m["attention_backward"] == fp8.ATTN_BWD_PRECISION
+    assert "attention_backward=" + fp8.ATTN_BWD_PRECISION in s
+    assert m["vocab_projection"].startswith("bf16")
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "_fp8_precision()" in src  # the record prints the map

@@ -146,12 +146,14 @@ def test_gpu_dp_rehearsal_matches_single_process(tmp_path, world, opt_mode, loss
     assert torch.allclose(r0["loss"], torch.stack(losses), rtol=1e-3, atol=1e-4)
 
 
-def _fp8_worker(rank, world, port, out, graph):
+def _fp8_worker(rank, world, port, out, graph, comm_thread="force"):
     """Config 5's data-parallel step (fp8 forward + FFN backward, per-bucket
-    Adam at the tail, bf16 gradient all-reduce) with `world` ranks on cuda:0."""
+    Adam at the tail, bf16 gradient all-reduce) with `world` ranks on cuda:0;
+    collectives issued by the host comm thread (comm_thread "force": the path
+    choose_dp_mode may pick on RCCL) or the process group's own handoff."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
-                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD="0")
+                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD=comm_thread)
     from tensorflow_distributed_on_gke_amd.train import step as step_mod
     step_mod.WAVE_TILES = 37
     step_mod.DP_OVERLAP_OPT = "tail"
@@ -171,6 +173,7 @@ def _fp8_worker(rank, world, port, out, graph):
     m = Transformer(cfg).build(info.device, seed=1 + rank)
     opt = Adam(m.store, m.cfg.d_model, lr=1e-3)
     ddp = DataParallel(m.store, bucket_mb=0.25, comm_dtype=torch.bfloat16)
+    assert (ddp._thread is not None) == (comm_thread == "force")
     ddp.broadcast_params(0)
     st = F.Fp8State(m)  # after the broadcast: weight scales from the common weights
     st.weights.calibrate()
@@ -200,14 +203,15 @@ def _fp8_worker(rank, world, port, out, graph):
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("world,graph", [(2, "seg"), (4, "seg"), (2, "")])
-def test_gpu_dp_fp8_replicas_identical(tmp_path, world, graph):
+@pytest.mark.parametrize("world,graph,comm_thread", [(2, "seg", "force"), (4, "seg", "force"),
+                                                     (2, "", "force"), (2, "seg", "0")])
+def test_gpu_dp_fp8_replicas_identical(tmp_path, world, graph, comm_thread):
     """fp8 + data parallel (BASELINE config 5 is DP = 8): replicas stay
     bitwise equal, every rank derives the same weight scales and e4m3 weight
     copies, and the losses are finite."""
     out = str(tmp_path / "res")
-    mp.start_processes(_fp8_worker, args=(world, _port(), out, graph), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_fp8_worker, args=(world, _port(), out, graph, comm_thread), nprocs=world,
+                       join=True, start_method="spawn")
     rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     for r in rs[1:]:
         assert torch.equal(rs[0]["flat"], r["flat"])

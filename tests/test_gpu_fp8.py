@@ -608,3 +608,67 @@ def test_fused_fp8_adam_matches_separate_refresh(monkeypatch):
                       torch.cat([w8.view(torch.uint8).reshape(-1) for _, w8, _, _ in st.weights.items]))
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+
+
+def test_adam_chunk_kernel_matches_grid_adam_and_quant_multi():
+    """adam_chunk_kernel on its own, against the grid-strided Adam kernel and
+    fp8_quant_multi: a table with a ragged last chunk (< 4096), a range whose
+    start is not a multiple of 4096, chunks refreshing two e4m3 copies (one
+    starting mid-buffer, one of a length that is not a multiple of 4096) and
+    plain chunks between them. p / m / v / the bf16 shadow must equal the
+    grid kernel's bitwise, the e4m3 copies and their amax must equal
+    fp8_quant_multi over the updated bf16 weights."""
+    from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+
+    torch.manual_seed(11)
+    total = 3 * 4096 + 2052  # ragged tail
+    p = torch.randn(total, device=DEV)
+    g = torch.randn(total, device=DEV) * 0.1
+    m0 = torch.randn(total, device=DEV) * 0.01
+    v0 = torch.rand(total, device=DEV) * 0.01
+    meta = F.Fp8Meta(DEV)
+    w_a, w_b = (1000, 5000), (8192, 6148)  # (offset, numel) of two weights with e4m3 copies
+    s_a, s_b = meta.slot("wa"), meta.slot("wb")
+    meta.scale[s_a], meta.scale[s_b] = 64.0, 128.0
+    y8a = torch.empty(w_a[1], dtype=F.FP8, device=DEV)
+    y8b = torch.empty(w_b[1], dtype=F.FP8, device=DEV)
+    rows = []
+    pos = 4  # the whole-step range starts past 0 (not a multiple of 4096)
+
+    def plain(a, b):
+        for c0 in range(a, b, 4096):
+            rows.append((c0, min(4096, b - c0), -1, 0))
+
+    for (off, n), slot, y8 in ((w_a, s_a, y8a), (w_b, s_b, y8b)):
+        plain(pos, off)
+        for c0 in range(0, n, 4096):
+            rows.append((off + c0, min(4096, n - c0), slot, y8.data_ptr() + c0))
+        pos = off + n
+    plain(pos, total)
+    F.validate_chunk_table(rows, total, meta.scale.numel(), [(y8a.data_ptr(), y8a.numel()),
+                                                               (y8b.data_ptr(), y8b.numel())])
+    tab = torch.tensor(rows, dtype=torch.int64, device=DEV)
+    args = (0.9, 0.98, 1e-9, 0.0, 512.0, 4000.0)
+
+    def run(chunked):
+        pp, gg, mm, vv = p.clone(), g.clone(), m0.clone(), v0.clone()
+        sh = torch.zeros(total, dtype=torch.bfloat16, device=DEV)
+        step = torch.tensor([7], dtype=torch.int64, device=DEV)
+        if chunked:
+            meta.amax.zero_()
+            kk.adam_chunks(pp, gg, mm, vv, sh, tab, step, *args, 1.0, 0.0, 1, True, True,
+                           meta.scale, meta.amax)
+        else:
+            sl = slice(4, total)
+            kk.adam(pp[sl], gg[sl], mm[sl], vv[sl], sh[sl], step, *args, 1.0, 0.0, 1, True, True)
+        torch.cuda.synchronize()
+        return pp, gg, mm, vv, sh, step
+
+    got, ref = run(True), run(False)
+    for a, b, name in zip(got, ref, ("p", "g", "m", "v", "shadow", "step")):
+        assert torch.equal(a, b), name
+    sh = got[4]
+    for (off, n), slot, y8 in ((w_a, s_a, y8a), (w_b, s_b, y8b)):
+        want = F.quantize(sh[off:off + n], meta, slot, record=False)
+        assert torch.equal(y8.view(torch.uint8), want.view(torch.uint8))
+        assert meta.amax_values()[slot].item() == sh[off:off + n].float().abs().max().item()

@@ -40,12 +40,17 @@ def _data(rank, world):
     return SyntheticPairs(4, 10, 11, 60, 50, seed=3, rank=rank, world=world, min_len=3)
 
 
-def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mode="replica_mean"):
+def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mode="replica_mean",
+            comm_thread=None, jitter_ms=0.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from tensorflow_distributed_on_gke_amd.train import step as step_mod
     step_mod.DP_OVERLAP_OPT = str(overlap_opt)
-    torch.set_num_threads(2)
+    if comm_thread is not None:  # the host comm-thread issue path (ddp.CommThread)
+        from tensorflow_distributed_on_gke_amd.parallel import ddp as ddp_mod
+        ddp_mod.COMM_THREAD = comm_thread
+        ddp_mod.ISSUE_JITTER_MS = jitter_ms
+    torch.set_num_threads(1 if world > 4 else 2)
     from tensorflow_distributed_on_gke_amd.parallel import dist as tdist
     from tensorflow_distributed_on_gke_amd.train.step import TrainStep
 
@@ -63,6 +68,8 @@ def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mo
         early.append(sum(b.updated for b in ddp.buckets) - before)
 
     ddp._on_release = spy
+    if comm_thread == "force":
+        assert ddp._thread is not None and ddp.comm_choice == "thread"
     step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
     data = _data(rank, world)
     losses = []
@@ -81,6 +88,7 @@ def _worker(rank, world, port, out, bucket_mb, comm=None, overlap_opt=0, loss_mo
     torch.save({"flat": m.store.flat.clone(), "loss": torch.stack(losses), "nb": len(ddp.last_buckets),
                 "diverged": diverged, "early": torch.tensor(early)},
                f"{out}.{rank}")
+    ddp.close()
     tdist.barrier()
     tdist.shutdown()
 
@@ -141,6 +149,30 @@ def test_dp4_matches_single_process(tmp_path):
     world = 4
     out = str(tmp_path / "res")
     mp.start_processes(_worker, args=(world, _free_port(), out, 0.05, None, 1),
+                       nprocs=world, join=True, start_method="spawn")
+    rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    assert rs[0]["nb"] > 3
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["flat"], r["flat"])
+    assert all(r["diverged"] for r in rs)
+    ref_flat, ref_loss = _single_process_reference(world)
+    assert torch.allclose(rs[0]["flat"], ref_flat, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(rs[0]["loss"], ref_loss, atol=1e-6)
+
+
+@pytest.mark.parametrize("overlap_opt", [1, 0])
+def test_dp8_comm_thread_with_issue_jitter(tmp_path, overlap_opt):
+    """Eight ranks -- a whole MI355X node's worth -- on the host comm-thread
+    issue path (forced over gloo), every collective issued after a random
+    per-rank 0-20 ms delay, small spans launched from inside backward (and,
+    with overlap_opt, per-span Adam mid-backward): no hang within the
+    process-group timeout, every replica bitwise equal after every step
+    (verify_replicas in the worker), and the update equal to one process
+    running all eight ranks' batches."""
+    world = 8
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, _free_port(), out, 0.05, None, overlap_opt, "replica_mean",
+                                      "force", 20.0),
                        nprocs=world, join=True, start_method="spawn")
     rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     assert rs[0]["nb"] > 3
