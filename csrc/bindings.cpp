@@ -27,12 +27,12 @@ int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
-               unsigned* amax8, hipStream_t st);
+               unsigned* amax8, void* kbits, hipStream_t st);
 int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, const float* rstd,
                const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
                float* dbeta, float* dbias, float* ws, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, int accumulate, int skip_reduce,
-               int rpb, void* ds8, const float* s8, unsigned* amax8,
+               int rpb, void* ds8, const float* s8, unsigned* amax8, const void* kbits,
                hipStream_t st);
 int tdg_reduce_partials_multi(const float* const* parts, float* const* outs, const int* nparts,
                               int G, int N, float beta, hipStream_t st);
@@ -91,6 +91,16 @@ int tdg_adam_chunks(float* p, float* g, float* m, float* v, void* shadow, long l
                     float weight_decay, int sched, int zero_grad, int inc_step,
                     const float* scale8, unsigned* amax8, hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
+int tdg_gemm_ln_fwd(const void* A, const void* W, const float* bias, const void* x,
+                    const float* gamma, const float* beta, void* y, void* hsave, float* mean,
+                    float* rstd, int M, int N, int K, int lda, int ldw, float p, uint64_t seed,
+                    const long long* ctr, uint64_t site, float eps, void* kbits, void* xch,
+                    unsigned* band_ctr, unsigned* err, int stages, int ablate, hipStream_t st);
+int tdg_gemm_ln_bwd(const void* A, const void* W, const void* C, const void* h, const float* mean,
+                    const float* rstd, const float* gamma, void* dh, void* ds, float* part, int M,
+                    int N, int K, int lda, int ldw, float beta, float p, uint64_t seed,
+                    const long long* ctr, uint64_t site, const void* kbits, void* xch,
+                    unsigned* band_ctr, unsigned* err, int stages, int ablate, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
 }
@@ -188,6 +198,129 @@ void gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tens
                           f32, (float)alpha, (float)beta, (int)tile_cfg, (int)splits, wptr,
                           stream_of(A));
   check_err(rc, "tdg gemm");
+}
+
+// ---------------------------------------------------------------- GEMM + LayerNorm
+// The band-exchange state shared by every fused launch of a device (one
+// stream): xch f32 [>= bands * 128 * 4 * 2], counters int32 [>= bands], err
+// int32 [1] (ops/kernels.py _ln_xch).
+void check_ln_xch(const Tensor& xch, const Tensor& band_ctr, const Tensor& err, int64_t M) {
+  const int64_t bands = (M + 127) / 128;
+  check_f32(xch, "xch");
+  TORCH_CHECK(xch.numel() >= bands * 128 * 4 * 2, "gemm_ln: exchange buffer too small");
+  TORCH_CHECK(band_ctr.is_cuda() && band_ctr.scalar_type() == at::kInt && band_ctr.numel() >= bands,
+              "gemm_ln: band counters int32 [>= bands]");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "gemm_ln: err int32");
+}
+
+// dropout keep-bit bitmap of a [M, D] LayerNorm: uint8 [M, D / 8]
+void check_kbits(const optional<Tensor>& kbits, int64_t M, int64_t D) {
+  if (!kbits.has_value()) return;
+  TORCH_CHECK(kbits->is_cuda() && kbits->scalar_type() == at::kByte && kbits->is_contiguous() &&
+                  kbits->numel() == M * D / 8 &&
+                  (reinterpret_cast<uintptr_t>(kbits->data_ptr()) % 4) == 0,
+              "kbits: uint8 [M, D / 8], 4-byte aligned");
+}
+
+int64_t ln_stages(int64_t stages, int64_t K) {
+  if (stages == 3 || stages == 4) return stages;
+  return K <= 512 ? 3 : 4;
+}
+
+// y, h, mean, rstd = LN(x + dropout(A @ W^T + bias)) for D = 512 (N of the GEMM)
+void gemm_ln_fwd(const Tensor& A, const Tensor& W, const Tensor& bias, const Tensor& x,
+                 const Tensor& gamma, const Tensor& beta, const Tensor& y, const Tensor& h,
+                 const Tensor& mean, const Tensor& rstd, double p, int64_t seed,
+                 const optional<Tensor>& ctr, int64_t site, double eps,
+                 const optional<Tensor>& kbits, const Tensor& xch, const Tensor& band_ctr,
+                 const Tensor& err, int64_t stages, int64_t ablate) {
+  check_bf16(A, "A");
+  check_bf16(W, "W");
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "gemm_ln_fwd: A [M,K], W [N,K]");
+  const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+  TORCH_CHECK(N == 512, "gemm_ln_fwd: d_model 512 only (4 column tiles per band)");
+  TORCH_CHECK(A.stride(1) == 1 && W.is_contiguous() && A.stride(0) % 8 == 0 && K % 8 == 0,
+              "gemm_ln_fwd: K-contiguous operands, rows 16-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0, "gemm_ln_fwd: A alignment");
+  for (auto* t : {&x, &y, &h}) {
+    check_bf16(*t, "x/y/h");
+    check_contig(*t, "x/y/h");
+    TORCH_CHECK(t->numel() == M * N, "gemm_ln_fwd: x / y / h must be [M, 512]");
+  }
+  for (auto* t : {&bias, &gamma, &beta}) {
+    check_f32(*t, "bias/gamma/beta");
+    TORCH_CHECK(t->numel() == N && t->is_contiguous(), "gemm_ln_fwd: bias / gamma / beta [512]");
+  }
+  for (auto* t : {&mean, &rstd}) {
+    check_f32(*t, "mean/rstd");
+    TORCH_CHECK(t->numel() >= M, "gemm_ln_fwd: mean / rstd [M]");
+  }
+  check_ln_xch(xch, band_ctr, err, M);
+  check_kbits(kbits, M, N);
+  const long long* cp = ctr.has_value() ? reinterpret_cast<const long long*>(ctr->data_ptr<int64_t>()) : nullptr;
+  c10::DeviceGuard g(A.device());
+  check_err(tdg_gemm_ln_fwd(A.data_ptr(), W.data_ptr(), bias.data_ptr<float>(), x.data_ptr(),
+                            gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                            h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)M,
+                            (int)N, (int)K, (int)A.stride(0), (int)K, (float)p, (uint64_t)seed, cp,
+                            (uint64_t)site, (float)eps,
+                            kbits.has_value() ? kbits->data_ptr() : nullptr, xch.data_ptr(),
+                            reinterpret_cast<unsigned*>(band_ctr.data_ptr()),
+                            reinterpret_cast<unsigned*>(err.data_ptr()), (int)ln_stages(stages, K),
+                            (int)ablate, stream_of(A)),
+            "tdg gemm_ln_fwd");
+}
+
+// dh, ds, column partials = LayerNorm backward of dy = dY @ W (+ C) for D = 512
+// (W [Kd, 512]: the GEMM's N = 512, K = Kd); part f32 [3][bands][512]
+void gemm_ln_bwd(const Tensor& A, const Tensor& W, const optional<Tensor>& C, const Tensor& h,
+                 const Tensor& mean, const Tensor& rstd, const Tensor& gamma, const Tensor& dh,
+                 const optional<Tensor>& ds, const Tensor& part, double p, int64_t seed,
+                 const optional<Tensor>& ctr, int64_t site, const optional<Tensor>& kbits,
+                 const Tensor& xch, const Tensor& band_ctr, const Tensor& err, int64_t stages,
+                 int64_t ablate) {
+  check_bf16(A, "A");
+  check_bf16(W, "W");
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2, "gemm_ln_bwd: A [M,K], W [K,N]");
+  const int64_t M = A.size(0), K = W.size(0), N = W.size(1);
+  TORCH_CHECK(N == 512, "gemm_ln_bwd: d_model 512 only (4 column tiles per band)");
+  TORCH_CHECK(A.size(1) >= K && A.stride(1) == 1 && A.stride(0) % 8 == 0 &&
+                  A.stride(0) >= (K + 7) / 8 * 8 && W.is_contiguous(),
+              "gemm_ln_bwd: dY K-contiguous (ld >= round8(K)), W contiguous");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0, "gemm_ln_bwd: A alignment");
+  check_extent(A, M, A.stride(0), (K + 7) / 8 * 8, "A");
+  std::vector<const Tensor*> outs = {&h, &dh};
+  if (C.has_value()) outs.push_back(&*C);
+  if (ds.has_value()) outs.push_back(&*ds);
+  for (auto* t : outs) {
+    check_bf16(*t, "h/dh/ds/C");
+    check_contig(*t, "h/dh/ds/C");
+    TORCH_CHECK(t->numel() == M * N, "gemm_ln_bwd: h / dh / ds / C must be [M, 512]");
+  }
+  check_f32(gamma, "gamma");
+  TORCH_CHECK(gamma.numel() == N, "gemm_ln_bwd: gamma [512]");
+  for (auto* t : {&mean, &rstd}) {
+    check_f32(*t, "mean/rstd");
+    TORCH_CHECK(t->numel() >= M, "gemm_ln_bwd: mean / rstd [M]");
+  }
+  check_f32(part, "part");
+  TORCH_CHECK(part.numel() >= 3 * ((M + 127) / 128) * N, "gemm_ln_bwd: partials [3][bands][512]");
+  check_ln_xch(xch, band_ctr, err, M);
+  check_kbits(kbits, M, N);
+  const long long* cp = ctr.has_value() ? reinterpret_cast<const long long*>(ctr->data_ptr<int64_t>()) : nullptr;
+  c10::DeviceGuard g(A.device());
+  check_err(tdg_gemm_ln_bwd(A.data_ptr(), W.data_ptr(), C.has_value() ? C->data_ptr() : nullptr,
+                            h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                            gamma.data_ptr<float>(), dh.data_ptr(),
+                            ds.has_value() ? ds->data_ptr() : nullptr, part.data_ptr<float>(),
+                            (int)M, (int)N, (int)K, (int)A.stride(0), (int)N,
+                            C.has_value() ? 1.f : 0.f, (float)p, (uint64_t)seed, cp,
+                            (uint64_t)site, kbits.has_value() ? kbits->data_ptr() : nullptr,
+                            xch.data_ptr(),
+                            reinterpret_cast<unsigned*>(band_ctr.data_ptr()),
+                            reinterpret_cast<unsigned*>(err.data_ptr()), (int)ln_stages(stages, K),
+                            (int)ablate, stream_of(A)),
+            "tdg gemm_ln_bwd");
 }
 
 void colsum(const Tensor& X, const Tensor& out, const Tensor& part, int64_t M, int64_t N,
@@ -481,7 +614,7 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
             const Tensor& y, const optional<Tensor>& hsave, const optional<Tensor>& mean,
             const optional<Tensor>& rstd, double p, int64_t seed, const optional<Tensor>& ctr,
             int64_t site, double eps, const optional<Tensor>& y8, const optional<Tensor>& s8,
-            const optional<Tensor>& amax8) {
+            const optional<Tensor>& amax8, const optional<Tensor>& kbits) {
   check_bf16(x, "x");
   check_contig(x, "x");
   const int64_t D = x.size(-1), M = x.numel() / D;
@@ -510,6 +643,11 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
     TORCH_CHECK(y8->numel() == x.numel() && y8->is_contiguous() && s8.has_value(), "ln: y8");
     check_f32(*s8, "s8");
   }
+  if (kbits.has_value()) {
+    TORCH_CHECK(kbits->is_cuda() && kbits->scalar_type() == at::kByte && kbits->is_contiguous() &&
+                    kbits->numel() == M * D / 8 && D >= 512 && s.has_value(),
+                "ln: kbits uint8 [M, D / 8] (D >= 512, dropout on s)");
+  }
   c10::DeviceGuard g(x.device());
   const int rc = tdg_ln_fwd(x.data_ptr(), s.has_value() ? s->data_ptr() : nullptr,
                             gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
@@ -518,7 +656,8 @@ void ln_fwd(const Tensor& x, const optional<Tensor>& s, const Tensor& gamma, con
                             rstd.has_value() ? rstd->data_ptr<float>() : nullptr, (int)M, (int)D,
                             (float)p, (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, (float)eps,
                             y8 ? y8->data_ptr() : nullptr, s8 ? s8->data_ptr<float>() : nullptr,
-                            amax_ptr(amax8), stream_of(x));
+                            amax_ptr(amax8), kbits.has_value() ? kbits->data_ptr() : nullptr,
+                            stream_of(x));
   check_err(rc, "tdg ln_fwd");
 }
 
@@ -531,7 +670,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
             const optional<Tensor>& dbias, const Tensor& ws, double p, int64_t seed,
             const optional<Tensor>& ctr, int64_t site, bool accumulate, bool skip_reduce,
             int64_t rpb, const optional<Tensor>& ds8, const optional<Tensor>& s8,
-            const optional<Tensor>& amax8) {
+            const optional<Tensor>& amax8,
+            const optional<Tensor>& kbits) {
   check_bf16(dy, "dy");
   check_contig(dy, "dy");
   const int64_t D = dy.size(-1), M = dy.numel() / D;
@@ -564,6 +704,12 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
   TORCH_CHECK(rpb == 16 || rpb == 32 || rpb == 64, "ln_bwd: rows per block 16 / 32 / 64");
   TORCH_CHECK(ws.numel() >= 3 * ((M + rpb - 1) / rpb) * D, "ln_bwd: workspace too small");
   c10::DeviceGuard g(dy.device());
+  if (kbits.has_value()) {
+    const int64_t D = dy.size(-1), M = dy.numel() / D;
+    TORCH_CHECK(kbits->is_cuda() && kbits->scalar_type() == at::kByte && kbits->is_contiguous() &&
+                    kbits->numel() == M * D / 8 && D >= 512,
+                "ln_bwd: kbits uint8 [M, D / 8] (D >= 512)");
+  }
   const int rc = tdg_ln_bwd(
       dy.data_ptr(), hsave.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
       gamma.data_ptr<float>(), dh.data_ptr(), ds.has_value() ? ds->data_ptr() : nullptr,
@@ -571,7 +717,8 @@ void ln_bwd(const Tensor& dy, const Tensor& hsave, const Tensor& mean, const Ten
       dbeta.data_ptr<float>(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
       ws.data_ptr<float>(), (int)M, (int)D, (float)p, (uint64_t)seed, ctr_ptr(ctr),
       (uint64_t)site, accumulate, skip_reduce, (int)rpb, ds8 ? ds8->data_ptr() : nullptr,
-      s8 ? s8->data_ptr<float>() : nullptr, amax_ptr(amax8), stream_of(dy));
+      s8 ? s8->data_ptr<float>() : nullptr, amax_ptr(amax8),
+      kbits.has_value() ? kbits->data_ptr() : nullptr, stream_of(dy));
   check_err(rc, "tdg ln_bwd");
 }
 
@@ -1207,6 +1354,8 @@ void to_bf16(const Tensor& p, const Tensor& o) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
+  m.def("gemm_ln_fwd", &gemm_ln_fwd);
+  m.def("gemm_ln_bwd", &gemm_ln_bwd);
   m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),

@@ -117,11 +117,22 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
                                            bf16_t* __restrict__ hsave, float* __restrict__ mean_out,
                                            float* __restrict__ rstd_out, float p, uint32_t thresh,
                                            uint64_t seed, const long long* ctr, uint64_t site,
-                                           float eps, RowVec<D / 64>& o, size_t wt_bytes = 0) {
+                                           float eps, RowVec<D / 64>& o, size_t wt_bytes = 0,
+                                           uint8_t* __restrict__ kbits = nullptr) {
   constexpr int VEC = D / 64;
   if (has_t) {
     if (p > 0.f) {
       const uint32_t km = keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
+      if constexpr (VEC >= 8) {
+        // the keep bits as a row-major bitmap (bit c % 8 of byte c / 8 of the
+        // row = column c): the fused LayerNorm backward reads them instead of
+        // regenerating the mask (tdg_gemm_ln.h)
+        if (kbits) {
+#pragma unroll
+          for (int c = 0; c < RowMap<VEC>::CH; ++c)
+            kbits[rbase / 8 + 64 * c + lane] = (uint8_t)(km >> (8 * c));
+        }
+      }
       const float sc = 1.f / (1.f - p);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) t.v[i] = ((km >> i) & 1u) ? t.v[i] * sc : 0.f;

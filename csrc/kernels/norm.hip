@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const float* __restrict__ beta, bf16_t* __restrict__ y, bf16_t* __restrict__ hsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, float p, uint32_t thresh,
     uint64_t seed, const long long* ctr, uint64_t site, float eps, uint8_t* __restrict__ y8,
-    const float* __restrict__ s8p, unsigned* __restrict__ amax8) {
+    const float* __restrict__ s8p, unsigned* __restrict__ amax8, uint8_t* __restrict__ kbits) {
   constexpr int VEC = D / 64;
   const int lane = threadIdx.x & 63;
   const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const size_t rbase = (size_t)row * D;
     RowVec<VEC> o;
     ln_row_fwd<D>(h[k], t[k], s != nullptr, rbase, row, lane, gamma, beta, y, hsave, mean_out,
-                  rstd_out, p, thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t));
+                  rstd_out, p, thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t), kbits);
     if (y8) ln_row_y8<D>(o, s8p[0], y8, rbase, lane, am);
   }
   if (y8) ln_amax_flush(am, red8, amax8);
@@ -109,7 +109,8 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     const bf16_t* __restrict__ dres_in, float* __restrict__ part_g, float* __restrict__ part_b,
     float* __restrict__ part_s, int M, float p, uint32_t thresh, uint64_t seed,
     const long long* ctr, uint64_t site, int iters, uint8_t* __restrict__ ds8,
-    const float* __restrict__ s8p, unsigned* __restrict__ amax8) {
+    const float* __restrict__ s8p, unsigned* __restrict__ amax8,
+    const uint8_t* __restrict__ kbits) {
   constexpr int VEC = D / 64;
   __shared__ float red[NWV][D];
   float am8 = 0.f;  // |ds| max of the e5m2 copy
@@ -131,6 +132,10 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
   if (r0 >= M) break;
   RowVec<VEC> g[RPW], h[RPW], e[RPW];
   float mean[RPW], rstd[RPW];
+  // the forward's keep bits (tdg_ln.h ln_row_fwd kbits; VEC >= 8): one
+  // byte per 8 columns, loaded with the rows instead of regenerating the
+  // Philox mask
+  uint32_t kb[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
     const int row = min(r0 + k, M - 1);
@@ -140,6 +145,13 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     if (dres_in) e[k].load_row(dres_in + rbase, lane);
     mean[k] = mean_in[row];
     rstd[k] = rstd_in[row];
+    kb[k] = 0u;
+    if constexpr (VEC >= 8) {
+      if (kbits) {
+#pragma unroll
+        for (int c = 0; c < RowMap<VEC>::CH; ++c) kb[k] |= (uint32_t)kbits[rbase / 8 + 64 * c + lane] << (8 * c);
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
@@ -164,7 +176,7 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     for (int i = 0; i < VEC; ++i) dh.v[i] = rstd[k] * (g[k].v[i] * gm[i] - sg - xh[i] * sgx);
     RowVec<VEC> ds = dh;
     if (p > 0.f) {
-      const uint32_t km = keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
+      const uint32_t km = (VEC >= 8 && kbits) ? kb[k] : keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) ds.v[i] = ((km >> i) & 1u) ? dh.v[i] * sc : 0.f;
     }
@@ -220,7 +232,7 @@ template <int D>
 void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* beta, void* y,
               void* hsave, float* mean, float* rstd, int M, float p, uint64_t seed,
               const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
-              unsigned* amax8, hipStream_t st) {
+              unsigned* amax8, void* kbits, hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
   // one row per wave measured best with dropout (2 rows: 8.1 vs 8.2 us
   // without, 11.1 vs 9.3 us with, D = 1024 x 8192 rows); a grid-strided
@@ -228,14 +240,14 @@ void ln_fwd_d(const void* x, const void* s, const float* gamma, const float* bet
   // stores the current one) lost 2-9 us per call (profiles/r3s2/ln_fwd_strided.txt)
   hipLaunchKernelGGL((ln_fwd_kernel<D, 1>), dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)s, gamma, beta, (bf16_t*)y, (bf16_t*)hsave, mean, rstd, M, p,
-                     thresh, seed, ctr, site, eps, (uint8_t*)y8, s8, amax8);
+                     thresh, seed, ctr, site, eps, (uint8_t*)y8, s8, amax8, (uint8_t*)kbits);
 }
 template <int D>
 void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float* rstd,
               const float* gamma, void* dh, void* ds, const void* dres, float* dgamma,
               float* dbeta, float* dbias, float* ws, int M, float p, uint64_t seed, const long long* ctr, uint64_t site,
               int accumulate, int skip_reduce, int rpb, void* ds8, const float* s8, unsigned* amax8,
-              hipStream_t st) {
+              const void* kbits, hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
   // rpb rows per block (kernels.py ln_bwd_nparts): 16 on 4 waves, 32 / 64 on
   // 8 waves (fewer partial rows for the fold); RPW rows per wave per pass
@@ -248,12 +260,12 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
     hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                        (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
-                       max(1, rpb / (RPW * 4)), (uint8_t*)ds8, s8, amax8);
+                       max(1, rpb / (RPW * 4)), (uint8_t*)ds8, s8, amax8, (const uint8_t*)kbits);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<D, RPW, 8>), dim3(nb), dim3(512), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)hsave, mean, rstd, gamma, (bf16_t*)dh, (bf16_t*)ds,
                        (const bf16_t*)dres, pg, pb, ps, M, p, thresh, seed, ctr, site,
-                       max(1, rpb / (RPW * 8)), (uint8_t*)ds8, s8, amax8);
+                       max(1, rpb / (RPW * 8)), (uint8_t*)ds8, s8, amax8, (const uint8_t*)kbits);
   if (skip_reduce) return;  // partials folded later by tdg_reduce_partials_multi
   const float beta = accumulate ? 1.f : 0.f;
   ReduceSet rs{{pg, pb, ps}, {dgamma, dbeta, dbias}};
@@ -265,9 +277,10 @@ void ln_bwd_d(const void* dy, const void* hsave, const float* mean, const float*
 extern "C" int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta,
                           void* y, void* hsave, float* mean, float* rstd, int M, int D, float p,
                           uint64_t seed, const long long* ctr, uint64_t site, float eps, void* y8,
-                          const float* s8, unsigned* amax8, hipStream_t st) {
+                          const float* s8, unsigned* amax8, void* kbits, hipStream_t st) {
+  if (kbits && D < 512) return -3;  // keep-bit bitmap: whole bytes per lane (D >= 512)
 #define TDG_LN_F(DD) \
-  ln_fwd_d<DD>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, y8, s8, amax8, st); \
+  ln_fwd_d<DD>(x, s, gamma, beta, y, hsave, mean, rstd, M, p, seed, ctr, site, eps, y8, s8, amax8, kbits, st); \
   return 0;
   switch (D) {
     case 128: TDG_LN_F(128)
@@ -285,12 +298,13 @@ extern "C" int tdg_ln_bwd(const void* dy, const void* hsave, const float* mean, 
                           float* dbeta, float* dbias, float* ws, int M, int D, float p,
                           uint64_t seed, const long long* ctr, uint64_t site, int accumulate,
                           int skip_reduce, int rpb, void* ds8, const float* s8, unsigned* amax8,
-                          hipStream_t st) {
+                          const void* kbits, hipStream_t st) {
   if (rpb != 16 && rpb != 32 && rpb != 64) return -2;
   if (ds8 && !s8) return -2;
+  if (kbits && D < 512) return -3;
 #define TDG_LN_B(DD)                                                                              \
   ln_bwd_d<DD>(dy, hsave, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, M, p, seed, \
-               ctr, site, accumulate, skip_reduce, rpb, ds8, s8, amax8, st);                     \
+               ctr, site, accumulate, skip_reduce, rpb, ds8, s8, amax8, kbits, st);              \
   return 0;
   switch (D) {
     case 128: TDG_LN_B(128)

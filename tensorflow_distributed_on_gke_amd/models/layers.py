@@ -33,6 +33,7 @@ Reference semantics (distributed_training_transformer/transformer_model.py):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -64,6 +65,9 @@ class RunCtx:
     fp8: Optional[object] = None
     # WgradQueue: weight gradients deferred to the end of backward (grouped)
     wgrad: Optional["WgradQueue"] = None
+    # the last post-LN block output whose LayerNorm backward may be fused
+    # into its consumer's dgrad (LnLink), until a consumer claims it
+    ln_out: Optional["LnLink"] = None
 
     @property
     def p(self) -> float:
@@ -81,6 +85,75 @@ class KVGrad:
     the cross-K/V projection backward is a single GEMM pair."""
 
     buf: Optional[torch.Tensor] = None
+
+
+@dataclass(eq=False)
+class LnLink:
+    """A post-LN block output y whose LayerNorm BACKWARD runs in the epilogue
+    of the dgrad that produces y's gradient -- the consumer's last GEMM (the
+    next block's input-projection / FFN1 dgrad, the batched cross K|V dgrad,
+    the vocabulary projection's dgrad; ops.kernels.dgrad_ln_bwd).
+
+    The producing block's forward publishes it (rt.ln_out); the consuming
+    block's forward claims it when its input IS y. In backward the consumer
+    computes (dh, ds) of the producer's LayerNorm and hands them over in
+    `fused`; the producer's backward then skips its own LayerNorm backward
+    (the gradient autograd passes it is that dh). Only on the GPU, bf16,
+    d_model 512, with the deferred weight-gradient queue (whose column-sum
+    folds it joins)."""
+    y: torch.Tensor
+    saved: tuple
+    gamma: Param
+    beta: Param
+    sub_bias: Param
+    site: int
+    fused: Optional[tuple] = None
+
+
+def _ln_linkable(rt: RunCtx, x: torch.Tensor) -> bool:
+    """This LayerNorm's backward will be fused into its consumer's dgrad (its
+    forward then also saves the dropout keep bits)."""
+    return (x.is_cuda and rt.training and rt.wgrad is not None and rt.fp8 is None
+            and K.ln_fused_ok(x.shape[-1]))
+
+
+def _publish_ln(rt: RunCtx, y: torch.Tensor, saved, gamma: Param, beta: Param, sub_bias: Param,
+                site: int) -> Optional[LnLink]:
+    if not (_ln_linkable(rt, y) and saved[3] is None):
+        rt.ln_out = None
+        return None
+    rt.ln_out = LnLink(y, saved, gamma, beta, sub_bias, site)
+    return rt.ln_out
+
+
+def _claim_ln(rt: RunCtx, x: torch.Tensor) -> Optional[LnLink]:
+    link = rt.ln_out
+    if link is not None and link.y is x:
+        rt.ln_out = None
+        return link
+    return None
+
+
+def _dgrad_ln(dy2: torch.Tensor, w: Param, N: int, dres: Optional[torch.Tensor],
+              link: Optional[LnLink], rt: RunCtx) -> torch.Tensor:
+    """The consumer's last dgrad: dx = dy2 @ w (+ dres, the residual gradient
+    already in dx). With a claimed link, the producer's LayerNorm backward
+    runs in the same launch: returns its dh (what autograd passes on as dx)
+    and leaves (dh, ds) in link.fused."""
+    if link is None:
+        if dres is None:
+            return K.linear_dgrad(dy2, w.compute, N)
+        return _dgrad_into(dy2, w, N, dres)
+    q = rt.wgrad
+    h, mean, rstd, _, kbits = link.saved
+    M, D = dy2.shape[0], w.shape[1]
+    dh, ds = K.dgrad_ln_bwd(dy2, w.compute, dres, h, mean, rstd, link.gamma.master, link.gamma.grad,
+                            link.beta.grad, link.sub_bias.grad, rt.p, rt.seed, rt.ctr, link.site,
+                            q.reductions, accumulate=rt.accumulate,
+                            stages=3 if N <= 512 else 4, kbits=kbits)
+    q.reduced_params += [(rt, link.gamma), (rt, link.beta), (rt, link.sub_bias)]
+    link.fused = (dh, ds)
+    return dh.view(M, D)
 
 
 def _keep_scale(rt: RunCtx, site: int, shape, device) -> Optional[torch.Tensor]:
@@ -372,12 +445,34 @@ def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int
     output-projection GEMM (bias fused) then the fused dropout + residual +
     LayerNorm kernel. (A single fused GEMM + LayerNorm launch measured slower
     on MI355X: every workgroup then streams all of W; csrc/lab/gemm_ln.hip.)"""
+    if x.is_cuda and rt.fp8 is None and K.ln_fused_fwd_ok(x.shape[-1]):
+        # one launch: the LayerNorm runs in the GEMM's epilogue
+        kbits = _kbits(rt, x)
+        y, h, mean, rstd = K.linear_ln_fwd(a2, w.compute, b.master, x.contiguous(), gamma.master,
+                                           beta.master, rt.p, rt.seed, rt.ctr, site, eps=LN_EPS,
+                                           stages=3, kbits=kbits)
+        return y.view(x.shape), (h.view(x.shape), mean, rstd, None, kbits)
     s = K.linear_fwd(a2, w.compute, b.master)
     return _ln_fwd(x, s.view(x.shape), gamma, beta, site, rt)
 
 
+# the training forward's LayerNorms save their dropout keep bits (1 bit per
+# element) for the backward, which reads them instead of regenerating the
+# Philox mask (ln_bwd / dgrad_ln_bwd kbits)
+LN_KEEP_BITS = os.environ.get("TDG_LN_KEEP_BITS", "1") != "0"
+
+
+def _kbits(rt: RunCtx, x: torch.Tensor) -> Optional[torch.Tensor]:
+    """Keep-bit bitmap [M, D / 8] of a training LayerNorm with dropout."""
+    D = x.shape[-1]
+    if LN_KEEP_BITS and x.is_cuda and rt.training and rt.p > 0 and D % 512 == 0:
+        return torch.empty(x.numel() // D, D // 8, dtype=torch.uint8, device=x.device)
+    return None
+
+
 def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
-    """Returns (y, saved) for y = LN(x + dropout(s))."""
+    """Returns (y, saved) for y = LN(x + dropout(s)); saved = (h, mean, rstd,
+    CPU keep scale, GPU keep bits)."""
     if x.is_cuda:
         y8 = s8 = a8 = None
         slot = rt.fp8.ln_slots.get(id(gamma)) if rt.fp8 is not None else None
@@ -385,24 +480,31 @@ def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
             y8 = torch.empty(x.shape, dtype=fp8.FP8, device=x.device)
             s8, a8 = rt.fp8.meta.s(slot), rt.fp8.meta.a(slot)
             rt.fp8.stash[slot] = y8
+        kbits = _kbits(rt, x)
         y, h, mean, rstd = K.ln_fwd(x.contiguous(), s.contiguous(), gamma.master, beta.master,
-                                    rt.p, rt.seed, rt.ctr, site, y8=y8, s8=s8, amax8=a8)
-        return y, (h, mean, rstd, None)
+                                    rt.p, rt.seed, rt.ctr, site, y8=y8, s8=s8, amax8=a8, kbits=kbits)
+        return y, (h, mean, rstd, None, kbits)
     ks = _keep_scale(rt, site, s.shape, s.device)
     h = x + (s * ks if ks is not None else s)
     mean = h.mean(-1, keepdim=True)
     rstd = torch.rsqrt(((h - mean) ** 2).mean(-1, keepdim=True) + LN_EPS)
-    return (h - mean) * rstd * gamma.master + beta.master, (h, mean, rstd, ks)
+    return (h - mean) * rstd * gamma.master + beta.master, (h, mean, rstd, ks, None)
 
 
 def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt: RunCtx,
-            ds8_slot: Optional[int] = None):
+            ds8_slot: Optional[int] = None, link: Optional[LnLink] = None):
     """Returns (dh, ds): dh = dL/d(residual input) (fresh, writable), ds =
     dL/d(sublayer output). Also writes dgamma, dbeta and the sublayer's output
     bias gradient (sum of ds over rows). ds8_slot (GPU, fp8 backward): ds is
     returned as its e5m2 copy only (scale slot ds8_slot of rt.fp8.gmeta,
     amax recorded), the bf16 ds is not written."""
-    h, mean, rstd, ks = saved
+    if link is not None and link.fused is not None:
+        # already computed by the consumer's dgrad epilogue (_dgrad_ln); its
+        # column-sum folds are queued and the parameters reported there
+        dh, ds = link.fused
+        link.fused = None
+        return dh.view(dy.shape), ds.view(dy.shape)
+    h, mean, rstd, ks = saved[:4]
     if dy.is_cuda:
         q = rt.wgrad
         ds8 = s8 = a8 = None
@@ -413,7 +515,7 @@ def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt
         dh, ds = K.ln_bwd(dy.contiguous(), h, mean, rstd, gamma.master, gamma.grad, beta.grad,
                           sub_bias.grad, rt.p, rt.seed, rt.ctr, site, want_ds=ds8 is None,
                           accumulate=rt.accumulate, defer=q.reductions if q is not None else None,
-                          ds8=ds8, s8=s8, amax8=a8)
+                          ds8=ds8, s8=s8, amax8=a8, kbits=saved[4])
         if ds8 is not None:
             ds = ds8
         if q is not None:  # folded (and reported ready) with the next wgrad flush
@@ -518,6 +620,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(hd)
         ctx.p = (wqkv, bqkv, wo, bo, gamma, beta)
         ctx.meta = (heads, causal, scale, site, rt)
+        ctx.in_link = _claim_ln(rt, x)
         x2 = x.reshape(B * L, d)
         ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * L, wqkv, wo, d)
         kx = [] if lean else None
@@ -555,6 +658,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(o.view(B * L, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
+        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, bo, site)
         ctx.save_for_backward(x2, qkv, o, aux, kv_len)
         return y
 
@@ -569,7 +673,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
         bt = _beta(rt)
         if ctx.lean:
             return SelfAttnBlockFn._backward_fp8(ctx, dy)
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, link=ctx.out_link)
         ds2 = ds.reshape(M, d)
         q5 = qkv.view(B, L, 3, heads, hd)
         if dy.is_cuda:
@@ -580,7 +684,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
             _wgrad(rt, dqkv, x2, 3 * d, wqkv, bqkv)
-            dx = _dgrad_into(dqkv, wqkv, 3 * d, dh)
+            dx = _dgrad_ln(dqkv, wqkv, 3 * d, dh, ctx.in_link, rt)
             if rt.wgrad is not None:
                 rt.wgrad.layer_end()  # self-attention is a layer's first block
             return (dx.view(B, L, d),) + (None,) * 11
@@ -652,6 +756,7 @@ class CrossKVFn(torch.autograd.Function):
         e2 = enc.reshape(B * S, d)
         ctx.p = (wkv, bkv)
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
+        ctx.in_link = _claim_ln(rt, enc)
         ctx.save_for_backward(e2)
         ctx.lean = lean = enc.is_cuda and _attn_lean(rt, B * S, wkv, None, d)
         kx = [] if lean else None
@@ -701,7 +806,7 @@ class CrossKVFn(torch.autograd.Function):
             _wgrad(rt, dkv, e2, N, wkv, bkv)
             if rt.wgrad is not None:
                 rt.wgrad.boundary()  # every decoder layer's backward is done
-            denc = K.linear_dgrad(dkv, wkv.compute, N)
+            denc = _dgrad_ln(dkv, wkv, N, None, ctx.in_link, rt)
         else:
             _write_grad(wkv, dkv.t() @ e2, rt)
             _write_grad(bkv, dkv.sum(0), rt)
@@ -727,6 +832,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(hd)
         ctx.p = (wq, bq, wo, bo, gamma, beta)
         ctx.meta = (heads, scale, site, rt, layer, kvh)
+        ctx.in_link = _claim_ln(rt, x)
         x2 = x.reshape(B * T, d)
         kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd) \
             if kv_all.is_contiguous() else None
@@ -772,6 +878,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(o.view(B * T, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
+        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, bo, site)
         ctx.save_for_backward(x2, kv_all, q, o, aux, kv_len)
         return y
 
@@ -822,7 +929,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)
             dkv_ret = dkv_all if layer == 0 else None
             return (dh.view(B, T, d), dkv_ret) + (None,) * 12
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, link=ctx.out_link)
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:
             _wgrad(rt, ds2, o.view(M, d), d, wo)
@@ -844,7 +951,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             _write_grad(wq, dq.t() @ x2, rt)
             _write_grad(bq, dq.sum(0), rt)
             _ready(rt, wq, bq)  # (GPU: reported by _wgrad / the deferred flush)
-        dx = _dgrad_into(dq, wq, d, dh)
+        dx = _dgrad_ln(dq, wq, d, dh, ctx.in_link, rt)
         # Only layer 0 hands the (by then complete) shared buffer to autograd;
         # the other layers contribute through the side channel, so no adds.
         dkv_ret = dkv_all if layer == 0 else None
@@ -862,6 +969,7 @@ class FFNBlockFn(torch.autograd.Function):
         x2 = x.reshape(B * L, d)
         ctx.p = (w1, b1, w2, b2, gamma, beta)
         ctx.meta = (site, rt)
+        ctx.in_link = _claim_ln(rt, x)
         ctx.f8 = None
         ctx.lean = False
         if x.is_cuda and rt.fp8 is not None:
@@ -894,6 +1002,7 @@ class FFNBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(h, w2, b2, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, f.view(B, L, d), gamma, beta, site, rt)
+        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, b2, site)
         ctx.save_for_backward(x2, h if h is not None else x2)  # (lean: h unused)
         return y
 
@@ -908,7 +1017,8 @@ class FFNBlockFn(torch.autograd.Function):
         f8w = ctx.lean
         bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if (dy.is_cuda and rt.fp8 is not None) else None
         # lean fp8 backward: the LayerNorm backward emits ds directly in e5m2
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt, ds8_slot=bw[0] if f8w else None)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt, ds8_slot=bw[0] if f8w else None,
+                         link=ctx.out_link)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
             if not f8w:
@@ -953,7 +1063,7 @@ class FFNBlockFn(torch.autograd.Function):
             else:
                 dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
             _wgrad(rt, dpre, x2, ff, w1, b1)
-            dx = _dgrad_into(dpre, w1, ff, dh)
+            dx = _dgrad_ln(dpre, w1, ff, dh, ctx.in_link, rt)
             return (dx.view(B, L, d),) + (None,) * 8
         else:
             _write_grad(w2, ds2.t() @ h, rt)

@@ -20,7 +20,8 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from tensorflow_distributed_on_gke_amd.models.layers import (_wgrad, CrossAttnBlockFn, CrossKVFn, EmbedFn,
+from tensorflow_distributed_on_gke_amd.models.layers import (_claim_ln, _dgrad_ln, _wgrad,
+                                                              CrossAttnBlockFn, CrossKVFn, EmbedFn,
                                                               FFNBlockFn, KVGrad, RunCtx,
                                                               SelfAttnBlockFn)
 from tensorflow_distributed_on_gke_amd.models.params import (ParamStore, TFSlot, const,
@@ -261,6 +262,7 @@ class Transformer:
 
     def features(self, src, tgt_in, rt: RunCtx, lengths=None):
         src_len, tgt_len = lengths if lengths is not None else (seq_lengths(src), seq_lengths(tgt_in))
+        rt.ln_out = None  # (a link of a previous forward is never claimed by this one)
         enc = self.encode(src, src_len, rt)
         return self.decode(tgt_in, enc, src_len, tgt_len, rt)
 
@@ -317,6 +319,9 @@ class Transformer:
         grad_ctx = torch.enable_grad() if backward else torch.no_grad()
         with grad_ctx:
             dec = self.features(src, tgt_in, rt, lengths)
+        # the decoder's last LayerNorm: its backward may run in the vocabulary
+        # projection's dgrad epilogue (layers.LnLink)
+        dec_link = _claim_ln(rt, dec) if backward else None
         dec2 = dec.detach().reshape(M, cfg.d_model)
         if dev.type == "cuda":
             logits = self.project(dec.detach())
@@ -332,7 +337,7 @@ class Transformer:
             beta = 1.0 if rt.accumulate else 0.0
             dl = logits  # now holds dlogits (pad columns zeroed)
             _wgrad(rt, dl, dec2.contiguous(), cfg.tgt_vocab, self.final.w, self.final.b)
-            ddec = K.linear_dgrad(dl, self.final.w.compute, cfg.tgt_vocab)
+            ddec = _dgrad_ln(dl, self.final.w, cfg.tgt_vocab, None, dec_link, rt)
         else:
             lg = self.project(dec.detach())
             lab = labels.reshape(-1)

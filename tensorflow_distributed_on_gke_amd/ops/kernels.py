@@ -387,12 +387,16 @@ def attn_bwd_g8_ok(Lq: int, Lk: int, hd: int) -> bool:
 
 def attn_bwd_g8(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bool, dq8,
                 dk8, dv8, sg8, amax8, cs_part, cs_ld: int, cs_q: int, cs_k: int, cs_v: int,
-                skip_bf16: bool = True) -> int:
+                skip_bf16: Optional[bool] = None) -> int:
     """attn_bwd that also writes e5m2 copies dq8 (dk8 / dv8 optional, same
     layout as dq / dk / dv) = e5m2(bf16(grad) * sg8), their amax into the
     slot amax8, and the bias-gradient column-sum partials cs_part[B *
     nblocks, cs_ld] (columns cs_q / cs_k / cs_v + head * 64 + j). skip_bf16:
-    the bf16 dq / dk / dv are not written. Returns the partial row count."""
+    the bf16 dq / dk / dv are not written (default: when the e5m2 dk8 / dv8
+    are requested -- without them the bf16 dK / dV are the output and must be
+    written). Returns the partial row count."""
+    if skip_bf16 is None:
+        skip_bf16 = dk8 is not None
     B, Lq = q.shape[0], q.shape[1]
     np_ = -(-Lq // 128)
     delta = workspace("attn_delta", lse.numel(), q.device)[: lse.numel()]
@@ -411,16 +415,17 @@ def attn_probs(q, k, kv_len, scale: float, causal: bool) -> torch.Tensor:
 
 # ------------------------------------------------------------------ layernorm
 def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, s8=None,
-           amax8=None):
+           amax8=None, kbits=None):
     """y = LN(x + dropout(s)); optionally also y8 = e4m3(y * s8) (fp8 copy,
-    amax recorded into amax8)."""
+    amax recorded into amax8) and kbits (uint8 [M, D / 8]): the dropout keep
+    mask as a row-major bitmap for a fused backward (dgrad_ln_bwd)."""
     D = x.shape[-1]
     M = x.numel() // D
     y = torch.empty_like(x)
     h = torch.empty_like(x) if save else None
     mean = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
     rstd = torch.empty(M, dtype=torch.float32, device=x.device) if save else None
-    C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps, y8, s8, amax8)
+    C().ln_fwd(x, s, gamma, beta, y, h, mean, rstd, p, seed, ctr, site, eps, y8, s8, amax8, kbits)
     return y, h, mean, rstd
 
 
@@ -443,13 +448,15 @@ def ln_bwd_nparts(M: int, D: int) -> int:
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, want_ds=True,
-           dres=None, accumulate=False, defer=None, ds8=None, s8=None, amax8=None):
+           dres=None, accumulate=False, defer=None, ds8=None, s8=None, amax8=None, kbits=None):
     """`defer` (a list): leave the dgamma / dbeta / dbias partial sums in a
     per-site workspace and append their fold to `defer` (run later, all
     LayerNorms of a backward in one launch, by reduce_partials_multi).
     ds8 (e5m2, shape of dy) with scale s8 / amax slot amax8: also the e5m2
     copy of ds for an fp8 backward; with want_ds=False the bf16 ds is then
-    not written at all (the bias column sums still come from ds)."""
+    not written at all (the bias column sums still come from ds). kbits
+    (uint8 [M, D / 8], from ln_fwd): the dropout mask read instead of
+    regenerated."""
     D = dy.shape[-1]
     M = dy.numel() // D
     dh = torch.empty_like(dy)
@@ -460,7 +467,7 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
     else:  # partials must survive until the fold: one workspace per site
         ws = workspace(f"ln_bwd_part_{site}", 3 * ln_bwd_nparts(M, D) * D, dy.device)
     C().ln_bwd(dy, h, mean, rstd, gamma, dh, ds, dres, dgamma, dbeta, dbias, ws, p, seed, ctr, site,
-               accumulate, defer is not None, ln_bwd_rpb(D), ds8, s8, amax8)
+               accumulate, defer is not None, ln_bwd_rpb(D), ds8, s8, amax8, kbits)
     if defer is not None:
         nb = ln_bwd_nparts(M, D)
         outs = [dgamma, dbeta] + ([dbias] if dbias is not None else [])
@@ -468,6 +475,109 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
             defer.append((ws[i * nb * D:(i + 1) * nb * D], o, nb, D, 1.0 if accumulate else 0.0))
     if ds is None:
         ds = dh
+    return dh, ds
+
+
+# Post-LN block tails fused into the d_model-wide GEMMs (csrc/include/tdg_gemm_ln.h):
+# the forward LayerNorm in the epilogue of the output projection / FFN2, the
+# LayerNorm backward in the epilogue of the dgrad that produces its input
+# gradient -- no separate ln_fwd / ln_bwd launch and no round trip of the
+# pre-LN sum / the LayerNorm input gradient through memory. d_model 512.
+# "0" (default): neither -- measured on MI355X, the fused tails cost more in
+# the GEMM epilogue (band-exchange latency, dropout mask, the second output
+# store, all serialised behind the main loop at 8 waves per CU) than the
+# separate LayerNorm launches they remove: headline step 4.84-4.86 ms
+# unfused vs 4.88-4.90 backward-fused vs 5.06-5.08 both (scripts/ln_fused_lab.py,
+# profiles/r5/ln_fused_ab.txt). "bwd": the backward only; "all": both.
+LN_FUSED = os.environ.get("TDG_LN_FUSED", "0")
+LN_FUSED_D = 512
+# lab only (scripts/ln_fused_lab.py): epilogue parts switched off (tdg_gemm_ln.h)
+LN_ABLATE = int(os.environ.get("TDG_LN_ABLATE", "0"))
+
+
+def _ln_mode() -> str:
+    v = LN_FUSED
+    if v is True or v == "1":
+        return "all"
+    if v is False or v is None:
+        return "0"
+    return str(v)
+
+
+def ln_fused_ok(D: int) -> bool:
+    """The LayerNorm backward of a d_model-D block runs in its consumer's dgrad."""
+    return _ln_mode() in ("bwd", "all") and D == LN_FUSED_D
+
+
+def ln_fused_fwd_ok(D: int) -> bool:
+    """The LayerNorm forward runs in the producing GEMM's epilogue."""
+    return _ln_mode() == "all" and D == LN_FUSED_D
+
+
+def _ln_xch(M: int, device):
+    """Band-exchange state of the fused launches: per-row partial pairs,
+    per-band arrival counters (monotonic, never reset: they must stay at a
+    multiple of 4 between launches, so they are allocated zeroed once and
+    only ever grown by reallocation) and the spin-failure flag."""
+    bands = -(-M // 128)
+    xch = workspace("ln_xch", bands * 128 * 4 * 2, device)
+    dev = torch.device(device)
+    key = (dev.index or 0, "ln_xch_state")
+    st = _WS.get(key)
+    if st is None or st[0].numel() < bands:
+        st = (torch.zeros(max(bands, 256), dtype=torch.int32, device=dev),
+              torch.zeros(1, dtype=torch.int32, device=dev))
+        _WS[key] = st
+    return xch, st[0], st[1]
+
+
+def ln_xch_check() -> None:
+    """Raise if a fused LayerNorm launch ever gave up waiting for a band
+    partner (bounded spin; its outputs were then wrong). Reads device flags: a
+    host sync -- tests and log points only."""
+    for k, v in list(_WS.items()):
+        if isinstance(k, tuple) and len(k) == 2 and k[1] == "ln_xch_state":
+            if int(v[1].item()):
+                raise RuntimeError("fused LayerNorm: a band exchange timed out (outputs invalid)")
+
+
+def linear_ln_fwd(a2, w, bias, x, gamma, beta, p, seed, ctr, site, eps=1e-6, stages=0, kbits=None):
+    """y, h, mean, rstd of y = LN(x + dropout(a2 @ w^T + bias)) in ONE launch
+    (the GEMM's epilogue; bitwise the unfused GEMM's bf16 s, the LayerNorm
+    statistics combined from per-tile partials)."""
+    M = a2.shape[0]
+    D = w.shape[0]
+    y = torch.empty(M, D, dtype=torch.bfloat16, device=a2.device)
+    h = torch.empty_like(y)
+    mean = torch.empty(M, dtype=torch.float32, device=a2.device)
+    rstd = torch.empty_like(mean)
+    xch, bctr, err = _ln_xch(M, a2.device)
+    C().gemm_ln_fwd(a2, w, bias, x.reshape(M, D), gamma, beta, y, h, mean, rstd, p, seed, ctr, site,
+                    eps, kbits, xch, bctr, err, stages, LN_ABLATE)
+    return y, h, mean, rstd
+
+
+def dgrad_ln_bwd(dy2, w, c, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site,
+                 defer, accumulate=False, stages=0, kbits=None):
+    """LayerNorm backward fused into the dgrad that produces its input
+    gradient dy = dy2 @ w (+ c, the residual gradient): returns (dh, ds).
+    The dgamma / dbeta / dbias column partials go to a per-site workspace
+    and their folds are appended to `defer` (reduce_partials_multi)."""
+    M = dy2.shape[0]
+    D = w.shape[1]
+    dh = torch.empty(M, D, dtype=torch.bfloat16, device=dy2.device)
+    # ds is its own tensor even without dropout: the caller accumulates the
+    # next dgrad into dh while deferred weight gradients still read ds
+    ds = torch.empty_like(dh)
+    nb = -(-M // 128)
+    part = workspace(f"ln_fbwd_part_{site}", 3 * nb * D, dy2.device)
+    xch, bctr, err = _ln_xch(M, dy2.device)
+    C().gemm_ln_bwd(dy2, w, c.reshape(M, D) if c is not None else None, h.reshape(M, D), mean, rstd,
+                    gamma, dh, ds, part, p, seed, ctr, site, kbits, xch, bctr, err, stages,
+                    LN_ABLATE)
+    b = 1.0 if accumulate else 0.0
+    for i, o in enumerate((dgamma, dbeta, dbias)):
+        defer.append((part[i * nb * D:(i + 1) * nb * D], o, nb, D, b))
     return dh, ds
 
 

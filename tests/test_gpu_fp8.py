@@ -559,9 +559,16 @@ def test_attn_bwd_emits_e5m2_grads(causal, L, S, kv):
     dk8 = torch.empty(k.shape, dtype=torch.float8_e5m2, device=DEV) if kv else None
     dv8 = torch.empty(v.shape, dtype=torch.float8_e5m2, device=DEV) if kv else None
     part = torch.full((B * -(-L // 128) * ncol,), float("nan"), device=DEV)
+    if not kv:  # skipping the bf16 dK / dV without their e5m2 copies would leave no output
+        with pytest.raises(RuntimeError, match="skip_bf16 needs dk8"):
+            kk.attn_bwd_g8(q, k, v, o, do, lse, dq2, dk2, dv2, kv_len, scale, causal, dq8, None,
+                           None, gm.s(i), gm.a(i), part, ncol, 0, d, 2 * d, skip_bf16=True)
     np_ = kk.attn_bwd_g8(q, k, v, o, do, lse, dq2, dk2, dv2, kv_len, scale, causal, dq8, dk8, dv8,
-                         gm.s(i), gm.a(i), part, ncol, 0, d, 2 * d, skip_bf16=True)
-    assert bool((dq2 == 7.0).all()) and bool((dk2 == 7.0).all())  # bf16 outputs skipped
+                         gm.s(i), gm.a(i), part, ncol, 0, d, 2 * d)
+    if kv:
+        assert bool((dq2 == 7.0).all()) and bool((dk2 == 7.0).all())  # bf16 outputs skipped
+    else:  # (default) the bf16 dK / dV are the output
+        assert torch.equal(dk2, dk) and torch.equal(dv2, dv)
 
     def e5(x):
         return (x.float() * 2.0 ** 12).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
