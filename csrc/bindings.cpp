@@ -24,6 +24,7 @@ int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
 int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
+int tdg_attn_bwd_f8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
                const long long* ctr, uint64_t site, float eps, void* y8, const float* s8,
@@ -564,6 +565,120 @@ void attn_bwd_g8(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor
   a.skip_bf16 = skip_bf16 ? 1 : 0;
   c10::DeviceGuard g(q.device());
   check_err(tdg_attn_bwd(&a, 64, stream_of(q)), "tdg attn_bwd_g8");
+}
+
+// fp8 attention backward (attention.hip attn_bwd_f8_kernel): e4m3 q8/k8/v8
+// (the forward's operands, scales sq/sk/sv), e5m2 do8 (scale sdo), bf16 o,
+// the forward's lse; dS quantised with sds (amax into amaxds). Outputs, each
+// written when given: bf16 dq/dk/dv, e5m2 dq8/dk8/dv8 (scale sg8, amax into
+// amaxg8), and one row per batch of bias-gradient column sums of the e5m2
+// outputs in cs_part[b * cs_ld + cs_{q,k,v} + h * 64 + col] (cs_np = 1).
+void attn_bwd_f8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Tensor& sq,
+                 const Tensor& sk, const Tensor& sv, const Tensor& o, const Tensor& do8,
+                 const Tensor& sdo, const Tensor& lse, const optional<Tensor>& kv_len, double scale,
+                 bool causal, const Tensor& sds, const Tensor& amaxds, const optional<Tensor>& dq,
+                 const optional<Tensor>& dk, const optional<Tensor>& dv, const optional<Tensor>& dq8,
+                 const optional<Tensor>& dk8, const optional<Tensor>& dv8,
+                 const optional<Tensor>& sg8, const optional<Tensor>& amaxg8,
+                 const optional<Tensor>& cs_part, int64_t cs_ld, int64_t cs_q, int64_t cs_k,
+                 int64_t cs_v) {
+  auto rows16 = [](const Tensor& t, const char* n) {
+    TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.size(3) == 64, n, ": [B,L,H,64] with hd contiguous");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0 && t.stride(0) % 16 == 0 &&
+                    t.stride(1) % 16 == 0 && t.stride(2) % 16 == 0,
+                n, ": rows must be 16-byte aligned");
+  };
+  for (auto* t : {&q8, &k8, &v8}) {
+    check_f8_fmt(*t, 0, "attn_bwd_f8 q8/k8/v8");
+    rows16(*t, "attn_bwd_f8 q8/k8/v8");
+  }
+  check_f8_fmt(do8, 1, "attn_bwd_f8 do8");
+  rows16(do8, "attn_bwd_f8 do8");
+  tdg::AttnArgs a{};
+  a.B = (int)q8.size(0);
+  a.Lq = (int)q8.size(1);
+  a.H = (int)q8.size(2);
+  a.Lk = (int)k8.size(1);
+  TORCH_CHECK(k8.size(0) == a.B && v8.size(0) == a.B && k8.size(2) == a.H && v8.size(2) == a.H &&
+                  v8.size(1) == a.Lk && do8.sizes() == q8.sizes(),
+              "attn_bwd_f8: q/k/v/do shape mismatch");
+  TORCH_CHECK(a.Lq <= 512 && a.Lk <= 512, "attn_bwd_f8: Lq, Lk <= 512 (all keys in one workgroup)");
+  a.q = (const uint16_t*)q8.data_ptr();
+  a.k = (const uint16_t*)k8.data_ptr();
+  a.v = (const uint16_t*)v8.data_ptr();
+  a.q_sb = q8.stride(0); a.q_sl = q8.stride(1); a.q_sh = (int)q8.stride(2);
+  a.k_sb = k8.stride(0); a.k_sl = k8.stride(1); a.k_sh = (int)k8.stride(2);
+  a.v_sb = v8.stride(0); a.v_sl = v8.stride(1); a.v_sh = (int)v8.stride(2);
+  a.dout = (const uint16_t*)do8.data_ptr();
+  a.do_sb = do8.stride(0); a.do_sl = do8.stride(1); a.do_sh = (int)do8.stride(2);
+  check_like(o, a, a.Lq, "o");
+  a.o = (const uint16_t*)o.data_ptr();
+  a.o_sb = o.stride(0); a.o_sl = o.stride(1); a.o_sh = (int)o.stride(2);
+  check_f32(lse, "lse");
+  check_contig(lse, "lse");
+  TORCH_CHECK(lse.numel() == (int64_t)a.B * a.H * a.Lq, "lse must be [B,H,Lq]");
+  a.lse = lse.data_ptr<float>();
+  for (auto* t : {&sq, &sk, &sv, &sdo, &sds}) check_f32(*t, "fp8 scale");
+  a.sq8 = sq.data_ptr<float>();
+  a.sk8 = sk.data_ptr<float>();
+  a.sv8 = sv.data_ptr<float>();
+  a.sdo8 = sdo.data_ptr<float>();
+  a.sds8 = sds.data_ptr<float>();
+  a.amaxds8 = amax_ptr(amaxds);
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.scale = (float)scale;
+  a.causal = causal;
+  // outputs: a bf16 / e5m2 pair shares its strides (one set per gradient)
+  auto out = [&](const optional<Tensor>& x, const optional<Tensor>& x8, int L, const char* n,
+                 uint16_t*& p, uint8_t*& p8, long long& sb, long long& sl, int& sh) {
+    TORCH_CHECK(x.has_value() || x8.has_value(), "attn_bwd_f8: no output for ", n);
+    const Tensor& ref = x.has_value() ? *x : *x8;
+    if (x.has_value()) {
+      check_like(*x, a, L, n);
+      p = (uint16_t*)x->data_ptr();
+    }
+    if (x8.has_value()) {
+      check_f8_fmt(*x8, 1, n);
+      TORCH_CHECK(x8->dim() == 4 && x8->size(0) == a.B && x8->size(1) == L && x8->size(2) == a.H &&
+                      x8->size(3) == 64 && x8->stride(3) == 1 &&
+                      (reinterpret_cast<uintptr_t>(x8->data_ptr()) % 4) == 0 &&
+                      x8->stride(1) % 4 == 0 && x8->stride(2) % 4 == 0 && x8->stride(0) % 4 == 0,
+                  n, ": e5m2 copy [B,L,H,64], 4-byte aligned rows");
+      TORCH_CHECK(!x.has_value() || x8->strides() == x->strides(), n, ": bf16 and e5m2 strides differ");
+      p8 = (uint8_t*)x8->data_ptr();
+    }
+    sb = ref.stride(0); sl = ref.stride(1); sh = (int)ref.stride(2);
+  };
+  out(dq, dq8, a.Lq, "dq", a.dq, a.dq8, a.dq_sb, a.dq_sl, a.dq_sh);
+  out(dk, dk8, a.Lk, "dk", a.dk, a.dk8, a.dk_sb, a.dk_sl, a.dk_sh);
+  out(dv, dv8, a.Lk, "dv", a.dv, a.dv8, a.dv_sb, a.dv_sl, a.dv_sh);
+  TORCH_CHECK(dk8.has_value() == dv8.has_value(), "attn_bwd_f8: dk8 and dv8 together");
+  TORCH_CHECK(!dk8.has_value() || dq8.has_value(), "attn_bwd_f8: dk8 / dv8 need dq8");
+  if (dq8.has_value()) {
+    TORCH_CHECK(sg8.has_value() && amaxg8.has_value(), "attn_bwd_f8: e5m2 outputs need sg8 and amaxg8");
+    check_f32(*sg8, "sg8");
+    a.sg8 = sg8->data_ptr<float>();
+    a.amaxg8 = amax_ptr(amaxg8);
+  }
+  if (cs_part.has_value()) {
+    TORCH_CHECK(dq8.has_value(), "attn_bwd_f8: column sums come with the e5m2 outputs");
+    check_f32(*cs_part, "cs_part");
+    TORCH_CHECK(cs_part->numel() >= (int64_t)a.B * cs_ld && cs_q >= 0 && cs_q + a.H * 64 <= cs_ld &&
+                    (!dk8.has_value() || (cs_k >= 0 && cs_v >= 0 && cs_k + a.H * 64 <= cs_ld &&
+                                          cs_v + a.H * 64 <= cs_ld)),
+                "attn_bwd_f8: column-sum partial extent");
+    a.cs_part = cs_part->data_ptr<float>();
+    a.cs_np = 1;
+    a.cs_ld = (int)cs_ld;
+    a.cs_q = (int)cs_q;
+    a.cs_k = (int)cs_k;
+    a.cs_v = (int)cs_v;
+  }
+  c10::DeviceGuard g(q8.device());
+  check_err(tdg_attn_bwd_f8(&a, 64, stream_of(q8)), "tdg attn_bwd_f8");
 }
 
 void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
@@ -1379,6 +1494,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd_fp8", &attn_fwd_fp8);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_g8", &attn_bwd_g8);
+  m.def("attn_bwd_f8", &attn_bwd_f8);
   m.def("attn_probs", &attn_probs);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

@@ -46,5 +46,12 @@ struct AttnArgs {
   float* cs_part;
   int cs_np, cs_ld, cs_q, cs_k, cs_v;
   int skip_bf16;
+  // fp8 backward (attn_bwd_f8_kernel): dout points at the e5m2 dO = e5m2(dO *
+  // sdo8[0]); dS is quantised e5m2(dS * sds8[0]) with its |max| recorded into
+  // the slot amaxds8 (delayed scaling: the next step's sds8). The bf16 dq / dk
+  // / dv and the e5m2 dq8 / dk8 / dv8 are each written when non-null.
+  const float* sdo8;
+  const float* sds8;
+  unsigned* amaxds8;
 };
 }  // namespace tdg

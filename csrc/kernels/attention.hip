@@ -1844,6 +1844,438 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
 #endif
 }
 
+// ============================================================================ backward, e4m3 / e5m2
+// BASELINE config 5's fp8 attention backward (reference: the autograd of
+// transformer_model.py:73-109). Operands: the e4m3 Q / K / V the forward ran
+// on (scales sq, sk, sv), the e5m2 dO (sdo8), P as e4m3(448 P) and dS as
+// e5m2(dS * sds8) -- five products on v_mfma_f32_16x16x32_{fp8,bf8}_{fp8,bf8}:
+//   S^T = K Q^T, dP^T = V dO^T, dV^T += dO^T P, dK^T += Q^T dS, dQ = dS K,
+// softmax recomputed in f32 from the forward's log2-domain LSE.
+// One workgroup per (batch, head) holds ALL of its <= 512 keys -- the e4m3
+// K image is 32 KiB and a wave's K / V fragments 32 registers, half the bf16
+// footprint -- so P and dS are computed once (the bf16 path recomputes them
+// in a dQ kernel and a dK/dV kernel) and dQ needs no sum across workgroups.
+// NW waves; wave w owns the 16-key subtiles s = w + NW u (u < U = 32 / NW:
+// interleaved, so causal work stays balanced) with their dK^T / dV^T in
+// accumulators. Per step of 32 queries (Q / dO tiles register-prefetched into
+// a 2-slot LDS ring):
+//  * S^T, dP^T with the key on the lane: lane cl of query half j reads the
+//    Q / dO image row 8 (cl >> 2) + 4 j + (cl & 3), so accumulator register r
+//    of lane group g is query 8 g + 4 j + r and the two halves' P / dS pack
+//    into the e4m3 / e5m2 B operand of dV^T / dK^T as they stand (queries
+//    8 g .. 8 g + 7 of the lane); dO^T / Q^T A operands by ds_read_b64_tr_b8;
+//  * dS^T goes to a [key][32 queries] e5m2 image (double-buffered), and the
+//    next step computes this step's dQ = dS K from it and the K image (both
+//    operands transposing reads): one barrier per step.
+// delta = rowsum(dO O) from the e5m2 dO actually used and the bf16 O
+// (consistent with dP) in the prologue, with lse, for all queries in LDS.
+// Swizzles (8-byte chunk c of row r): K image c ^ 2 ((r >> 2) & 3); Q / dO
+// images c ^ 2 (((r >> 2) ^ (r >> 4)) & 3) (conflict-free for both the
+// permuted row reads and the transposing reads); dS image c ^ 2 ((r >> 3) & 1).
+__device__ __forceinline__ int f8k_off(int r, int c) { return r * 64 + 8 * (c ^ (2 * ((r >> 2) & 3))); }
+__device__ __forceinline__ int f8q_off(int r, int c) {
+  return r * 64 + 8 * (c ^ (2 * (((r >> 2) ^ (r >> 4)) & 3)));
+}
+__device__ __forceinline__ int f8s_off(int r, int c) { return r * 32 + 8 * (c ^ (2 * ((r >> 3) & 1))); }
+__device__ __forceinline__ long lds_tr8(const char* p) { return lds_read_tr8_async(p); }
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
+  constexpr int LMAX = 512, QT = 32, U = 32 / NW, NT = NW * 64;
+  constexpr int KIMG = LMAX * 64, QIMG = QT * 64, SIMG = LMAX * QT;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ldsK = smem;
+  char* ldsV = smem + KIMG;          // (the same layout; its row fragments only)
+  char* ldsQ = ldsV + KIMG;          // slot i: Q at 2 i QIMG, dO at (2 i + 1) QIMG
+  char* ldsS = ldsQ + 4 * QIMG;      // dS^T images, 2 x SIMG
+  float* ldsL = reinterpret_cast<float*>(ldsS + 2 * SIMG);  // lse - log2(448)
+  float* ldsD = ldsL + LMAX;                                 // delta * sds / 448
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, h = blockIdx.y;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  const uint8_t* qb = reinterpret_cast<const uint8_t*>(a.q) + b * a.q_sb + h * a.q_sh;
+  const uint8_t* kb = reinterpret_cast<const uint8_t*>(a.k) + b * a.k_sb + h * a.k_sh;
+  const uint8_t* vb = reinterpret_cast<const uint8_t*>(a.v) + b * a.v_sb + h * a.v_sh;
+  const uint8_t* db = reinterpret_cast<const uint8_t*>(a.dout) + b * a.do_sb + h * a.do_sh;
+  const bf16_t* ob = a.o + b * a.o_sb + h * a.o_sh;
+  const float sq = a.sq8[0], sk = a.sk8[0], sv = a.sv8[0], sdo = a.sdo8[0], sds = a.sds8[0];
+  const float c8 = scl * LOG2E / (sq * sk);     // log2-domain logit per raw S product
+  const float k1 = sds / 448.f;                 // e5m2 dS = P448 (dP - delta) * k1
+  const float cdp = k1 / (sdo * sv);            // raw dP product -> dP * k1
+  const int nq = (a.Lq + QT - 1) / QT;
+
+  // ---- prologue: K image, Q / dO tile 0, lse / delta of every query, V fragments
+#pragma unroll
+  for (int i = 0; i < 2 * KIMG / 16 / NT; ++i) {  // K, then V
+    const int id = tid + i * NT, r = (id >> 2) & (LMAX - 1), p = id & 3;
+    const bool isv = id >= KIMG / 16;
+    const uint8_t* src = (isv ? vb + (long long)min(r, a.Lk - 1) * a.v_sl
+                              : kb + (long long)min(r, a.Lk - 1) * a.k_sl) + 16 * p;
+    uint4 v = *reinterpret_cast<const uint4*>(src);
+    if (r >= a.Lk) v = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>((isv ? ldsV : ldsK) + r * 64 + 16 * (p ^ ((r >> 2) & 3))) = v;
+  }
+  // Q / dO tile t, piece tid (< 256): tensor tid >> 7, row (tid >> 2) & 31, 16-byte piece tid & 3
+  const int pr = (tid >> 2) & 31, pp = tid & 3;
+  const bool pdo = (tid >> 7) & 1;
+  // (the load's zero-select is applied at the LDS write, so that the
+  // prefetch of the next tile is not waited for where it is issued)
+  auto tile_load = [&](int t) {
+    const int q = min(t * QT + pr, a.Lq - 1);
+    const uint8_t* src = (pdo ? db + (long long)q * a.do_sl : qb + (long long)q * a.q_sl) + 16 * pp;
+    return *reinterpret_cast<const uint4*>(src);
+  };
+  auto tile_put = [&](int t, uint4 v) {
+    if (t * QT + pr >= a.Lq) v = make_uint4(0u, 0u, 0u, 0u);
+    char* dst = ldsQ + (2 * (t & 1) + (pdo ? 1 : 0)) * QIMG;
+    *reinterpret_cast<uint4*>(dst + pr * 64 + 16 * (pp ^ (((pr >> 2) ^ (pr >> 4)) & 3))) = v;
+  };
+  if (tid < 256) tile_put(0, tile_load(0));
+  for (int q = tid; q < LMAX; q += NT) {
+    float l = INFINITY, d = 0.f;
+    if (q < a.Lq) {
+      l = a.lse[((long long)b * a.H + h) * a.Lq + q] - LOG2_448;
+      const uint8_t* dr = db + (long long)q * a.do_sl;
+      const bf16_t* orow = ob + (long long)q * a.o_sl;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {  // 8 elements per chunk
+        const uint2 d8 = *reinterpret_cast<const uint2*>(dr + 8 * c);
+        const short8_t o8 = *reinterpret_cast<const short8_t*>(orow + 8 * c);
+        const auto x0 = __builtin_amdgcn_cvt_pk_f32_bf8(d8.x, false);
+        const auto x1 = __builtin_amdgcn_cvt_pk_f32_bf8(d8.x, true);
+        const auto x2 = __builtin_amdgcn_cvt_pk_f32_bf8(d8.y, false);
+        const auto x3 = __builtin_amdgcn_cvt_pk_f32_bf8(d8.y, true);
+        const float dv8[8] = {x0[0], x0[1], x1[0], x1[1], x2[0], x2[1], x3[0], x3[1]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += dv8[e] * bf2f((bf16_t)o8[e]);
+      }
+      d *= k1 / sdo;
+    }
+    ldsL[q] = l;
+    ldsD[q] = d;
+  }
+  __syncthreads();
+
+  f32x4 dk[U][4], dv[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dk[u][i] = dv[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float amx = 0.f;  // max |dS| * sds
+  // dQ: 8 output blocks of 16 queries x 16 head dims per step, blocks w + NW i;
+  // the column sums of the bf16-rounded dQ (bias gradient) over every step
+  const float gq = a.scale / (sds * sk), s8 = a.sg8 ? a.sg8[0] : 0.f;
+  float csq[4] = {0.f, 0.f, 0.f, 0.f}, amq = 0.f;
+  const long long dq_base = b * a.dq_sb + h * a.dq_sh;
+  auto dq_step = [&](int t) {
+    const int q0 = t * QT;
+    const char* sS = ldsS + (t & 1) * SIMG;
+    const int nkc = min(causal ? t + 1 : LMAX / 32, (klim + 31) / 32);
+#pragma unroll
+    for (int i = 0; i < 8 / NW; ++i) {
+      const int blk = w + NW * i, qbk = blk >> 2, dt = blk & 3;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = 8 * g + (cl >> 1);
+      // batches of 4 key chunks, the next batch's reads in flight behind the
+      // current batch's MFMAs (chunks past nkc: clamped address, zero operand)
+#define TDG_F8_RD(KT, ST, KC0)                                                     \
+  _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                  \
+    const int kc = min((KC0) + c, nkc - 1);                                        \
+    KT[c] = lds_tr8(ldsK + f8k_off(32 * kc + row, 2 * dt + (cl & 1)));             \
+    ST[c] = lds_tr8(sS + f8s_off(32 * kc + row, 2 * qbk + (cl & 1)));              \
+  }
+#define TDG_F8_MM(KT, ST, KC0)                                                     \
+  _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                  \
+    tie(KT[c]);                                                                    \
+    tie(ST[c]);                                                                    \
+    const long z = 0;                                                              \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(KT[c], (KC0) + c < nkc ? ST[c] : z, acc, 0, 0, 0); \
+  }
+      long ka[4], sa[4], kb2[4], sb[4];
+      TDG_F8_RD(ka, sa, 0)
+      for (int kc0 = 0; kc0 < nkc; kc0 += 8) {
+        const bool hb = kc0 + 4 < nkc;
+        if (hb) {
+          TDG_F8_RD(kb2, sb, kc0 + 4)
+          lgkm_wait<8>();
+        } else {
+          lgkm_wait<0>();
+        }
+        TDG_F8_MM(ka, sa, kc0)
+        if (hb) {
+          if (kc0 + 8 < nkc) {
+            TDG_F8_RD(ka, sa, kc0 + 8)
+            lgkm_wait<8>();
+          } else {
+            lgkm_wait<0>();
+          }
+          TDG_F8_MM(kb2, sb, kc0 + 4)
+        }
+      }
+#undef TDG_F8_RD
+#undef TDG_F8_MM
+      const int q = q0 + 16 * qbk + cl;
+      const bool ok = q < a.Lq;
+      // (uniform base + 32-bit lane offset: a 64-bit per-lane address kept
+      // across the loop was spilled)
+      const long long off = dq_base + (q * (int)a.dq_sl + 16 * dt + 4 * g);
+      float v[4];
+      bf16_t e[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        e[r] = f2bf(acc[r] * gq);
+        v[r] = ok ? bf2f(e[r]) : 0.f;
+        csq[r] += v[r];
+        amq = fmaxf(amq, fabsf(v[r]));
+      }
+      if (ok && a.dq)
+        *reinterpret_cast<uint2*>(a.dq + off) = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16),
+                                                           (uint32_t)e[2] | ((uint32_t)e[3] << 16));
+      if (ok && a.dq8) {
+        int w8 = pack2_e5m2c<false>(v[0] * s8, v[1] * s8, 0);
+        w8 = pack2_e5m2c<true>(v[2] * s8, v[3] * s8, w8);
+        *reinterpret_cast<int*>(a.dq8 + off) = w8;
+      }
+    }
+  };
+
+  // Q / dO tile t by LDS-DMA (waves 0-3, one 1 KiB piece each: wave wq
+  // fills tensor wq >> 1, rows 16 (wq & 1) .. +15, lane l the 16-byte
+  // position l & 3 of row l >> 2 -- the source piece is swizzled instead of
+  // the destination). Rows past Lq repeat row Lq - 1 (finite; their P and dS
+  // are masked to 0). No destination registers: nothing for a later register
+  // reuse to wait on.
+  auto tile_dma = [&](int t) {
+    if (w < 4) {
+      const int r = 16 * (w & 1) + (lane >> 2);
+      const int q = min(t * QT + r, a.Lq - 1);
+      const int pc = (lane & 3) ^ (((r >> 2) ^ (r >> 4)) & 3);
+      const uint8_t* src = ((w >> 1) ? db + (long long)q * a.do_sl : qb + (long long)q * a.q_sl) + 16 * pc;
+      char* dst = ldsQ + (2 * (t & 1) + (w >> 1)) * QIMG + 16 * (w & 1) * 64;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst,
+                                       16, 0, 0);
+    }
+  };
+  for (int it = 0; it < nq; ++it) {
+    if (it > 0) {
+      wait_vmcnt<0>();  // this tile's DMA (issued a whole step ago)
+      lds_barrier();
+    }
+    const int q0 = it * QT;
+    const char* sQ = ldsQ + 2 * (it & 1) * QIMG;
+    const char* sO = sQ + QIMG;
+    char* sS = ldsS + (it & 1) * SIMG;
+    // dQ of the previous tile first, then the next tile's DMA: a register
+    // reload inside dq_step waits for every VMEM operation in flight
+    if (it > 0) dq_step(it - 1);
+    if (it + 1 < nq) tile_dma(it + 1);
+    long qf[2][2], of[2][2], qT[4], oT[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 8 * (cl >> 2) + 4 * j + (cl & 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qf[j][ks] = *reinterpret_cast<const long*>(sQ + f8q_off(row, 4 * ks + g));
+        of[j][ks] = *reinterpret_cast<const long*>(sO + f8q_off(row, 4 * ks + g));
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int row = 8 * g + (cl >> 1);
+      qT[dt] = lds_tr8(sQ + f8q_off(row, 2 * dt + (cl & 1)));
+      oT[dt] = lds_tr8(sO + f8q_off(row, 2 * dt + (cl & 1)));
+    }
+    // (lse / delta of the lane's queries are re-read per subtile: held across
+    // the subtile loop they pushed the kernel into spilling, and a spill's
+    // reload waits for the tile prefetch in flight)
+    const float* lq = ldsL + q0 + 8 * g;
+    const float* dq4 = ldsD + q0 + 8 * g;
+    lgkm_wait<0>();
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      tie(qT[dt]);
+      tie(oT[dt]);
+    }
+    // subtile u: S^T / dP^T, P and dS (e4m3 / e5m2 packed as they stand), the
+    // dV^T / dK^T updates and dS^T into the image. (A branch-free copy of this
+    // body for the all-active, unmasked case made the compiler spill 262
+    // registers: one uniform branch per subtile instead.)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int s16 = 16 * (w + NW * u);  // the subtile's first key (wave-uniform)
+        const bool act = s16 < klim && (!causal || s16 <= q0 + QT - 1);
+        long pS = 0;
+        if (act) {
+          // the subtile's K / V row fragments (key on the lane), from the images
+          long kf[2], vf[2];
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            kf[ks] = *reinterpret_cast<const long*>(ldsK + f8k_off(s16 + cl, 4 * ks + g));
+            vf[ks] = *reinterpret_cast<const long*>(ldsV + f8k_off(s16 + cl, 4 * ks + g));
+          }
+          f32x4 s[2], dp[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][0], kf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][1], kf[1], s[j], 0, 0, 0);
+            dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][0], vf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][1], vf[1], dp[j], 0, 0, 0);
+          }
+          const bool full = s16 + 15 < klim && q0 + QT <= a.Lq && (!causal || s16 + 15 <= q0);
+          f32x4 L4[2], D4[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            L4[j] = *reinterpret_cast<const f32x4*>(lq + 4 * j);
+            D4[j] = *reinterpret_cast<const f32x4*>(dq4 + 4 * j);
+          }
+          float x[2][4];
+          if (full) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[j][r] = fmaf(s[j][r], c8, -L4[j][r]);
+          } else {
+            const int key = s16 + cl;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int q = q0 + 8 * g + 4 * j + r;
+                const bool ok = (key < klim) & (q < a.Lq) & (!causal | (key <= q));  // (no short circuit)
+                const float xv = fmaf(s[j][r], c8, -L4[j][r]);
+                x[j][r] = ok ? xv : -INFINITY;
+              }
+          }
+          int pw[2], sw[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float p[4], ds[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p[r] = fminf(fast_exp2(x[j][r]), 448.f);
+              ds[r] = p[r] * fmaf(dp[j][r], cdp, -D4[j][r]);
+              amx = fmaxf(amx, fabsf(ds[r]));
+              ds[r] = __builtin_amdgcn_fmed3f(ds[r], -E5M2_MAX_F, E5M2_MAX_F);
+            }
+            const int pv = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], 0, false);
+            pw[j] = __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], pv, true);
+            const int sv2 = __builtin_amdgcn_cvt_pk_bf8_f32(ds[0], ds[1], 0, false);
+            sw[j] = __builtin_amdgcn_cvt_pk_bf8_f32(ds[2], ds[3], sv2, true);
+          }
+          const long pP = (long)(uint32_t)pw[0] | ((long)pw[1] << 32);
+          pS = (long)(uint32_t)sw[0] | ((long)sw[1] << 32);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            dv[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(oT[dt], pP, dv[u][dt], 0, 0, 0);
+            dk[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(qT[dt], pS, dk[u][dt], 0, 0, 0);
+          }
+        }
+        *reinterpret_cast<long*>(sS + f8s_off(s16 + cl, g)) = pS;
+      }
+  }
+  wait_vmcnt<0>();
+  lds_barrier();
+  dq_step(nq - 1);
+
+  // ---- epilogue: dK / dV (key rows on lanes) bf16 and / or e5m2, amax and
+  // the bias-gradient column sums (dQ's, dK's, dV's) of this (b, h)
+  const float gk = a.scale / (sds * sq), gv = 1.f / (448.f * sdo);
+  float csk[4][4], csv[4][4], amk = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csk[dt][r] = csv[dt][r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int key = 16 * (w + NW * u) + cl;
+    const bool ok = key < a.Lk;
+    const long long offk = b * a.dk_sb + (long long)key * a.dk_sl + h * a.dk_sh;
+    const long long offv = b * a.dv_sb + (long long)key * a.dv_sl + h * a.dv_sh;
+    uint32_t klo[4], khi[4], vlo[4], vhi[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      pack_acc(dk[u][dt], gk, klo[dt], khi[dt]);
+      pack_acc(dv[u][dt], gv, vlo[dt], vhi[dt]);
+    }
+    if (a.dk) store_row16<4>(a.dk + offk, klo, khi, g, ok);
+    if (a.dv) store_row16<4>(a.dv + offv, vlo, vhi, g, ok);
+    if (a.dk8) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float k4[4] = {__uint_as_float(klo[dt] << 16), __uint_as_float(klo[dt] & 0xffff0000u),
+                             __uint_as_float(khi[dt] << 16), __uint_as_float(khi[dt] & 0xffff0000u)};
+        const float v4[4] = {__uint_as_float(vlo[dt] << 16), __uint_as_float(vlo[dt] & 0xffff0000u),
+                             __uint_as_float(vhi[dt] << 16), __uint_as_float(vhi[dt] & 0xffff0000u)};
+        int wk = pack2_e5m2c<false>(k4[0] * s8, k4[1] * s8, 0);
+        wk = pack2_e5m2c<true>(k4[2] * s8, k4[3] * s8, wk);
+        int wv = pack2_e5m2c<false>(v4[0] * s8, v4[1] * s8, 0);
+        wv = pack2_e5m2c<true>(v4[2] * s8, v4[3] * s8, wv);
+        if (ok) {
+          *reinterpret_cast<int*>(a.dk8 + offk + 16 * dt + 4 * g) = wk;
+          *reinterpret_cast<int*>(a.dv8 + offv + 16 * dt + 4 * g) = wv;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          csk[dt][r] += ok ? k4[r] : 0.f;
+          csv[dt][r] += ok ? v4[r] : 0.f;
+          amk = fmaxf(amk, ok ? fmaxf(fabsf(k4[r]), fabsf(v4[r])) : 0.f);
+        }
+      }
+    }
+  }
+  // amax: dS (its own slot), the gradients (the projection's e5m2 slot)
+  amx = wave_max(amx);
+  if (lane == 0 && a.amaxds8) atomic_amax(amax_word(a.amaxds8, b * 7 + h * 13 + w), amx / sds);
+  const float amg = wave_max(fmaxf(amq, amk));
+  if (lane == 0 && a.amaxg8 && (a.dq8 || a.dk8)) atomic_amax(amax_word(a.amaxg8, b * 5 + h * 11 + w), amg);
+  if (!a.cs_part) return;
+  // column sums: over the wave's 16 rows per lane group (shuffles), then the
+  // waves through LDS (the Q / dO ring is free: every read of it is behind the
+  // last barrier)
+  float* red = reinterpret_cast<float*>(ldsQ);  // [3][NW][64]
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int sh = 1; sh < 16; sh <<= 1) csq[r] += __shfl_xor(csq[r], sh, 64);
+  if (a.dk8) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int sh = 1; sh < 16; sh <<= 1) {
+          csk[dt][r] += __shfl_xor(csk[dt][r], sh, 64);
+          csv[dt][r] += __shfl_xor(csv[dt][r], sh, 64);
+        }
+  }
+  if (cl == 0) {
+    const int dtq = w & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * dt + 4 * g + r;
+        red[w * 64 + col] = dt == dtq ? csq[r] : 0.f;
+        red[(NW + w) * 64 + col] = csk[dt][r];
+        red[(2 * NW + w) * 64 + col] = csv[dt][r];
+      }
+  }
+  __syncthreads();
+  float* prow = a.cs_part + ((long long)b * a.cs_np) * a.cs_ld + h * 64;
+  if (tid < 64 * (a.dk8 ? 3 : 1)) {
+    const int m = tid >> 6, col = tid & 63;
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) sum += red[(m * NW + i) * 64 + col];
+    prow[(m == 0 ? a.cs_q : m == 1 ? a.cs_k : a.cs_v) + col] = sum;
+  }
+}
+
 // ============================================================================ probabilities (inference maps)
 // One wave per (b, h, q) row: emits the full softmax row [Lk] in f32, the
 // attention_weights the reference returns (transformer_model.py:104-109,
@@ -2021,6 +2453,26 @@ extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, hipStream_t st) {
   hipLaunchKernelGGL(attn_fwd_fp8_kernel<NS>, dim3(cdiv(a->Lq, 128), a->H, a->B), dim3(512),
                      NS * 2 * 64 * 64, st, *a);
   return 0;
+}
+namespace {
+template <int NW>
+int bwd_f8_nw(const AttnArgs& a, hipStream_t st) {
+  constexpr int lds = 2 * 512 * 64 + 4 * 32 * 64 + 2 * 512 * 32 + 2 * 512 * 4;  // 108 KiB
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_bwd_f8_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_bwd_f8_kernel<NW>, dim3(1, a.H, a.B), dim3(NW * 64), lds, st, a);
+  return 0;
+}
+}  // namespace
+// hd 64, Lq, Lk <= 512: one 8-wave workgroup per (batch, head) (4 waves of
+// 8 subtiles each -- one wave per SIMD -- spilled 155 registers at -O3)
+extern "C" int tdg_attn_bwd_f8(const AttnArgs* a, int hd, hipStream_t st) {
+  if (hd != 64 || a->Lq < 1 || a->Lk < 1 || a->Lq > 512 || a->Lk > 512) return -1;
+  return bwd_f8_nw<8>(*a, st);
 }
 extern "C" int tdg_attn_probs(const AttnArgs* a, int hd, float* probs, hipStream_t st) {
   TDG_HD_CASES(probs_hd, *a, probs, st)

@@ -439,6 +439,22 @@ def _fp8_dgrad_into(g8, g_slot: int, w: Param, out: torch.Tensor, rt: RunCtx, be
                        w_plain=fp8.DGRAD_PLAIN_W)
 
 
+def _fp8_dgrad8(g8, g_slot: int, w: Param, out_slot: int, rt: RunCtx) -> torch.Tensor:
+    """e5m2 copy only (no bf16 output) of dequant(g8 (e5m2) @ w) in the
+    gradient slot out_slot (amax recorded): the fp8 attention backward's dO."""
+    st = rt.fp8
+    wt8, swt = st.weights.get(w, transposed=not fp8.DGRAD_PLAIN_W)
+    return fp8.gemm_bf8_dgrad(g8, st.gmeta, g_slot, wt8, st.meta, swt, None, out8_slot=out_slot,
+                              w_plain=fp8.DGRAD_PLAIN_W)
+
+
+def _attn_f8_bwd(ctx, Lq: int, Lk: int, hd: int) -> bool:
+    """Does this attention block's fp8 backward run on the fp8 kernel
+    (its forward ran e4m3 and the shape is covered)?"""
+    return (fp8.ATTN_BWD_F8 and getattr(ctx, "q8", None) is not None
+            and K.attn_bwd_f8_ok(Lq, Lk, hd))
+
+
 # =============================================================================== LN helpers
 def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int, rt: RunCtx):
     """GPU block tail y = LN(x + dropout(a2 @ w^T + b)) -> (y, saved): the
@@ -632,9 +648,11 @@ class SelfAttnBlockFn(torch.autograd.Function):
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd)
             o8e = None
+            ctx.q8 = None
             if qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
                 q85 = qkv8.view(B, L, 3, heads, hd)
                 s8 = rt.fp8.meta.s(r[2])
+                ctx.q8 = (qkv8, r[2])  # (the fp8 attention backward's operands)
                 # (lean: the epilogue also emits the e4m3 O of the output projection)
                 o8e = rt.fp8.o8_for(wo, (B, L, heads, hd), x.device) if lean else None
                 o, aux = K.attn_fwd_fp8(q85[:, :, 0], q85[:, :, 1], q85[:, :, 2], s8, s8, s8, kv_len,
@@ -716,12 +734,32 @@ class SelfAttnBlockFn(torch.autograd.Function):
         os_, go = st.attn_out[id(wo)]
         dh, ds8 = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, ds8_slot=go)
         ds8 = ds8.view(M, d)
+        gq = st.proj_bwd[id(wqkv)]
+        if _attn_f8_bwd(ctx, L, L, hd):
+            # fp8 attention backward: e5m2 dO straight from the output
+            # projection's dgrad, e4m3 Q/K/V of the forward -> e5m2 dQ|dK|dV
+            gdo, gds = st.attn_bwd8[id(wo)]
+            do8 = _fp8_dgrad8(ds8, go, wo, gdo, rt)
+            qkv8, qs = ctx.q8
+            q85 = qkv8.view(B, L, 3, heads, hd)
+            s8 = st.meta.s(qs)
+            dqkv8 = torch.empty(M, 3 * d, dtype=st.gmeta.dtype, device=dy.device)
+            g85 = dqkv8.view(B, L, 3, heads, hd)
+            part = K.workspace(f"f8cs_qkv{site}", B * 3 * d, dy.device)
+            nparts = K.attn_bwd_f8(q85[:, :, 0], q85[:, :, 1], q85[:, :, 2], s8, s8, s8, o,
+                                   do8.view(B, L, heads, hd), st.gmeta.s(gdo), aux, kv_len, scale,
+                                   causal, st.gmeta.s(gds), st.gmeta.a(gds), dq8=g85[:, :, 0],
+                                   dk8=g85[:, :, 1], dv8=g85[:, :, 2], sg8=st.gmeta.s(gq),
+                                   amaxg8=st.gmeta.a(gq), cs_part=part, cs_ld=3 * d, cs_q=0,
+                                   cs_k=d, cs_v=2 * d)
+            _fold_bias_later(rt, part[: nparts * 3 * d], nparts, 3 * d, bqkv)
+            return SelfAttnBlockFn._finish_fp8(ctx, rt, st, dh, ds8, go, dqkv8, gq, x8, xs, o8, os_,
+                                               M, d, B, L, bt)
         do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
         _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
         q5 = qkv.view(B, L, 3, heads, hd)
         dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
         g5 = dqkv.view(B, L, 3, heads, hd)
-        gq = st.proj_bwd[id(wqkv)]
         if fp8.ATTN_BWD_G8 and K.attn_bwd_g8_ok(L, L, hd):
             # the attention backward emits e5m2 dQ|dK|dV, their amax and the
             # bias-gradient partials itself (no bf16 dQ|dK|dV pass)
@@ -737,6 +775,14 @@ class SelfAttnBlockFn(torch.autograd.Function):
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
             dqkv8 = _fp8_grad_bias(dqkv, gq, bqkv, rt, f"qkv{site}")
+        return SelfAttnBlockFn._finish_fp8(ctx, rt, st, dh, ds8, go, dqkv8, gq, x8, xs, o8, os_, M,
+                                           d, B, L, bt)
+
+    @staticmethod
+    def _finish_fp8(ctx, rt, st, dh, ds8, go, dqkv8, gq, x8, xs, o8, os_, M, d, B, L, bt):
+        """input-projection dgrad into the residual gradient, both weight
+        gradients in fp8"""
+        wqkv, bqkv, wo = ctx.p[0], ctx.p[1], ctx.p[2]
         _fp8_dgrad_into(dqkv8, gq, wqkv, dh.view(M, d), rt, 1.0)
         q = rt.wgrad
         q.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
@@ -847,6 +893,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
             if q is None:
                 q = K.linear_fwd(x2, wq.compute, bq.master)
+            ctx.q8 = None
             if q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
                 kv8, kvs = rt.fp8.kv8
                 if kv8.shape != kv_all.shape:
@@ -854,6 +901,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
                                        f"{tuple(kv_all.shape)}")
                 kv85 = kv8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
                 skv = rt.fp8.meta.s(kvs)
+                ctx.q8 = (q8, r[2], kv85, kvs)  # (the fp8 attention backward's operands)
                 o8e = rt.fp8.o8_for(wo, (B, T, heads, hd), x.device) if lean else None
                 o, aux = K.attn_fwd_fp8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],
                                         rt.fp8.meta.s(r[2]), skv, skv, kv_len, scale, False,
@@ -903,10 +951,31 @@ class CrossAttnBlockFn(torch.autograd.Function):
             os_, go = st.attn_out[id(wo)]
             dh, ds8 = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, ds8_slot=go)
             ds8 = ds8.view(M, d)
+            gq = st.proj_bwd[id(wq)]
+            if _attn_f8_bwd(ctx, T, S, hd):
+                # fp8 attention backward: e5m2 dQ (+ amax, bias sums), bf16
+                # dK / dV into the batched cross K|V gradient
+                gdo, gds = st.attn_bwd8[id(wo)]
+                do8 = _fp8_dgrad8(ds8, go, wo, gdo, rt)
+                q8, qs, kv85, kvs = ctx.q8
+                skv = st.meta.s(kvs)
+                dq8 = torch.empty(M, d, dtype=st.gmeta.dtype, device=dy.device)
+                part = K.workspace(f"f8cs_q{site}", B * d, dy.device)
+                nparts = K.attn_bwd_f8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],
+                                       st.meta.s(qs), skv, skv, o, do8.view(B, T, heads, hd),
+                                       st.gmeta.s(gdo), aux, kv_len, scale, False, st.gmeta.s(gds),
+                                       st.gmeta.a(gds), dk=g5[:, :, 0], dv=g5[:, :, 1],
+                                       dq8=dq8.view(B, T, heads, hd), sg8=st.gmeta.s(gq),
+                                       amaxg8=st.gmeta.a(gq), cs_part=part, cs_ld=d, cs_q=0)
+                _fold_bias_later(rt, part[: nparts * d], nparts, d, bq)
+                _fp8_dgrad_into(dq8, gq, wq, dh.view(M, d), rt, 1.0)
+                rt.wgrad.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
+                rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)
+                dkv_ret = dkv_all if layer == 0 else None
+                return (dh.view(B, T, d), dkv_ret) + (None,) * 12
             do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
             _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
             dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
-            gq = st.proj_bwd[id(wq)]
             if fp8.ATTN_BWD_G8 and K.attn_bwd_g8_ok(T, S, hd):
                 # e5m2 dQ (+ amax, bias partials) from the attention backward;
                 # dK / dV stay bf16 (summed over the layers into the batched

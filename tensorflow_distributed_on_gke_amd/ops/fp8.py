@@ -14,13 +14,15 @@ kernel itself (adam_chunk_kernel) with the scale the next forward uses.
 What runs in which format is `precision_map()` (bench.py prints it in its
 record for `--dtype fp8`): every projection GEMM of the encoder / decoder
 layers -- forward, dgrad and weight gradient -- and the attention forward
-are fp8; the attention backward, the vocabulary projection, LayerNorm,
-embeddings, cross-entropy and the fp32 Adam are not. Measured (docs/PERF.md):
-Transformer-big seq 512 fp8 11.78 vs 13.59 ms/step bf16 on one box (round 4).
+and backward (sequences of 129-512) are fp8; the vocabulary projection,
+LayerNorm, embeddings, cross-entropy and the fp32 Adam are not. Measured
+(docs/PERF.md): Transformer-big seq 512 fp8 11.78 vs 13.59 ms/step bf16 on
+one box (round 4, before the fp8 attention backward).
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -64,7 +66,7 @@ def precision_map() -> Dict[str, str]:
         "attention_input_projections_forward": "e4m3 x e4m3 (self Q|K|V, cross Q, batched cross K|V)",
         "attention_output_projection_forward": "e4m3 x e4m3" if ATTN_PROJ_FP8 else "bf16",
         "attention_forward": "e4m3 Q/K/V and P, fp32 softmax (hd 64, seq > 128; else bf16)",
-        "attention_backward": ATTN_BWD_PRECISION,
+        "attention_backward": _attn_bwd_precision(),
         "ffn_dgrads": "e5m2 x e4m3 (ReLU-backward epilogue)",
         "attention_projection_dgrads": proj_bwd,
         "ffn_weight_gradients": "e5m2 x e4m3" if WGRAD_FP8 else "bf16",
@@ -77,9 +79,23 @@ def precision_map() -> Dict[str, str]:
     }
 
 
-# the attention backward's format (precision_map): its MFMAs read the
-# dequantised e4m3 Q/K/V of the forward and bf16 dO
-ATTN_BWD_PRECISION = "bf16 MFMA on the dequantised e4m3 Q/K/V, bf16 dO (e5m2 dQ|dK|dV out)"
+# fp8 attention backward (attention.hip attn_bwd_f8_kernel, sequences of
+# 129-512 at hd 64): the forward's e4m3 Q/K/V and e4m3 P, e5m2 dO and dS on
+# the fp8 MFMAs, every key of a (batch, head) in one workgroup (P and dS once)
+ATTN_BWD_F8 = os.environ.get("TDG_ATTN_BWD_F8", "1") != "0"
+_ATTN_BWD_F8_STR = ("e4m3 Q/K/V/P x e5m2 dO/dS on fp8 MFMA (v_mfma_f32_16x16x32 fp8/bf8), f32 "
+                    "softmax from the forward LSE (seq 129-512); e5m2 dQ|dK|dV out (cross-attention "
+                    "dK/dV bf16 into the batched K|V gradient)")
+_ATTN_BWD_BF16_STR = "bf16 MFMA on the dequantised e4m3 Q/K/V, bf16 dO (e5m2 dQ|dK|dV out)"
+
+
+def _attn_bwd_precision() -> str:
+    return _ATTN_BWD_F8_STR if ATTN_BWD_F8 else _ATTN_BWD_BF16_STR
+
+
+# the attention backward's format as configured at import (precision_map
+# reads the flag when called)
+ATTN_BWD_PRECISION = _attn_bwd_precision()
 
 
 def precision_string() -> str:
@@ -483,6 +499,7 @@ class Fp8State:
         # (DGRAD_PLAIN_W: the forward's copies, read N-contiguous) and the
         # forward's e4m3 input
         self.attn_out: Dict[int, Tuple[int, int]] = {}
+        self.attn_bwd8: Dict[int, Tuple[int, int]] = {}
         self.proj_bwd: Dict[int, int] = {}
         if backward and ATTN_PROJ_FP8:
             outs = [l.o.w for l in enc] + [w for l in dec for w in (l.o1.w, l.o2.w)]
@@ -491,6 +508,8 @@ class Fp8State:
                 if not DGRAD_PLAIN_W:
                     self.weights.add(w, transposed=True)
                 self.attn_out[id(w)] = (self.meta.slot("o:" + w.name), self.gmeta.slot("go:" + w.name))
+                # fp8 attention backward of this block: e5m2 dO and dS slots
+                self.attn_bwd8[id(w)] = (self.gmeta.slot("gdo:" + w.name), self.gmeta.slot("gds:" + w.name))
             ins = [l.qkv.w for l in enc] + [w for l in dec for w in (l.qkv1.w, l.q2.w)] + [model.cross_kv.w]
             for w in ins:
                 if not DGRAD_PLAIN_W:
