@@ -208,6 +208,13 @@ __device__ __forceinline__ long lds_read_b64_at(uint32_t a) {
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
   return r;
 }
+// 8-byte LDS store at a compile-time offset, untracked like the reads above
+// (a later lgkmcnt wait -- e.g. lds_barrier -- covers it)
+template <int OFF>
+__device__ __forceinline__ void lds_write_b64_at(uint32_t a, long v) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS offset field");
+  asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
+}
 template <int OFF>
 __device__ __forceinline__ long lds_read_tr8_at(uint32_t a) {
   static_assert(OFF >= 0 && OFF < 65536, "DS offset field");

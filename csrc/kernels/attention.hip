@@ -1877,7 +1877,6 @@ __device__ __forceinline__ int f8q_off(int r, int c) {
   return r * 64 + 8 * (c ^ (2 * (((r >> 2) ^ (r >> 4)) & 3)));
 }
 __device__ __forceinline__ int f8s_off(int r, int c) { return r * 32 + 8 * (c ^ (2 * ((r >> 3) & 1))); }
-__device__ __forceinline__ long lds_tr8(const char* p) { return lds_read_tr8_async(p); }
 
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
@@ -1967,58 +1966,67 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) dk[u][i] = dv[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float amx = 0.f;  // max |dS| * sds
+  // LDS addresses: every image row base below is a multiple of 16 (32 for the
+  // dS image), so each swizzle term is the lane's own and a fragment address
+  // is a per-lane offset plus a wave-uniform base plus a compile-time
+  // immediate (no address arithmetic per read; all reads are the untracked
+  // asm forms, waited for by count -- the compiler had merged tracked K / V
+  // and Q / dO reads into ds_read2st64, whose 32-bank rule made them conflict)
+  const uint32_t lK = (uint32_t)(uintptr_t)ldsK, lQ = (uint32_t)(uintptr_t)ldsQ;
+  const uint32_t lS = (uint32_t)(uintptr_t)ldsS, lL = (uint32_t)(uintptr_t)ldsL;
+  // K / V row fragments of subtile u: lK + 1024 w + kvo[ks] + 8192 u (+ KIMG for V)
+  const uint32_t kvb0 = lK + 1024 * w + cl * 64 + 8 * ((0 + g) ^ (2 * ((cl >> 2) & 3)));
+  const uint32_t kvb1 = lK + 1024 * w + cl * 64 + 8 * ((4 + g) ^ (2 * ((cl >> 2) & 3)));
+  // Q / dO row fragments (row 8 (cl >> 2) + 4 j + (cl & 3)) and transposed ones
+  uint32_t qo[2][2], to[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qo[j][ks] = f8q_off(8 * (cl >> 2) + 4 * j + (cl & 3), 4 * ks + g);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) to[dt] = f8q_off(8 * g + (cl >> 1), 2 * dt + (cl & 1));
+  // dS^T image row of subtile u: lS + 512 w + so + 4096 u (+ SIMG for odd steps)
+  const uint32_t sob = lS + 512 * w + f8s_off(cl, g);
+  // lse / delta of the lane's queries q0 + 8 g .. +7
+  const uint32_t lgb = lL + 32 * g;
+
   // dQ: 8 output blocks of 16 queries x 16 head dims per step, blocks w + NW i;
   // the column sums of the bf16-rounded dQ (bias gradient) over every step
   const float gq = a.scale / (sds * sk), s8 = a.sg8 ? a.sg8[0] : 0.f;
   float csq[4] = {0.f, 0.f, 0.f, 0.f}, amq = 0.f;
   const long long dq_base = b * a.dq_sb + h * a.dq_sh;
+  const int drow = 8 * g + (cl >> 1);
   auto dq_step = [&](int t) {
     const int q0 = t * QT;
-    const char* sS = ldsS + (t & 1) * SIMG;
     const int nkc = min(causal ? t + 1 : LMAX / 32, (klim + 31) / 32);
 #pragma unroll
     for (int i = 0; i < 8 / NW; ++i) {
       const int blk = w + NW * i, qbk = blk >> 2, dt = blk & 3;
+      // chunk kc: K^T at lK + dko + 2048 kc, dS at the step's image + dso + 1024 kc
+      uint32_t ka = lK + f8k_off(drow, 2 * dt + (cl & 1));
+      uint32_t sa = lS + (t & 1) * SIMG + f8s_off(drow, 2 * qbk + (cl & 1));
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int row = 8 * g + (cl >> 1);
-      // batches of 4 key chunks, the next batch's reads in flight behind the
-      // current batch's MFMAs (chunks past nkc: clamped address, zero operand)
-#define TDG_F8_RD(KT, ST, KC0)                                                     \
-  _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                  \
-    const int kc = min((KC0) + c, nkc - 1);                                        \
-    KT[c] = lds_tr8(ldsK + f8k_off(32 * kc + row, 2 * dt + (cl & 1)));             \
-    ST[c] = lds_tr8(sS + f8s_off(32 * kc + row, 2 * qbk + (cl & 1)));              \
-  }
-#define TDG_F8_MM(KT, ST, KC0)                                                     \
-  _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                  \
-    tie(KT[c]);                                                                    \
-    tie(ST[c]);                                                                    \
-    const long z = 0;                                                              \
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(KT[c], (KC0) + c < nkc ? ST[c] : z, acc, 0, 0, 0); \
-  }
-      long ka[4], sa[4], kb2[4], sb[4];
-      TDG_F8_RD(ka, sa, 0)
-      for (int kc0 = 0; kc0 < nkc; kc0 += 8) {
-        const bool hb = kc0 + 4 < nkc;
-        if (hb) {
-          TDG_F8_RD(kb2, sb, kc0 + 4)
-          lgkm_wait<8>();
-        } else {
-          lgkm_wait<0>();
+      // batches of 4 chunks; a partial last batch reads clamped chunks and
+      // zeroes their dS operand
+      for (int kc0 = 0; kc0 < nkc; kc0 += 4) {
+        long kt[4], st[4];
+        static_for<4>([&](auto cc) {
+          constexpr int c = decltype(cc)::value;
+          kt[c] = lds_read_tr8_at<2048 * c>(ka);
+          st[c] = lds_read_tr8_at<1024 * c>(sa);
+        });
+        lgkm_wait<0>();
+        const int nv = nkc - kc0;  // valid chunks of this batch (wave-uniform)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          tie(kt[c]);
+          tie(st[c]);
+          if (c > 0 && nv <= c) st[c] = 0;
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(kt[c], st[c], acc, 0, 0, 0);
         }
-        TDG_F8_MM(ka, sa, kc0)
-        if (hb) {
-          if (kc0 + 8 < nkc) {
-            TDG_F8_RD(ka, sa, kc0 + 8)
-            lgkm_wait<8>();
-          } else {
-            lgkm_wait<0>();
-          }
-          TDG_F8_MM(kb2, sb, kc0 + 4)
-        }
+        ka += 4 * 2048;
+        sa += 4 * 1024;
       }
-#undef TDG_F8_RD
-#undef TDG_F8_MM
       const int q = q0 + 16 * qbk + cl;
       const bool ok = q < a.Lq;
       // (uniform base + 32-bit lane offset: a 64-bit per-lane address kept
@@ -2043,7 +2051,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
       }
     }
   };
-
   // Q / dO tile t by LDS-DMA (waves 0-3, one 1 KiB piece each: wave wq
   // fills tensor wq >> 1, rows 16 (wq & 1) .. +15, lane l the 16-byte
   // position l & 3 of row l >> 2 -- the source piece is swizzled instead of
@@ -2063,120 +2070,132 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
   };
   for (int it = 0; it < nq; ++it) {
     if (it > 0) {
-      wait_vmcnt<0>();  // this tile's DMA (issued a whole step ago)
+      if (w < 4) wait_vmcnt<0>();  // this tile's DMA (issued a whole step ago by waves 0-3)
       lds_barrier();
     }
     const int q0 = it * QT;
-    const char* sQ = ldsQ + 2 * (it & 1) * QIMG;
-    const char* sO = sQ + QIMG;
-    char* sS = ldsS + (it & 1) * SIMG;
-    // dQ of the previous tile first, then the next tile's DMA: a register
-    // reload inside dq_step waits for every VMEM operation in flight
+    // dQ of the previous tile first, then the next tile's DMA
     if (it > 0) dq_step(it - 1);
     if (it + 1 < nq) tile_dma(it + 1);
+    const uint32_t sQa = lQ + 2 * (it & 1) * QIMG;
     long qf[2][2], of[2][2], qT[4], oT[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = 8 * (cl >> 2) + 4 * j + (cl & 3);
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        qf[j][ks] = *reinterpret_cast<const long*>(sQ + f8q_off(row, 4 * ks + g));
-        of[j][ks] = *reinterpret_cast<const long*>(sO + f8q_off(row, 4 * ks + g));
+        qf[j][ks] = lds_read_b64_at<0>(sQa + qo[j][ks]);
+        of[j][ks] = lds_read_b64_at<QIMG>(sQa + qo[j][ks]);
       }
-    }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int row = 8 * g + (cl >> 1);
-      qT[dt] = lds_tr8(sQ + f8q_off(row, 2 * dt + (cl & 1)));
-      oT[dt] = lds_tr8(sO + f8q_off(row, 2 * dt + (cl & 1)));
+      qT[dt] = lds_read_tr8_at<0>(sQa + to[dt]);
+      oT[dt] = lds_read_tr8_at<QIMG>(sQa + to[dt]);
     }
-    // (lse / delta of the lane's queries are re-read per subtile: held across
-    // the subtile loop they pushed the kernel into spilling, and a spill's
-    // reload waits for the tile prefetch in flight)
-    const float* lq = ldsL + q0 + 8 * g;
-    const float* dq4 = ldsD + q0 + 8 * g;
     lgkm_wait<0>();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        tie(qf[j][ks]);
+        tie(of[j][ks]);
+      }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       tie(qT[dt]);
       tie(oT[dt]);
     }
+    const uint32_t sw0 = sob + (it & 1) * SIMG;
+    const uint32_t lgq = lgb + 4 * q0;
     // subtile u: S^T / dP^T, P and dS (e4m3 / e5m2 packed as they stand), the
     // dV^T / dK^T updates and dS^T into the image. (A branch-free copy of this
     // body for the all-active, unmasked case made the compiler spill 262
     // registers: one uniform branch per subtile instead.)
+    static_for<U>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      const int s16 = 16 * (w + NW * u);  // the subtile's first key (wave-uniform)
+      const bool act = s16 < klim && (!causal || s16 <= q0 + QT - 1);
+      long pS = 0;
+      if (act) {
+        // the subtile's K / V row fragments (key on the lane) and the lse /
+        // delta of the lane's 8 queries
+        long kf[2], vf[2];
+        kf[0] = lds_read_b64_at<8192 * u>(kvb0);
+        kf[1] = lds_read_b64_at<8192 * u>(kvb1);
+        vf[0] = lds_read_b64_at<KIMG + 8192 * u>(kvb0);
+        vf[1] = lds_read_b64_at<KIMG + 8192 * u>(kvb1);
+        f32x4 L4[2], D4[2];
+        L4[0] = __builtin_bit_cast(f32x4, lds_read_b128_at<0>(lgq));
+        L4[1] = __builtin_bit_cast(f32x4, lds_read_b128_at<16>(lgq));
+        D4[0] = __builtin_bit_cast(f32x4, lds_read_b128_at<4 * LMAX>(lgq));
+        D4[1] = __builtin_bit_cast(f32x4, lds_read_b128_at<4 * LMAX + 16>(lgq));
+        lgkm_wait<4>();
+        tie(kf[0]);
+        tie(kf[1]);
+        tie(vf[0]);
+        tie(vf[1]);
+        f32x4 s[2], dp[2];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int s16 = 16 * (w + NW * u);  // the subtile's first key (wave-uniform)
-        const bool act = s16 < klim && (!causal || s16 <= q0 + QT - 1);
-        long pS = 0;
-        if (act) {
-          // the subtile's K / V row fragments (key on the lane), from the images
-          long kf[2], vf[2];
+        for (int j = 0; j < 2; ++j) {
+          s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][0], kf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][1], kf[1], s[j], 0, 0, 0);
+          dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][0], vf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][1], vf[1], dp[j], 0, 0, 0);
+        }
+        lgkm_wait<0>();
+        tie(L4[0]);
+        tie(L4[1]);
+        tie(D4[0]);
+        tie(D4[1]);
+        const bool full = s16 + 15 < klim && q0 + QT <= a.Lq && (!causal || s16 + 15 <= q0);
+        float x[2][4];
+        if (full) {
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            kf[ks] = *reinterpret_cast<const long*>(ldsK + f8k_off(s16 + cl, 4 * ks + g));
-            vf[ks] = *reinterpret_cast<const long*>(ldsV + f8k_off(s16 + cl, 4 * ks + g));
-          }
-          f32x4 s[2], dp[2];
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][0], kf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            s[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(qf[j][1], kf[1], s[j], 0, 0, 0);
-            dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][0], vf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(of[j][1], vf[1], dp[j], 0, 0, 0);
-          }
-          const bool full = s16 + 15 < klim && q0 + QT <= a.Lq && (!causal || s16 + 15 <= q0);
-          f32x4 L4[2], D4[2];
+            for (int r = 0; r < 4; ++r) x[j][r] = fmaf(s[j][r], c8, -L4[j][r]);
+        } else {
+          const int key = s16 + cl;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            L4[j] = *reinterpret_cast<const f32x4*>(lq + 4 * j);
-            D4[j] = *reinterpret_cast<const f32x4*>(dq4 + 4 * j);
-          }
-          float x[2][4];
-          if (full) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) x[j][r] = fmaf(s[j][r], c8, -L4[j][r]);
-          } else {
-            const int key = s16 + cl;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int q = q0 + 8 * g + 4 * j + r;
-                const bool ok = (key < klim) & (q < a.Lq) & (!causal | (key <= q));  // (no short circuit)
-                const float xv = fmaf(s[j][r], c8, -L4[j][r]);
-                x[j][r] = ok ? xv : -INFINITY;
-              }
-          }
-          int pw[2], sw[2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            float p[4], ds[4];
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              p[r] = fminf(fast_exp2(x[j][r]), 448.f);
-              ds[r] = p[r] * fmaf(dp[j][r], cdp, -D4[j][r]);
-              amx = fmaxf(amx, fabsf(ds[r]));
-              ds[r] = __builtin_amdgcn_fmed3f(ds[r], -E5M2_MAX_F, E5M2_MAX_F);
+              const int q = q0 + 8 * g + 4 * j + r;
+              const bool ok = (key < klim) & (q < a.Lq) & (!causal | (key <= q));  // (no short circuit)
+              const float xv = fmaf(s[j][r], c8, -L4[j][r]);
+              x[j][r] = ok ? xv : -INFINITY;
             }
-            const int pv = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], 0, false);
-            pw[j] = __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], pv, true);
-            const int sv2 = __builtin_amdgcn_cvt_pk_bf8_f32(ds[0], ds[1], 0, false);
-            sw[j] = __builtin_amdgcn_cvt_pk_bf8_f32(ds[2], ds[3], sv2, true);
-          }
-          const long pP = (long)(uint32_t)pw[0] | ((long)pw[1] << 32);
-          pS = (long)(uint32_t)sw[0] | ((long)sw[1] << 32);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            dv[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(oT[dt], pP, dv[u][dt], 0, 0, 0);
-            dk[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(qT[dt], pS, dk[u][dt], 0, 0, 0);
-          }
         }
-        *reinterpret_cast<long*>(sS + f8s_off(s16 + cl, g)) = pS;
+        int pw[2], sw[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          // 448 P = exp2(x): x <= 0 up to rounding (the forward's LSE over the
+          // same e4m3 products), so 448 P rounds to at most e4m3's 448
+          float p[4], ds[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[r] = fast_exp2(x[j][r]);
+            ds[r] = p[r] * fmaf(dp[j][r], cdp, -D4[j][r]);
+          }
+          amx = fmaxf(amx, fmaxf(fmaxf(fabsf(ds[0]), fabsf(ds[1])), fmaxf(fabsf(ds[2]), fabsf(ds[3]))));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ds[r] = __builtin_amdgcn_fmed3f(ds[r], -E5M2_MAX_F, E5M2_MAX_F);
+          // (the first convert's old operand: any register -- the second one
+          // overwrites its other half)
+          const int pv = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], __float_as_int(p[2]), false);
+          pw[j] = __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], pv, true);
+          const int sv2 = __builtin_amdgcn_cvt_pk_bf8_f32(ds[0], ds[1], __float_as_int(ds[2]), false);
+          sw[j] = __builtin_amdgcn_cvt_pk_bf8_f32(ds[2], ds[3], sv2, true);
+        }
+        const long pP = (long)(uint32_t)pw[0] | ((long)pw[1] << 32);
+        pS = (long)(uint32_t)sw[0] | ((long)sw[1] << 32);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(oT[dt], pP, dv[u][dt], 0, 0, 0);
+          dk[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(qT[dt], pS, dk[u][dt], 0, 0, 0);
+        }
       }
+      lds_write_b64_at<4096 * u>(sw0, pS);
+    });
   }
   wait_vmcnt<0>();
   lds_barrier();
