@@ -448,11 +448,18 @@ def _fp8_dgrad8(g8, g_slot: int, w: Param, out_slot: int, rt: RunCtx) -> torch.T
                               w_plain=fp8.DGRAD_PLAIN_W)
 
 
+def _f8_bwd_planned(rt: RunCtx, lean: bool, Lq: int, Lk: int, hd: int) -> bool:
+    """Forward-time decision: will this (e4m3-forward) attention block's
+    backward run on the fp8 kernel? Then the bf16 copies of its projection
+    outputs are never read and not written. (Not with attention maps: they
+    read the bf16 Q / K.)"""
+    return (lean and fp8.ATTN_BWD_F8 and rt.attn_maps is None and K.attn_bwd_f8_ok(Lq, Lk, hd))
+
+
 def _attn_f8_bwd(ctx, Lq: int, Lk: int, hd: int) -> bool:
-    """Does this attention block's fp8 backward run on the fp8 kernel
-    (its forward ran e4m3 and the shape is covered)?"""
-    return (fp8.ATTN_BWD_F8 and getattr(ctx, "q8", None) is not None
-            and K.attn_bwd_f8_ok(Lq, Lk, hd))
+    """Does this attention block's fp8 backward run on the fp8 kernel (its
+    forward decided so: _f8_bwd_planned, and kept the e4m3 operands)?"""
+    return getattr(ctx, "f8b", False) and getattr(ctx, "q8", None) is not None
 
 
 # =============================================================================== LN helpers
@@ -642,11 +649,14 @@ class SelfAttnBlockFn(torch.autograd.Function):
         kx = [] if lean else None
         if x.is_cuda:
             f8 = rt.fp8 is not None and K.attn_fwd_fp8_ok(L, L, hd)
-            r = rt.fp8.linear(x2, wqkv, bqkv, want8=f8, keep_x8=kx) if rt.fp8 is not None else None
+            # the fp8 backward reads only the e4m3 Q|K|V: no bf16 copy then
+            ctx.f8b = f8 and _f8_bwd_planned(rt, lean, L, L, hd)
+            r = (rt.fp8.linear(x2, wqkv, bqkv, want8=f8, keep_x8=kx, want_y=not ctx.f8b)
+                 if rt.fp8 is not None else None)
             qkv, qkv8 = (r[0], r[1]) if f8 and r is not None else (r, None)
-            if qkv is None:
+            if qkv is None and not ctx.f8b:
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
-            q5 = qkv.view(B, L, 3, heads, hd)
+            q5 = qkv.view(B, L, 3, heads, hd) if qkv is not None else None
             o8e = None
             ctx.q8 = None
             if qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
@@ -665,7 +675,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
             q5 = qkv.view(B, L, 3, heads, hd)
             o, aux = _ref_attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len, causal, scale)
             s = o.reshape(B * L, d) @ wo.master.t() + bo.master
-        if rt.attn_maps is not None:
+        if rt.attn_maps is not None:  # (_f8_bwd_planned: q5 exists when maps are asked for)
             rt.attn_maps[site] = attention_probs(q5[:, :, 0], q5[:, :, 1], kv_len, causal, scale)
         ctx.f8a = None
         if lean:  # e4m3 output projection; keep the e4m3 operands for the backward
@@ -889,9 +899,11 @@ class CrossAttnBlockFn(torch.autograd.Function):
         if x.is_cuda:
             o8e = None
             f8 = (rt.fp8 is not None and rt.fp8.kv8 is not None and K.attn_fwd_fp8_ok(T, S, hd))
-            r = rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx) if rt.fp8 is not None else None
+            ctx.f8b = f8 and _f8_bwd_planned(rt, lean, T, S, hd)
+            r = (rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx, want_y=not ctx.f8b)
+                 if rt.fp8 is not None else None)
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
-            if q is None:
+            if q is None and not ctx.f8b:
                 q = K.linear_fwd(x2, wq.compute, bq.master)
             ctx.q8 = None
             if q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
@@ -915,7 +927,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             o, aux = _ref_attn_fwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], kv_len,
                                    False, scale)
             s = o.reshape(B * T, d) @ wo.master.t() + bo.master
-        if rt.attn_maps is not None:
+        if rt.attn_maps is not None:  # (_f8_bwd_planned: q exists when maps are asked for)
             rt.attn_maps[site] = attention_probs(q.view(B, T, heads, hd), kv5[:, :, 0], kv_len, False, scale)
         ctx.f8a = None
         if lean:  # e4m3 output projection; keep the e4m3 operands for the backward

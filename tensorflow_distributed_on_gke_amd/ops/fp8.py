@@ -517,12 +517,15 @@ class Fp8State:
                 self.proj_bwd[id(w)] = self.gmeta.slot("gp:" + w.name)
         self.weights.calibrate()
 
-    def linear(self, x2: torch.Tensor, w, b, want8: bool = False, keep_x8: Optional[list] = None):
+    def linear(self, x2: torch.Tensor, w, b, want8: bool = False, keep_x8: Optional[list] = None,
+               want_y: bool = True):
         """y = x2 @ w^T + b with e4m3 operands when `w` is an fp8 attention
         projection (the input's e4m3 copy comes from its LayerNorm, else it is
         quantised here); None otherwise. want8: also the e4m3 copy of y from
-        the GEMM epilogue -- returns (y, y8, scale slot of y8). keep_x8 (a
-        list): receives (x8, its scale slot) for the fp8 weight gradient."""
+        the GEMM epilogue -- returns (y, y8, scale slot of y8); want_y = False
+        (with want8): y is not written (None) -- its consumers all read y8.
+        keep_x8 (a list): receives (x8, its scale slot) for the fp8 weight
+        gradient."""
         xs = self.proj_slots.get(id(w))
         if xs is None:
             return None
@@ -536,7 +539,10 @@ class Fp8State:
         ys = self.out_slots[id(w)] if want8 else None
         # want8: y is the dequantised y8 (the attention backward reads y and
         # must see the operands the e4m3 attention forward used)
-        y, y8 = gemm_fp8(x8, w8, b.master, self.meta, xs, ws, out8_slot=ys, c_deq=want8)
+        if want8 and not want_y:
+            y, y8 = gemm_fp8(x8, w8, b.master, self.meta, xs, ws, out8_slot=ys, want_y=False)
+        else:
+            y, y8 = gemm_fp8(x8, w8, b.master, self.meta, xs, ws, out8_slot=ys, c_deq=want8)
         return (y, y8, ys) if want8 else y
 
     def o8_for(self, w, shape, device):

@@ -206,7 +206,8 @@ def test_attention_fwd_fp8(causal, Lq, Lk):
 
 def test_fp8_attention_training_tracks_bf16(monkeypatch):
     """fp8 mode with e4m3 attention (hd 64, sequences > 128: the input
-    projections emit e4m3 Q|K|V, attn_fwd_fp8 consumes them) trains like
+    projections emit e4m3 Q|K|V, attn_fwd_fp8 consumes them, the fp8
+    attention backward attn_bwd_f8 runs on them and an e5m2 dO) trains like
     bf16 on the copy task."""
     from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
@@ -214,14 +215,19 @@ def test_fp8_attention_training_tracks_bf16(monkeypatch):
     from tensorflow_distributed_on_gke_amd.train.optim import Adam
     from tensorflow_distributed_on_gke_amd.train.step import TrainStep
 
-    calls = {"n": 0}
-    real = kk.attn_fwd_fp8
+    calls = {"n": 0, "bwd": 0}
+    real, real_bwd = kk.attn_fwd_fp8, kk.attn_bwd_f8
 
     def counting(*a, **k):
         calls["n"] += 1
         return real(*a, **k)
 
+    def counting_bwd(*a, **k):
+        calls["bwd"] += 1
+        return real_bwd(*a, **k)
+
     monkeypatch.setattr(kk, "attn_fwd_fp8", counting)
+    monkeypatch.setattr(kk, "attn_bwd_f8", counting_bwd)
     cfg = model_config("tiny", heads=2, src_vocab=64, tgt_vocab=64, dropout=0.0)
     data = SyntheticPairs(batch=8, src_len=160, tgt_len=161, src_vocab=64, tgt_vocab=64, copy_task=True, seed=0)
     finals = {}
@@ -236,6 +242,7 @@ def test_fp8_attention_training_tracks_bf16(monkeypatch):
             losses.append(step(src.cuda(), tgt.cuda())[0].item())
         finals[mode] = (losses[0], sum(losses[-10:]) / 10)
     assert calls["n"] > 0, "e4m3 attention did not run"
+    assert calls["bwd"] > 0 or not F.ATTN_BWD_F8, "the fp8 attention backward did not run"
     (b0, b1), (f0, f1) = finals["bf16"], finals["fp8"]
     assert b1 < 0.9 * b0 and f1 < 0.9 * f0, finals  # (long copy task: slower start)
     assert abs(f1 - b1) < 0.1 * b1 + 0.05, finals
