@@ -340,6 +340,15 @@ void colsum(const Tensor& X, const Tensor& out, const Tensor& part, int64_t M, i
 }
 
 // ---------------------------------------------------------------- attention
+// XCD-grouped workgroup order of the attention kernels (tdg_attn.h xcd):
+// TDG_ATTN_XCD=0 restores the plain grid order
+static int attn_xcd() {
+  static const int v = [] {
+    const char* e = getenv("TDG_ATTN_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
 // q/k/v/o/do/dq/dk/dv are 4-D [B, L, H, hd] views (any strides, hd contiguous).
 void fill_qkv(tdg::AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
   for (auto* t : {&q, &k, &v}) {
@@ -379,6 +388,7 @@ void check_like(const Tensor& t, const tdg::AttnArgs& a, int L, const char* n) {
 void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out,
               const Tensor& lse, const optional<Tensor>& kv_len, double scale, bool causal) {
   tdg::AttnArgs a{};
+  a.xcd = attn_xcd();
   fill_qkv(a, q, k, v);
   check_like(out, a, a.Lq, "out");
   check_f32(lse, "lse");
@@ -418,6 +428,7 @@ void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Te
                   q8.stride(1) % 8 == 0 && q8.stride(2) % 8 == 0,
               "attn_fwd_fp8: Q rows must be 8-byte aligned");
   tdg::AttnArgs a{};
+  a.xcd = attn_xcd();
   a.B = (int)q8.size(0);
   a.Lq = (int)q8.size(1);
   a.H = (int)q8.size(2);
@@ -468,6 +479,7 @@ static tdg::AttnArgs attn_bwd_args(const Tensor& q, const Tensor& k, const Tenso
                                    const Tensor& dv, const optional<Tensor>& kv_len, double scale,
                                    bool causal) {
   tdg::AttnArgs a{};
+  a.xcd = attn_xcd();
   fill_qkv(a, q, k, v);
   check_like(o, a, a.Lq, "o");
   check_like(dout, a, a.Lq, "dout");
@@ -595,6 +607,7 @@ void attn_bwd_f8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Ten
   check_f8_fmt(do8, 1, "attn_bwd_f8 do8");
   rows16(do8, "attn_bwd_f8 do8");
   tdg::AttnArgs a{};
+  a.xcd = attn_xcd();
   a.B = (int)q8.size(0);
   a.Lq = (int)q8.size(1);
   a.H = (int)q8.size(2);
@@ -684,6 +697,7 @@ void attn_bwd_f8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Ten
 void attn_probs(const Tensor& q, const Tensor& k, const Tensor& probs,
                 const optional<Tensor>& kv_len, double scale, bool causal) {
   tdg::AttnArgs a{};
+  a.xcd = attn_xcd();
   fill_qkv(a, q, k, k);
   check_f32(probs, "probs");
   check_contig(probs, "probs");

@@ -53,5 +53,10 @@ struct AttnArgs {
   const float* sdo8;
   const float* sds8;
   unsigned* amaxds8;
+  // workgroup -> (block, head, batch) order: 1 = XCD-grouped by batch (each
+  // XCD takes a contiguous run of batch elements, as the projection GEMMs'
+  // xcd_remap'd tiles do: their Q/K/V / dO tiles are then in that XCD's L2),
+  // 0 = the plain grid order (one head per XCD)
+  int xcd;
 };
 }  // namespace tdg

@@ -110,6 +110,18 @@ __device__ __forceinline__ void key_window(const AttnArgs& a, int b, int& klim, 
     }
   }
 }
+// (block, head, batch) of this workgroup over a (blocks, H, B) grid; with
+// a.xcd the linear order is xcd_remap'd (tdg_common.h), so the XCD that ran
+// the projection GEMM tiles of a batch element's rows (their run of tile ids
+// covers whole row bands) also runs that element's attention workgroups
+__device__ __forceinline__ void attn_coords(const AttnArgs& a, int& xb, int& h, int& b) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  int t = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if (a.xcd) t = xcd_remap(t, gx * gy * gridDim.z);
+  xb = t % gx;
+  h = (t / gx) % gy;
+  b = t / (gx * gy);
+}
 constexpr int QB = 64;  // rows per workgroup
 constexpr int KB = 64;  // keys per tile
 
@@ -351,7 +363,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
   char* ldsK = smem;
   char* ldsV = smem + (KT / 64) * T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int q0 = xb * QBW;
   int qrow[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
@@ -479,7 +493,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int q0 = xb * QBW;
   int qrow[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
@@ -628,7 +644,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   const uint8_t* v8 = reinterpret_cast<const uint8_t*>(a.v);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int q0 = xb * QBW;
   const int qrow = q0 + 16 * w + cl;
   int klim;
   float scl;
@@ -817,7 +835,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   float* ldsD = ldsL + QB;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int k0 = xb * KBW;
   int key[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) key[u] = k0 + 16 * (U * w + u) + cl;
@@ -960,7 +980,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   char* ldsV = smem + T::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int q0 = xb * QBW;
   int qrow[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
@@ -1159,7 +1181,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * KBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int k0 = xb * KBW;
   int key[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) key[u] = k0 + 16 * (U * w + u) + cl;
@@ -1366,7 +1390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   if (a.dk8) {  // e5m2 dK / dV (+ amax, + bias-gradient partials)
     const float s8 = a.sg8[0];
     float* red = reinterpret_cast<float*>(smem);
-    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + blockIdx.x) * a.cs_ld + h * 64 : nullptr;
+    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + xb) * a.cs_ld + h * 64 : nullptr;
     attn_emit_g8<U>(dk, a.scale, key, a.Lk, a.dk8 + b * a.dk_sb + h * a.dk_sh, a.dk_sl, s8, a.amaxg8,
                     prow ? prow + a.cs_k : nullptr, red, lane, w);
     attn_emit_g8<U>(dv, 1.f, key, a.Lk, a.dv8 + b * a.dv_sb + h * a.dv_sh, a.dv_sl, s8, a.amaxg8,
@@ -1386,7 +1410,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QBW;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
+  const int q0 = xb * QBW;
   int qrow[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) qrow[u] = q0 + 16 * (U * w + u) + cl;
@@ -1570,7 +1596,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   }
   }
   if (a.dq8) {  // e5m2 dQ (+ amax, + bias-gradient partials)
-    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + blockIdx.x) * a.cs_ld + h * 64 + a.cs_q
+    float* prow = a.cs_part ? a.cs_part + ((long long)b * a.cs_np + xb) * a.cs_ld + h * 64 + a.cs_q
                             : nullptr;
     attn_emit_g8<U>(dq, a.scale, qrow, a.Lq, a.dq8 + b * a.dq_sb + h * a.dq_sh, a.dq_sl, a.sg8[0],
                     a.amaxg8, prow, reinterpret_cast<float*>(smem), lane, w);
@@ -1610,7 +1636,7 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
   float* ldsD = ldsL + R;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
-  const int bh = blockIdx.x;
+  const int bh = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int b = bh / a.H, h = bh % a.H;
   int klim;
   float scl;
@@ -1892,7 +1918,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
   float* ldsD = ldsL + LMAX;                                 // delta * sds / 448
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.z, h = blockIdx.y;
+  int xb, h, b;
+  attn_coords(a, xb, h, b);
   int klim;
   float scl;
   bool causal;
