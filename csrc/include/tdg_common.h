@@ -61,15 +61,42 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------- reductions
+// Whole-wave sum / max without the LDS crossbar: DPP row rotations (by 8, 4,
+// 2, 1 within each 16-lane row: pairs combine symmetrically, every lane of a
+// row ends with the same value), then the GFX9 row broadcasts (row_bcast:15
+// into rows 1 and 3, row_bcast:31 into rows 2 and 3) and lane 63 read out as
+// a scalar -- the bitwise-same value in every lane. The __shfl_xor butterfly
+// compiles to ds_bpermute_b32, whose lanes l and l + 32 hit the same LDS bank
+// on every step (the LayerNorm backward's 14 % conflict cycles,
+// profiles/r4/pmc_base_end_round4.txt). (v_permlane16/32_swap of a register
+// with a copy of itself folded to one operand under -O3: not used here.)
+// Every lane of the wave must be active.
+template <int CTRL, int ROWS = 0xF, bool BC = true>
+__device__ __forceinline__ float dpp_f(float v, float old = 0.f) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, v), CTRL, ROWS,
+                                                               0xF, BC));
+}
+__device__ __forceinline__ float lane63(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0x128>(v);  // row_ror:8
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x122>(v);  // row_ror:2
+  v += dpp_f<0x121>(v);  // row_ror:1
+  v += dpp_f<0x142, 0xA, false>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xC, false>(v);  // row_bcast:31 -> rows 2, 3
+  return lane63(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_f<0x128>(v, v));
+  v = fmaxf(v, dpp_f<0x124>(v, v));
+  v = fmaxf(v, dpp_f<0x122>(v, v));
+  v = fmaxf(v, dpp_f<0x121>(v, v));
+  v = fmaxf(v, dpp_f<0x142, 0xA, false>(v, v));
+  v = fmaxf(v, dpp_f<0x143, 0xC, false>(v, v));
+  return lane63(v);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
