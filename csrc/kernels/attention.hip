@@ -1618,10 +1618,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 // U: 16-key (phase 1) / 16-query (phase 2) subtiles per wave, 8 / U waves.
 // U = 2 reads every Q / dO / K fragment from LDS once for two MFMAs (the
 // U = 1 loops issue one LDS read per MFMA).
+// dS^T image of the fused backward: 128 key rows x 128 queries (bf16, 256-B
+// rows). ATile<128>'s 32-byte segment swizzle (segment ^ row & 7) keeps the
+// transposing dQ-phase reads conflict-free, but the key-row-per-lane 8-byte
+// stores of a 16-lane group (one row each, the same column) then land on only
+// 4 bank positions (a 256-B row is 0 mod 32 banks): 4-way conflicts. Rows with
+// bit 3 set also swap the 16-byte halves of each segment: 2-way for the stores,
+// the reads (8 consecutive rows per 32-lane half, bit 3 constant) unchanged.
+struct DsImg {
+  static constexpr int RB = 256;
+  __device__ static __forceinline__ int off(int row, int byte) {
+    const int seg = (byte >> 5) ^ (row & 7);
+    return row * RB + (seg << 5) + ((byte & 31) ^ (((row >> 3) & 1) << 4));
+  }
+  // ATile<128>::frag_tr with this image's offsets
+  __device__ static __forceinline__ short8_t frag_tr(const char* lds, int s2, int dt, int lane) {
+    const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+    const int r1 = 32 * s2 + 4 * g + q;
+    const int byte = (16 * dt + 4 * p) * 2;
+    return cat4(lds_read_tr(lds + off(r1, byte)), lds_read_tr(lds + off(r1 + 16, byte)));
+  }
+};
+
 template <int HD, int U>
 __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 ? (HD <= 64 ? 4 : 2) : 2))) void attn_bwd_fused_kernel(AttnArgs a) {
   using T = ATile<HD>;
-  using TS = ATile<128>;  // dS image: 128 key rows x 128 queries (bf16)
+  using TS = DsImg;  // dS image: 128 key rows x 128 queries (bf16)
   constexpr int R = 128;
   constexpr int NT = 512 / U;  // threads
   constexpr int TB = R * T::RB;  // bytes of one 128-row tile image
