@@ -593,7 +593,8 @@ void attn_bwd_f8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Ten
                  const optional<Tensor>& dk8, const optional<Tensor>& dv8,
                  const optional<Tensor>& sg8, const optional<Tensor>& amaxg8,
                  const optional<Tensor>& cs_part, int64_t cs_ld, int64_t cs_q, int64_t cs_k,
-                 int64_t cs_v) {
+                 int64_t cs_v, const optional<Tensor>& sgkv8, const optional<Tensor>& amaxgkv8,
+                 const optional<Tensor>& cs_part2, int64_t cs_ld2) {
   auto rows16 = [](const Tensor& t, const char* n) {
     TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.size(3) == 64, n, ": [B,L,H,64] with hd contiguous");
     TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0 && t.stride(0) % 16 == 0 &&
@@ -676,12 +677,28 @@ void attn_bwd_f8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Ten
     a.sg8 = sg8->data_ptr<float>();
     a.amaxg8 = amax_ptr(amaxg8);
   }
+  // dK / dV e5m2 in a slot of their own (scale + amax together)
+  TORCH_CHECK(sgkv8.has_value() == amaxgkv8.has_value(), "attn_bwd_f8: sgkv8 with amaxgkv8");
+  if (sgkv8.has_value()) {
+    TORCH_CHECK(dk8.has_value(), "attn_bwd_f8: sgkv8 needs dk8 / dv8");
+    check_f32(*sgkv8, "sgkv8");
+    a.sgkv8 = sgkv8->data_ptr<float>();
+    a.amaxgkv8 = amax_ptr(amaxgkv8);
+  }
+  const int64_t ld2 = cs_part2.has_value() ? cs_ld2 : cs_ld;
+  if (cs_part2.has_value()) {
+    TORCH_CHECK(cs_part.has_value() && dk8.has_value(), "attn_bwd_f8: cs_part2 needs cs_part and dk8");
+    check_f32(*cs_part2, "cs_part2");
+    TORCH_CHECK(cs_part2->numel() >= (int64_t)a.B * cs_ld2, "attn_bwd_f8: cs_part2 extent");
+    a.cs_part2 = cs_part2->data_ptr<float>();
+    a.cs_ld2 = (int)cs_ld2;
+  }
   if (cs_part.has_value()) {
     TORCH_CHECK(dq8.has_value(), "attn_bwd_f8: column sums come with the e5m2 outputs");
     check_f32(*cs_part, "cs_part");
     TORCH_CHECK(cs_part->numel() >= (int64_t)a.B * cs_ld && cs_q >= 0 && cs_q + a.H * 64 <= cs_ld &&
-                    (!dk8.has_value() || (cs_k >= 0 && cs_v >= 0 && cs_k + a.H * 64 <= cs_ld &&
-                                          cs_v + a.H * 64 <= cs_ld)),
+                    (!dk8.has_value() || (cs_k >= 0 && cs_v >= 0 && cs_k + a.H * 64 <= ld2 &&
+                                          cs_v + a.H * 64 <= ld2)),
                 "attn_bwd_f8: column-sum partial extent");
     a.cs_part = cs_part->data_ptr<float>();
     a.cs_np = 1;

@@ -53,6 +53,14 @@ struct AttnArgs {
   const float* sdo8;
   const float* sds8;
   unsigned* amaxds8;
+  // fp8 backward, separate e5m2 format of dK / dV (the batched cross K|V
+  // gradient of the decoder layers): scale / amax slot of dk8 / dv8 when
+  // non-null (else sg8 / amaxg8), and their bias-gradient column sums into
+  // cs_part2[b * cs_ld2 + cs_k / cs_v + h * 64 + col] when non-null
+  const float* sgkv8;
+  unsigned* amaxgkv8;
+  float* cs_part2;
+  int cs_ld2;
   // workgroup -> (block, head, batch) order: 1 = XCD-grouped by batch (each
   // XCD takes a contiguous run of batch elements, as the projection GEMMs'
   // xcd_remap'd tiles do: their Q/K/V / dO tiles are then in that XCD's L2),

@@ -2253,6 +2253,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
   // ---- epilogue: dK / dV (key rows on lanes) bf16 and / or e5m2, amax and
   // the bias-gradient column sums (dQ's, dK's, dV's) of this (b, h)
   const float gk = a.scale / (sds * sq), gv = 1.f / (448.f * sdo);
+  const float s8kv = a.sgkv8 ? a.sgkv8[0] : s8;  // dK / dV e5m2 scale
   float csk[4][4], csv[4][4], amk = 0.f;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -2279,10 +2280,10 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
                              __uint_as_float(khi[dt] << 16), __uint_as_float(khi[dt] & 0xffff0000u)};
         const float v4[4] = {__uint_as_float(vlo[dt] << 16), __uint_as_float(vlo[dt] & 0xffff0000u),
                              __uint_as_float(vhi[dt] << 16), __uint_as_float(vhi[dt] & 0xffff0000u)};
-        int wk = pack2_e5m2c<false>(k4[0] * s8, k4[1] * s8, 0);
-        wk = pack2_e5m2c<true>(k4[2] * s8, k4[3] * s8, wk);
-        int wv = pack2_e5m2c<false>(v4[0] * s8, v4[1] * s8, 0);
-        wv = pack2_e5m2c<true>(v4[2] * s8, v4[3] * s8, wv);
+        int wk = pack2_e5m2c<false>(k4[0] * s8kv, k4[1] * s8kv, 0);
+        wk = pack2_e5m2c<true>(k4[2] * s8kv, k4[3] * s8kv, wk);
+        int wv = pack2_e5m2c<false>(v4[0] * s8kv, v4[1] * s8kv, 0);
+        wv = pack2_e5m2c<true>(v4[2] * s8kv, v4[3] * s8kv, wv);
         if (ok) {
           *reinterpret_cast<int*>(a.dk8 + offk + 16 * dt + 4 * g) = wk;
           *reinterpret_cast<int*>(a.dv8 + offv + 16 * dt + 4 * g) = wv;
@@ -2299,8 +2300,14 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
   // amax: dS (its own slot), the gradients (the projection's e5m2 slot)
   amx = wave_max(amx);
   if (lane == 0 && a.amaxds8) atomic_amax(amax_word(a.amaxds8, b * 7 + h * 13 + w), amx / sds);
-  const float amg = wave_max(fmaxf(amq, amk));
-  if (lane == 0 && a.amaxg8 && (a.dq8 || a.dk8)) atomic_amax(amax_word(a.amaxg8, b * 5 + h * 11 + w), amg);
+  if (a.amaxgkv8) {  // dK / dV in their own slot
+    const float amq_w = wave_max(amq), amk_w = wave_max(amk);
+    if (lane == 0 && a.amaxg8 && a.dq8) atomic_amax(amax_word(a.amaxg8, b * 5 + h * 11 + w), amq_w);
+    if (lane == 0 && a.dk8) atomic_amax(amax_word(a.amaxgkv8, b * 5 + h * 11 + w), amk_w);
+  } else {
+    const float amg = wave_max(fmaxf(amq, amk));
+    if (lane == 0 && a.amaxg8 && (a.dq8 || a.dk8)) atomic_amax(amax_word(a.amaxg8, b * 5 + h * 11 + w), amg);
+  }
   if (!a.cs_part) return;
   // column sums: over the wave's 16 rows per lane group (shuffles), then the
   // waves through LDS (the Q / dO ring is free: every read of it is behind the
@@ -2335,12 +2342,14 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_f8_kernel(AttnArgs a) {
   }
   __syncthreads();
   float* prow = a.cs_part + ((long long)b * a.cs_np) * a.cs_ld + h * 64;
+  float* prow2 = a.cs_part2 ? a.cs_part2 + (long long)b * a.cs_ld2 + h * 64 : prow;
   if (tid < 64 * (a.dk8 ? 3 : 1)) {
     const int m = tid >> 6, col = tid & 63;
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) sum += red[(m * NW + i) * 64 + col];
-    prow[(m == 0 ? a.cs_q : m == 1 ? a.cs_k : a.cs_v) + col] = sum;
+    if (m == 0) prow[a.cs_q + col] = sum;
+    else prow2[(m == 1 ? a.cs_k : a.cs_v) + col] = sum;
   }
 }
 

@@ -82,9 +82,19 @@ class RunCtx:
 @dataclass
 class KVGrad:
     """Side channel collecting every decoder layer's d(K|V) into one buffer so
-    the cross-K/V projection backward is a single GEMM pair."""
+    the cross-K/V projection backward is a single GEMM pair. With the fp8
+    attention backward on every decoder layer (`f8b`, decided by the forward
+    of CrossKVFn), the layers write the e5m2 d(K|V) straight into `buf8` and
+    their bias-gradient column sums into `part` ([B, layers * 2d]), and the
+    bf16 K|V / d(K|V) are never materialised."""
 
     buf: Optional[torch.Tensor] = None
+    dec_len: int = 0  # decoder sequence length of this forward (Transformer.decode)
+    heads: int = 0
+    f8b: bool = False
+    buf8: Optional[torch.Tensor] = None
+    part: Optional[torch.Tensor] = None
+    wkv: Optional["Param"] = None  # the batched K|V projection (its e5m2 gradient slot)
 
 
 @dataclass(eq=False)
@@ -817,15 +827,23 @@ class CrossKVFn(torch.autograd.Function):
         ctx.lean = lean = enc.is_cuda and _attn_lean(rt, B * S, wkv, None, d)
         kx = [] if lean else None
         ctx.f8a = None
+        T = kvh.dec_len
+        hd = d // kvh.heads if kvh.heads else 0
+        # every decoder layer's cross-attention runs e4m3 forward + fp8
+        # backward: the bf16 K|V are never read (and d(K|V) come as e5m2)
+        kvh.f8b = bool(lean and enc.is_cuda and T and K.attn_fwd_fp8_ok(T, S, hd)
+                       and fp8.wgrad_fp8_ok(B * T, d, d) and _f8_bwd_planned(rt, True, T, S, hd))
         if enc.is_cuda:
             kv = None
             if rt.fp8 is not None:
-                r = rt.fp8.linear(e2.contiguous(), wkv, bkv, want8=True, keep_x8=kx)
+                r = rt.fp8.linear(e2.contiguous(), wkv, bkv, want8=True, keep_x8=kx, want_y=not kvh.f8b)
                 if lean and r is not None:
                     ctx.f8a = tuple(kx)
                 if r is not None:  # its e4m3 copy feeds the decoders' e4m3 attention
                     kv = r[0]
                     rt.fp8.kv8 = (r[1].view(B, S, -1), r[2])
+                    if kvh.f8b:  # (autograd needs the output tensor; its values are never read)
+                        kv = torch.empty(B * S, r[1].shape[1], dtype=torch.bfloat16, device=enc.device)
             if kv is None:
                 kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
         else:
@@ -840,8 +858,9 @@ class CrossKVFn(torch.autograd.Function):
         (e2,) = ctx.saved_tensors
         # filled slice-by-slice by every CrossAttnBlockFn.backward (layer 0
         # also hands it to autograd, which delivers it here as dkv_in)
-        dkv = (dkv_in if dkv_in is not None else ctx.kvh.buf).reshape(B * S, -1)
-        ctx.kvh.buf = None
+        kvh = ctx.kvh
+        dkv = (dkv_in if dkv_in is not None else kvh.buf).reshape(B * S, -1)
+        kvh.buf = None
         N = wkv.shape[0]
         bt = _beta(rt)
         if e2.is_cuda and ctx.f8a is not None:
@@ -850,7 +869,12 @@ class CrossKVFn(torch.autograd.Function):
             st = rt.fp8
             x8, xs = ctx.f8a
             gk = st.proj_bwd[id(wkv)]
-            dkv8 = _fp8_grad_bias(dkv.contiguous(), gk, bkv, rt, "kv")
+            if kvh.f8b:  # written by the layers' fp8 attention backward (e5m2 + bias sums)
+                dkv8 = kvh.buf8.reshape(B * S, -1)
+                _fold_bias_later(rt, kvh.part, B, N, bkv)
+                kvh.buf8 = kvh.part = None
+            else:
+                dkv8 = _fp8_grad_bias(dkv.contiguous(), gk, bkv, rt, "kv")
             rt.wgrad.add_fp8(dkv8, st.gmeta.s(gk), x8, st.meta.s(xs), wkv, bt, rt)
             rt.wgrad.boundary()
             denc = torch.empty(B * S, d, dtype=torch.bfloat16, device=dkv.device)
@@ -900,6 +924,9 @@ class CrossAttnBlockFn(torch.autograd.Function):
             o8e = None
             f8 = (rt.fp8 is not None and rt.fp8.kv8 is not None and K.attn_fwd_fp8_ok(T, S, hd))
             ctx.f8b = f8 and _f8_bwd_planned(rt, lean, T, S, hd)
+            if kvh.f8b and not ctx.f8b:
+                raise RuntimeError("cross-attention: the batched K|V were produced for the fp8 "
+                                   "backward (no bf16 copy) but this layer does not run it")
             r = (rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx, want_y=not ctx.f8b)
                  if rt.fp8 is not None else None)
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
@@ -973,12 +1000,26 @@ class CrossAttnBlockFn(torch.autograd.Function):
                 skv = st.meta.s(kvs)
                 dq8 = torch.empty(M, d, dtype=st.gmeta.dtype, device=dy.device)
                 part = K.workspace(f"f8cs_q{site}", B * d, dy.device)
+                if kvh.f8b:
+                    # e5m2 d(K|V) straight into the batched buffer (the cross K|V
+                    # projection's gradient slot), bias sums into kvh.part
+                    NKV = kv_all.shape[2]
+                    if kvh.buf8 is None:
+                        kvh.buf8 = torch.empty(B, S, NKV, dtype=st.gmeta.dtype, device=dy.device)
+                        kvh.part = torch.empty(B, NKV, dtype=torch.float32, device=dy.device)
+                    g85 = kvh.buf8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+                    gk = st.proj_bwd[id(kvh.wkv)]
+                    kvo = dict(dk8=g85[:, :, 0], dv8=g85[:, :, 1], sgkv8=st.gmeta.s(gk),
+                               amaxgkv8=st.gmeta.a(gk), cs_part2=kvh.part, cs_ld2=NKV,
+                               cs_k=layer * 2 * d, cs_v=layer * 2 * d + d)
+                else:
+                    kvo = dict(dk=g5[:, :, 0], dv=g5[:, :, 1])
                 nparts = K.attn_bwd_f8(q8.view(B, T, heads, hd), kv85[:, :, 0], kv85[:, :, 1],
                                        st.meta.s(qs), skv, skv, o, do8.view(B, T, heads, hd),
                                        st.gmeta.s(gdo), aux, kv_len, scale, False, st.gmeta.s(gds),
-                                       st.gmeta.a(gds), dk=g5[:, :, 0], dv=g5[:, :, 1],
-                                       dq8=dq8.view(B, T, heads, hd), sg8=st.gmeta.s(gq),
-                                       amaxg8=st.gmeta.a(gq), cs_part=part, cs_ld=d, cs_q=0)
+                                       st.gmeta.a(gds), dq8=dq8.view(B, T, heads, hd),
+                                       sg8=st.gmeta.s(gq), amaxg8=st.gmeta.a(gq), cs_part=part,
+                                       cs_ld=d, cs_q=0, **kvo)
                 _fold_bias_later(rt, part[: nparts * d], nparts, d, bq)
                 _fp8_dgrad_into(dq8, gq, wq, dh.view(M, d), rt, 1.0)
                 rt.wgrad.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)

@@ -250,6 +250,7 @@ class Transformer:
         if tgt_in.shape[1] > self.cfg.max_tgt_len:
             raise ValueError(f"target length {tgt_in.shape[1]} > positional table {self.cfg.max_tgt_len}")
         kvh = KVGrad()
+        kvh.dec_len, kvh.heads, kvh.wkv = tgt_in.shape[1], self.cfg.heads, self.cross_kv.w
         kv_all = CrossKVFn.apply(enc, self.cross_kv.w, self.cross_kv.b, kvh, rt)
         x = EmbedFn.apply(self.store.anchor, tgt_in.contiguous(), self.dec_emb, self.pe_tgt, self.dec_site, rt)
         try:

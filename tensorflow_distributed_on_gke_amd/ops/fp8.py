@@ -314,6 +314,38 @@ def choose_fp8(M: int, N: int, Kd: int) -> int:
     return 5
 
 
+def _tkey_str(k: tuple) -> str:
+    return ",".join(str(int(x)) for x in k)
+
+
+def save_tuned(path: str) -> None:
+    """Persist the fp8 forward GEMM tile choices (JSON: "M,N,K,epi,y8,y" ->
+    cfg), e.g. from scripts/tune_fp8_in_model.py."""
+    import json
+
+    with open(path, "w") as f:
+        json.dump({_tkey_str(k): v for k, v in sorted(_TUNED.items())}, f, indent=0)
+
+
+def load_tuned(path: str) -> int:
+    import json
+
+    if not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        data = json.load(f)
+    for ks, v in data.items():
+        M, N, Kd, epi, y8, y = (int(x) for x in ks.split(","))
+        _TUNED[(M, N, Kd, epi, bool(y8), bool(y))] = int(v)
+    return len(data)
+
+
+# in-model measured tiles of the Transformer-big fp8 forward GEMMs
+# (scripts/tune_fp8_in_model.py); shapes not in it: choose_fp8
+TUNED_FILE = os.environ.get("TDG_FP8_TUNED_FILE") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "fp8_tuned_gfx950.json")
+
+
 def _autotune(run) -> int:
     times = {}
     for rnd in range(2):
@@ -582,3 +614,6 @@ class Fp8State:
         reads anything the optimizer writes)."""
         self.meta.update()
         self.gmeta.update()
+
+
+load_tuned(TUNED_FILE)

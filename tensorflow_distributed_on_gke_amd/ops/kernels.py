@@ -414,16 +414,19 @@ def attn_bwd_f8_ok(Lq: int, Lk: int, hd: int) -> bool:
 def attn_bwd_f8(q8, k8, v8, sq, sk, sv, o, do8, sdo, lse, kv_len, scale: float, causal: bool,
                 sds, amaxds, dq=None, dk=None, dv=None, dq8=None, dk8=None, dv8=None, sg8=None,
                 amaxg8=None, cs_part=None, cs_ld: int = 0, cs_q: int = 0, cs_k: int = 0,
-                cs_v: int = 0) -> int:
+                cs_v: int = 0, sgkv8=None, amaxgkv8=None, cs_part2=None, cs_ld2: int = 0) -> int:
     """Attention backward on fp8 MFMAs: the forward's e4m3 q8 / k8 / v8
     (scales sq / sk / sv), the e5m2 do8 (scale sdo), bf16 o and the forward's
     lse; dS in e5m2 with scale sds (its amax into the slot amaxds). Writes each
     given output: bf16 dq / dk / dv, e5m2 dq8 / dk8 / dv8 = e5m2(bf16(grad) *
     sg8) (amax into amaxg8) and the bias-gradient column sums of the e5m2
     outputs, one row per batch element: cs_part[b, cs_{q,k,v} + head * 64 + j].
-    Returns the partial row count (B)."""
+    sgkv8 / amaxgkv8: dk8 / dv8 in their own e5m2 slot (the batched cross
+    K|V gradient); cs_part2 / cs_ld2: their column sums in a buffer of their
+    own. Returns the partial row count (B)."""
     C().attn_bwd_f8(q8, k8, v8, sq, sk, sv, o, do8, sdo, lse, kv_len, scale, causal, sds, amaxds,
-                    dq, dk, dv, dq8, dk8, dv8, sg8, amaxg8, cs_part, cs_ld, cs_q, cs_k, cs_v)
+                    dq, dk, dv, dq8, dk8, dv8, sg8, amaxg8, cs_part, cs_ld, cs_q, cs_k, cs_v, sgkv8,
+                    amaxgkv8, cs_part2, cs_ld2)
     return q8.shape[0]
 
 

@@ -500,6 +500,46 @@ def test_fp8_attention_projection_grads_match_bf16_path(monkeypatch):
         assert rel < 0.15, (n, rel)
 
 
+def test_fp8_attention_backward_grads_match_bf16_backward(monkeypatch):
+    """Sequences > 128 (the fp8 attention backward, and with it the e5m2
+    cross K|V gradient written straight by the decoder layers' kernels) vs
+    the same fp8 step with the bf16 attention backward: projection weight /
+    bias gradients within fp8 gradient noise, same loss."""
+    from tensorflow_distributed_on_gke_amd.data.synthetic import SyntheticPairs
+    from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
+    from tensorflow_distributed_on_gke_amd.models.layers import RunCtx, WgradQueue
+
+    cfg = model_config("tiny", heads=2, src_vocab=64, tgt_vocab=64, dropout=0.0)
+    data = SyntheticPairs(batch=8, src_len=160, tgt_len=161, src_vocab=64, tgt_vocab=64, copy_task=True, seed=0)
+    src, tgt = (t.cuda() for t in data.batch(0))
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(F, "ATTN_BWD_F8", mode)
+        m = Transformer(cfg).build("cuda", seed=1)
+        st = F.Fp8State(m)
+        rt = RunCtx(training=True, dropout=0.0, seed=3, store=m.store, fp8=st,
+                    ctr=torch.zeros(1, dtype=torch.int64, device="cuda"))
+        rt.wgrad = WgradQueue()
+        rt.wgrad.layers_per_step = 2 * cfg.layers
+        for _ in range(2):  # second step: delayed scales (dO, dS, gradients) calibrated
+            m.store.zero_grad()
+            out = m.loss_and_backward(src, tgt, rt, 1.0)
+            st.after_step()
+        torch.cuda.synchronize()
+        ps = [m.cross_kv.w, m.cross_kv.b]
+        for l in m.enc_layers:
+            ps += [l.qkv.w, l.qkv.b]
+        for l in m.dec_layers:
+            ps += [l.qkv1.w, l.q2.w, l.q2.b]
+        res[mode] = (float(out[0]), {p.name: p.grad.clone() for p in ps})
+    (l16, g16), (l8, g8) = res[False], res[True]
+    assert abs(l8 - l16) < 0.02 * abs(l16)
+    for n, a in g16.items():
+        assert torch.isfinite(g8[n]).all(), n
+        rel = ((g8[n] - a).norm() / (a.norm() + 1e-12)).item()
+        assert rel < 0.2, (n, rel)
+
+
 @pytest.mark.parametrize("R,NC", [(1024, 3072), (300, 520), (64, 8)])
 def test_quant_t_matches_transpose_then_quantize(R, NC):
     """The transposing weight quantisation equals quantising the transposed
