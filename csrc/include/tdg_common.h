@@ -68,8 +68,7 @@ __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) 
 // a scalar -- the bitwise-same value in every lane. The __shfl_xor butterfly
 // compiles to ds_bpermute_b32, whose lanes l and l + 32 hit the same LDS bank
 // on every step (the LayerNorm backward's 14 % conflict cycles,
-// profiles/r4/pmc_base_end_round4.txt). (v_permlane16/32_swap of a register
-// with a copy of itself folded to one operand under -O3: not used here.)
+// profiles/r4/pmc_base_end_round4.txt).
 // Every lane of the wave must be active.
 template <int CTRL, int ROWS = 0xF, bool BC = true>
 __device__ __forceinline__ float dpp_f(float v, float old = 0.f) {
@@ -97,6 +96,39 @@ __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, dpp_f<0x142, 0xA, false>(v, v));
   v = fmaxf(v, dpp_f<0x143, 0xC, false>(v, v));
   return lane63(v);
+}
+
+// Per lane position, the four 16-lane rows combined (lanes l, l ^ 16, l ^ 32,
+// l ^ 48: the xor-16 / xor-32 butterfly of __shfl_xor) on v_permlane16_swap /
+// v_permlane32_swap -- VALU ops, no ds_bpermute round trip through the LDS
+// crossbar. Each swap takes the value and a copy made by an asm move with an
+// early-clobber output (a distinct register the compiler cannot fold back
+// into the operand: a swap of one register with itself only rotates it).
+// swap16: row pairs (0,1), (2,3) exchange -> op gives the xor-16 combine in
+// every lane; swap32: halves exchange -> xor-32.
+template <class Op>
+__device__ __forceinline__ float rows_reduce(float v, Op op) {
+  // (elements copied out before the bit casts: __builtin_bit_cast of a vector
+  // element r[1] read element 0 -- the clang front end took the vector's
+  // address; that, not the swap, was the earlier "miscompile")
+  float t;
+  asm("v_mov_b32 %0, %1" : "=&v"(t) : "v"(v));
+  auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v),
+                                            __builtin_bit_cast(unsigned, t), false, false);
+  unsigned r0 = r[0], r1 = r[1];
+  v = op(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
+  asm("v_mov_b32 %0, %1" : "=&v"(t) : "v"(v));
+  r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v),
+                                       __builtin_bit_cast(unsigned, t), false, false);
+  r0 = r[0];
+  r1 = r[1];
+  return op(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
+}
+__device__ __forceinline__ float rows_max(float v) {
+  return rows_reduce(v, [](float a, float b) { return fmaxf(a, b); });
+}
+__device__ __forceinline__ float rows_sum(float v) {
+  return rows_reduce(v, [](float a, float b) { return a + b; });
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

@@ -23,6 +23,8 @@
 // gradients are bitwise deterministic.
 #include "tdg_common.h"
 #include "tdg_attn.h"
+
+#include <cstdlib>
 #include "tdg_gemm.h"
 
 
@@ -306,8 +308,7 @@ __device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l
   for (int t = 0; t < NT16; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[t][r]);
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  tmax = rows_max(tmax);
   const float mn = fmaxf(m, masked ? tmax : tmax * c);
   if (__ballot(mn > m)) {  // wave-uniform: rescale only when a row max grew
     const float alpha = fast_exp2(m - mn);  // m = -inf (nothing yet): 0, and O, l are 0
@@ -454,8 +455,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     float lu = l[u];
-    lu += __shfl_xor(lu, 16, 64);
-    lu += __shfl_xor(lu, 32, 64);
+    lu = rows_sum(lu);
     const bool ok = qrow[u] < a.Lq;
     const float inv = lu > 0.f ? 1.f / lu : 0.f;
     bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
@@ -604,8 +604,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     float lu = l[u];
-    lu += __shfl_xor(lu, 16, 64);
-    lu += __shfl_xor(lu, 32, 64);
+    lu = rows_sum(lu);
     const bool ok = qrow[u] < a.Lq;
     const float inv = lu > 0.f ? 1.f / lu : 0.f;
     bf16_t* op = a.out + b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
@@ -633,9 +632,12 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2))) v
 // that the S accumulator (t, g, r) is key 32 (t >> 1) + 8 g + 4 (t & 1) + r,
 // which makes the P registers the PV B operand as they stand. The backward
 // stays bf16 (it recomputes P from the bf16 Q, K and this LSE).
-template <int NS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_fp8_kernel(AttnArgs a) {
-  constexpr int NWV = 8, HD = 64, RB = 64, TB = 64 * RB, SLOT = 2 * TB, QBW = 16 * NWV;
+template <int NS, int U>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 : 2))) void attn_fwd_fp8_kernel(AttnArgs a) {
+  // U 16-query subtiles per wave (16 U queries): every K / V fragment feeds U
+  // MFMAs and each wave carries U independent softmax chains (U = 2: one
+  // round of 4 waves per SIMD at seq 512 instead of 1.33 rounds of 6)
+  constexpr int NWV = 8, HD = 64, RB = 64, TB = 64 * RB, SLOT = 2 * TB, QBW = 16 * U * NWV;
   constexpr int NT16 = 4, DT = 4;
   static_assert(NS >= 3, "ring: refilled, being read, landed");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -647,21 +649,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   int xb, h, b;
   attn_coords(a, xb, h, b);
   const int q0 = xb * QBW;
-  const int qrow = q0 + 16 * w + cl;
+  const int wq0 = q0 + 16 * U * w;
+  int qrow[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) qrow[u] = wq0 + 16 * u + cl;
   int klim;
   float scl;
   bool causal;
   key_window(a, b, klim, scl, causal);
   if (causal) klim = min(klim, q0 + QBW);
   const int nkt = (klim + 63) / 64;
+  // (causal: the wave's last key tile; later tiles are staged for the other
+  // waves but skipped here)
+  const int wkt = causal ? min(nkt, (wq0 + 16 * U + 63) / 64) : nkt;
 
   // Q fragments (B operand of S^T): lane (g, q) holds Q[q][32 ks + 8 g .. +7]
-  long qf[2];
-  {
-    const uint8_t* qp = q8 + b * a.q_sb + (long long)min(qrow, a.Lq - 1) * a.q_sl + h * a.q_sh;
+  long qf[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint8_t* qp = q8 + b * a.q_sb + (long long)min(qrow[u], a.Lq - 1) * a.q_sl + h * a.q_sh;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
-      qf[ks] = qrow < a.Lq ? *reinterpret_cast<const long*>(qp + 32 * ks + 8 * g) : 0;
+      qf[u][ks] = qrow[u] < a.Lq ? *reinterpret_cast<const long*>(qp + 32 * ks + 8 * g) : 0;
   }
   // staging: wave w < 4 fills K image rows 16w.., w >= 4 V image rows 16(w-4)..
   const bool isv = w >= 4;
@@ -696,15 +705,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   }
   const float inv_qk = 1.f / (a.sq8[0] * a.sk8[0]);
   const float c = scl * LOG2E * inv_qk;
-  const int wq0 = q0 + 16 * w;
-  f32x4 oacc[DT];
+  f32x4 oacc[U][DT];
+  float m[U], l[U];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int u = 0; u < U; ++u) {
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DT; ++i) oacc[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   for (int kt = 0; kt < nkt; ++kt) {
     wait_tiles<1, NS - 2>(min(NS - 2, nkt - 1 - kt));
     lds_barrier();
     if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+    if (kt >= wkt) continue;  // (wave-uniform)
     const uint32_t slot = (uint32_t)(uintptr_t)smem + (uint32_t)((kt % NS) * SLOT);
     const int k0 = 64 * kt;
     // S^T: K rows 16 t + cl, hd bytes 32 ks + 8 g (8-byte chunk 4 ks + g);
@@ -716,7 +730,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
       kfr[t][0] = lds_read_b64_at<16 * t * RB>(ka0);
       kfr[t][1] = lds_read_b64_at<16 * t * RB>(ka1);
     });
-    f32x4 s[NT16];
+    f32x4 s[U][NT16];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (half == 0) lgkm_wait<NT16>();
@@ -725,14 +739,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
       for (int t = half * 2; t < half * 2 + 2; ++t) {
         tie(kfr[t][0]);
         tie(kfr[t][1]);
-        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(kfr[t][ks], qf[ks], s[t], 0, 0, 0);
+        for (int u = 0; u < U; ++u) {
+          s[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(kfr[t][ks], qf[u][ks], s[u][t], 0, 0, 0);
+        }
       }
     }
     const bool msk = tile_masked(k0, 64, klim, causal, wq0);
-    softmax_max<NT16, DT, true>(s, m, l, oacc, msk, k0, klim, causal, qrow, g, c);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      softmax_max<NT16, DT, true>(s[u], m[u], l[u], oacc[u], msk, k0, klim, causal, qrow[u], g, c);
     // V^T fragments: lane pair (2 r8 + hh) of group g passes V row 32 s2 + 8 g + r8,
     // 8-byte chunk 2 dt + hh; lane i receives hd column 16 dt + i, keys 8 g .. +7
     long vfr[2][DT];
@@ -746,24 +765,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     // P448), then e4m3(P448) in PV operand order: P <= 1 against the running
     // max, so P448 <= 448 needs no clamp and the 448 costs no multiply
     const float cs = msk ? 1.f : c;
-    const float nm = (m == -INFINITY ? 0.f : -m) + LOG2_448;
-    float rs = 0.f;
+    long pf[U][2];
 #pragma unroll
-    for (int t = 0; t < NT16; ++t)
+    for (int u = 0; u < U; ++u) {
+      const float nm = (m[u] == -INFINITY ? 0.f : -m[u]) + LOG2_448;
+      float rs = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[t][r] = fast_exp2(fmaf(s[t][r], cs, nm));
-        rs += s[t][r];
+      for (int t = 0; t < NT16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[u][t][r] = fast_exp2(fmaf(s[u][t][r], cs, nm));
+          rs += s[u][t][r];
+        }
+      l[u] += rs;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2][0], s[u][2 * s2][1], 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2][2], s[u][2 * s2][3], lo, true);
+        int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2 + 1][0], s[u][2 * s2 + 1][1], 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2 + 1][2], s[u][2 * s2 + 1][3], hi, true);
+        pf[u][s2] = (long)(uint32_t)lo | ((long)hi << 32);
       }
-    l += rs;
-    long pf[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2][0], s[2 * s2][1], 0, false);
-      lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2][2], s[2 * s2][3], lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2 + 1][0], s[2 * s2 + 1][1], 0, false);
-      hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[2 * s2 + 1][2], s[2 * s2 + 1][3], hi, true);
-      pf[s2] = (long)(uint32_t)lo | ((long)hi << 32);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -772,53 +794,56 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         tie(vfr[s2][dt]);
-        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(vfr[s2][dt], pf[s2], oacc[dt], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(vfr[s2][dt], pf[u][s2], oacc[u][dt], 0, 0, 0);
       }
     }
   }
   wait_vmcnt<0>();
-  float lu = l;
-  lu += __shfl_xor(lu, 16, 64);
-  lu += __shfl_xor(lu, 32, 64);
-  const bool valid = qrow < a.Lq;
-  const float inv = lu > 0.f ? 1.f / (lu * a.sv8[0]) : 0.f;  // (lu: the row sum of P448)
-  const long long ooff = b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
-  bf16_t* op = a.out + ooff;
   // e4m3 copy of O for the e4m3 output projection: from the bf16-rounded
   // values (what quantising the bf16 O gives), wave amax -> one atomic
   const float so = a.out8 ? a.so8[0] : 0.f;
   float am = 0.f;
-  // (8-byte stores: the 16-byte form of store_row16 measured 4 % slower here,
-  // 739 vs 708 us per step over 18 calls, profiles/r4/ab_grouped_tiles_fp8_kstats.txt)
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    bf16_t e[4];
+  for (int u = 0; u < U; ++u) {
+    float lu = l[u];
+    lu = rows_sum(lu);
+    const bool valid = qrow[u] < a.Lq;
+    const float inv = lu > 0.f ? 1.f / (lu * a.sv8[0]) : 0.f;  // (lu: the row sum of P448)
+    const long long ooff = b * a.o_sb + (long long)qrow[u] * a.o_sl + h * a.o_sh;
+    bf16_t* op = a.out + ooff;
+    // (8-byte stores: the 16-byte form of store_row16 measured 4 % slower here,
+    // 739 vs 708 us per step over 18 calls, profiles/r4/ab_grouped_tiles_fp8_kstats.txt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) e[r] = f2bf(oacc[dt][r] * inv);
-    if (valid) {
-      const uint32_t lo = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
-      const uint32_t hi = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
-      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
-    }
-    if (a.out8) {
-      float v[4];
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16_t e[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = bf2f(e[r]);
-        am = fmaxf(am, valid ? fabsf(v[r]) : 0.f);
+      for (int r = 0; r < 4; ++r) e[r] = f2bf(oacc[u][dt][r] * inv);
+      if (valid) {
+        const uint32_t lo = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
+        const uint32_t hi = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+        *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = make_uint2(lo, hi);
       }
-      int w8 = pack2_e4m3<false>(v[0] * so, v[1] * so, 0);
-      w8 = pack2_e4m3<true>(v[2] * so, v[3] * so, w8);
-      if (valid) *reinterpret_cast<int*>(a.out8 + ooff + 16 * dt + 4 * g) = w8;
+      if (a.out8) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = bf2f(e[r]);
+          am = fmaxf(am, valid ? fabsf(v[r]) : 0.f);
+        }
+        int w8 = pack2_e4m3<false>(v[0] * so, v[1] * so, 0);
+        w8 = pack2_e4m3<true>(v[2] * so, v[3] * so, w8);
+        if (valid) *reinterpret_cast<int*>(a.out8 + ooff + 16 * dt + 4 * g) = w8;
+      }
     }
+    if (valid && g == 0)
+      a.lse[((long long)b * a.H + h) * a.Lq + qrow[u]] = lu > 0.f ? m[u] + (log2f(lu) - LOG2_448) : INFINITY;
   }
   if (a.out8) {
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 64));
+    am = wave_max(am);
     if (lane == 0) atomic_amax(amax_word(a.amax8, blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z), am);
   }
-  if (valid && g == 0)
-    a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + (log2f(lu) - LOG2_448) : INFINITY;
 }
 
 // ============================================================================ dK, dV
@@ -1019,8 +1044,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[e]);
     }
-    d += __shfl_xor(d, 16, 64);
-    d += __shfl_xor(d, 32, 64);
+    d = rows_sum(d);
     if (qvalid && g == 0) a.delta[bh] = d;
     D[u] = d;
   }
@@ -1467,8 +1491,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int s = 0; s < T::KS; ++s)
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += bf2f((bf16_t)of[u][s][e]) * bf2f((bf16_t)ov[u][s][e]);
-    d += __shfl_xor(d, 16, 64);
-    d += __shfl_xor(d, 32, 64);
+    d = rows_sum(d);
     if (qrow[u] < a.Lq && g == 0) a.delta[((long long)b * a.H + h) * a.Lq + qrow[u]] = d;
     D[u] = d;
   }
@@ -2518,18 +2541,38 @@ extern "C" int tdg_attn_fwd(const AttnArgs* a, int hd, hipStream_t st) {
 extern "C" int tdg_attn_bwd(const AttnArgs* a, int hd, hipStream_t st) {
   TDG_HD_CASES(bwd_hd, *a, st)
 }
-extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, hipStream_t st) {
-  if (hd != 64) return -1;
-  constexpr int NS = 3;
+namespace {
+template <int NS, int U>
+int fwd_fp8_u(const AttnArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)attn_fwd_fp8_kernel<NS>,
+    hipFuncSetAttribute((const void*)attn_fwd_fp8_kernel<NS, U>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(attn_fwd_fp8_kernel<NS>, dim3(cdiv(a->Lq, 128), a->H, a->B), dim3(512),
-                     NS * 2 * 64 * 64, st, *a);
+  hipLaunchKernelGGL((attn_fwd_fp8_kernel<NS, U>), dim3(cdiv(a.Lq, 128 * U), a.H, a.B), dim3(512),
+                     NS * 2 * 64 * 64, st, a);
   return 0;
+}
+int fwd_fp8_ns() {
+  static const int v = [] {
+    const char* e = getenv("TDG_ATTN_FWD8_NS");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+}  // namespace
+// u: queries per wave / 16 (1 or 2; 0 = by shape); ring depth NS from
+// TDG_ATTN_FWD8_NS (3, 4 or 6)
+extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, int u, hipStream_t st) {
+  if (hd != 64) return -1;
+  if (u <= 0) u = 1;
+  if (u == 2) return fwd_fp8_u<3, 2>(*a, st);
+  switch (fwd_fp8_ns()) {
+    case 4: return fwd_fp8_u<4, 1>(*a, st);
+    case 6: return fwd_fp8_u<6, 1>(*a, st);
+    default: return fwd_fp8_u<3, 1>(*a, st);
+  }
 }
 namespace {
 template <int NW>
