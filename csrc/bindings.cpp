@@ -23,7 +23,7 @@ void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld, in
 int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
-int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, int u, hipStream_t st);
+int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_bwd_f8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
@@ -349,15 +349,6 @@ static int attn_xcd() {
   }();
   return v;
 }
-// queries per wave / 16 of the e4m3 attention forward (TDG_ATTN_FWD8_U: 1 or
-// 2; unset: by shape)
-static int attn_fwd8_u() {
-  static const int v = [] {
-    const char* e = getenv("TDG_ATTN_FWD8_U");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 // q/k/v/o/do/dq/dk/dv are 4-D [B, L, H, hd] views (any strides, hd contiguous).
 void fill_qkv(tdg::AttnArgs& a, const Tensor& q, const Tensor& k, const Tensor& v) {
   for (auto* t : {&q, &k, &v}) {
@@ -423,8 +414,7 @@ void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Te
                   const Tensor& lse, const optional<Tensor>& kv_len, const Tensor& sq,
                   const Tensor& sk, const Tensor& sv, double scale, bool causal,
                   const optional<Tensor>& out8, const optional<Tensor>& so8,
-                  const optional<Tensor>& amax8, int64_t u) {
-  TORCH_CHECK(u >= 0 && u <= 2, "attn_fwd_fp8: u is 0 (default), 1 or 2");
+                  const optional<Tensor>& amax8) {
   for (auto* t : {&q8, &k8, &v8}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat8_e4m3fn, "attn_fwd_fp8: e4m3 q/k/v");
     TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1 && t->size(3) == 64,
@@ -480,7 +470,7 @@ void attn_fwd_fp8(const Tensor& q8, const Tensor& k8, const Tensor& v8, const Te
   a.scale = (float)scale;
   a.causal = causal;
   c10::DeviceGuard g(q8.device());
-  check_err(tdg_attn_fwd_fp8(&a, 64, u ? (int)u : attn_fwd8_u(), stream_of(q8)), "tdg attn_fwd_fp8");
+  check_err(tdg_attn_fwd_fp8(&a, 64, stream_of(q8)), "tdg attn_fwd_fp8");
 }
 
 static tdg::AttnArgs attn_bwd_args(const Tensor& q, const Tensor& k, const Tensor& v,

@@ -98,6 +98,21 @@ __device__ __forceinline__ float wave_max(float v) {
   return lane63(v);
 }
 
+// f32 max without the canonicalising v_max_f32 x, x that fmaxf puts in front
+// of every operand the compiler cannot prove quiet (MFMA results, permlane
+// outputs: two extra VALU per fmaxf in the softmax row max). Operands are
+// never signalling NaNs here.
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // Per lane position, the four 16-lane rows combined (lanes l, l ^ 16, l ^ 32,
 // l ^ 48: the xor-16 / xor-32 butterfly of __shfl_xor) on v_permlane16_swap /
 // v_permlane32_swap -- VALU ops, no ds_bpermute round trip through the LDS
@@ -125,7 +140,7 @@ __device__ __forceinline__ float rows_reduce(float v, Op op) {
   return op(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
 }
 __device__ __forceinline__ float rows_max(float v) {
-  return rows_reduce(v, [](float a, float b) { return fmaxf(a, b); });
+  return rows_reduce(v, [](float a, float b) { return vmax(a, b); });
 }
 __device__ __forceinline__ float rows_sum(float v) {
   return rows_reduce(v, [](float a, float b) { return a + b; });

@@ -303,13 +303,16 @@ __device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l
         s[t][r] = key < klim && (!causal || key <= qrow) ? s[t][r] * c : -INFINITY;
       }
   }
-  float tmax = s[0][0];
+  // (asm max3 chain: no canonicalising moves on the MFMA results)
+  float tmax = vmax3(s[0][0], s[0][1], s[0][2]);
+  tmax = vmax(tmax, s[0][3]);
 #pragma unroll
-  for (int t = 0; t < NT16; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[t][r]);
+  for (int t = 1; t < NT16; ++t) {
+    tmax = vmax3(tmax, s[t][0], s[t][1]);
+    tmax = vmax3(tmax, s[t][2], s[t][3]);
+  }
   tmax = rows_max(tmax);
-  const float mn = fmaxf(m, masked ? tmax : tmax * c);
+  const float mn = vmax(m, masked ? tmax : tmax * c);
   if (__ballot(mn > m)) {  // wave-uniform: rescale only when a row max grew
     const float alpha = fast_exp2(m - mn);  // m = -inf (nothing yet): 0, and O, l are 0
 #pragma unroll
@@ -681,27 +684,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 
   const uint8_t* src0 = (isv ? v8 + b * a.v_sb + h * a.v_sh : k8 + b * a.k_sb + h * a.k_sh) + 16 * chunk;
   const long long sl = isv ? a.v_sl : a.k_sl;
   char* dst0 = smem + (isv ? TB : 0) + (w & 3) * 1024;
-  auto issue = [&](int kt) {
-    const int key = min(64 * kt + kin, a.Lk - 1);
-    __builtin_amdgcn_global_load_lds((const void*)(src0 + key * sl),
-                                     (__attribute__((address_space(3))) void*)(dst0 + (kt % NS) * SLOT),
-                                     16, 0, 0);
+  // DMA source: a 32-bit byte offset stepped by 64 rows per tile (no 64-bit
+  // multiply per issue); only the tiles that reach past Lk clamp their row
+  const uint8_t* srcb = src0 + (long long)kin * sl;
+  const uint32_t step = (uint32_t)(64 * sl);
+  const int klast = a.Lk - 1 - kin;  // (64 kt > klast: this lane's row is clamped)
+  auto issue = [&](int kt, auto slc) {
+    constexpr int SL = decltype(slc)::value;
+    const uint8_t* sp = 64 * kt <= klast ? srcb + (uint32_t)kt * step : src0 + (long long)(a.Lk - 1) * sl;
+    __builtin_amdgcn_global_load_lds((const void*)sp,
+                                     (__attribute__((address_space(3))) void*)(dst0 + SL * SLOT), 16, 0, 0);
   };
   // prologue tiles issued unconditionally (clamped rows, never read) so the
   // DMA count behind the Q loads is a constant
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue(s);
+  static_for<NS - 1>([&](auto sc) { issue(decltype(sc)::value, sc); });
   wait_vmcnt_known<NS - 1>();
 
   // lane parts of the fragment addresses (the swizzle term (row >> 2) & 3 is
-  // the same for every 16-row K tile t and both 32-row V halves s2)
-  uint32_t koff[2], voff[DT];
+  // the same for every 16-row K tile t and both 32-row V halves s2); the ring
+  // slot and the tile rows are immediate offsets (the tile loop is unrolled
+  // by NS, so tile kt's slot kt % NS is a constant)
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  uint32_t ka[2], va[DT];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) koff[ks] = cl * RB + 8 * ((4 * ks + g) ^ (((cl >> 2) & 3) << 1));
+  for (int ks = 0; ks < 2; ++ks) ka[ks] = sbase + cl * RB + 8 * ((4 * ks + g) ^ (((cl >> 2) & 3) << 1));
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     const int row = 8 * g + (cl >> 1);
-    voff[dt] = row * RB + 8 * ((2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1));
+    va[dt] = sbase + TB + row * RB + 8 * ((2 * dt + (cl & 1)) ^ (((row >> 2) & 3) << 1));
   }
   const float inv_qk = 1.f / (a.sq8[0] * a.sk8[0]);
   const float c = scl * LOG2E * inv_qk;
@@ -714,21 +724,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 
 #pragma unroll
     for (int i = 0; i < DT; ++i) oacc[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int kt = 0; kt < nkt; ++kt) {
+  auto tile = [&](int kt, auto slc) {
+    constexpr int SL = decltype(slc)::value;
     wait_tiles<1, NS - 2>(min(NS - 2, nkt - 1 - kt));
     lds_barrier();
-    if (kt + NS - 1 < nkt) issue(kt + NS - 1);
-    if (kt >= wkt) continue;  // (wave-uniform)
-    const uint32_t slot = (uint32_t)(uintptr_t)smem + (uint32_t)((kt % NS) * SLOT);
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1, std::integral_constant<int, (SL + NS - 1) % NS>{});
+    if (kt >= wkt) return;  // (wave-uniform)
     const int k0 = 64 * kt;
     // S^T: K rows 16 t + cl, hd bytes 32 ks + 8 g (8-byte chunk 4 ks + g);
-    // lane part of the address koff[ks], the 16 t rows an immediate offset
+    // lane part of the address ka[ks], slot and 16 t rows immediate offsets
     long kfr[NT16][2];
-    const uint32_t ka0 = slot + koff[0], ka1 = slot + koff[1];
     static_for<NT16>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      kfr[t][0] = lds_read_b64_at<16 * t * RB>(ka0);
-      kfr[t][1] = lds_read_b64_at<16 * t * RB>(ka1);
+      kfr[t][0] = lds_read_b64_at<SL * SLOT + 16 * t * RB>(ka[0]);
+      kfr[t][1] = lds_read_b64_at<SL * SLOT + 16 * t * RB>(ka[1]);
     });
     f32x4 s[U][NT16];
 #pragma unroll
@@ -757,9 +766,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 
     long vfr[2][DT];
     static_for<DT>([&](auto dc) {
       constexpr int dt = decltype(dc)::value;
-      const uint32_t va = slot + TB + voff[dt];
-      vfr[0][dt] = lds_read_tr8_at<0>(va);
-      vfr[1][dt] = lds_read_tr8_at<32 * RB>(va);
+      vfr[0][dt] = lds_read_tr8_at<SL * SLOT>(va[dt]);
+      vfr[1][dt] = lds_read_tr8_at<SL * SLOT + 32 * RB>(va[dt]);
     });
     // P448 = 448 exp2(c S - m) = exp2(c S - m + log2 448) (f32 row sum l of
     // P448), then e4m3(P448) in PV operand order: P <= 1 against the running
@@ -769,20 +777,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float nm = (m[u] == -INFINITY ? 0.f : -m[u]) + LOG2_448;
-      float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < NT16; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[u][t][r] = fast_exp2(fmaf(s[u][t][r], cs, nm));
-          rs += s[u][t][r];
-        }
+        for (int r = 0; r < 4; ++r) s[u][t][r] = fast_exp2(fmaf(s[u][t][r], cs, nm));
+      float rs = s[u][0][0];
+#pragma unroll
+      for (int i = 1; i < 4 * NT16; ++i) rs += s[u][i / 4][i % 4];
       l[u] += rs;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2][0], s[u][2 * s2][1], 0, false);
+        // (the first convert of each word writes its low half: its old value
+        // is any register, the high half is written next -- no zeroing move)
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2][0], s[u][2 * s2][1],
+                                                 __builtin_bit_cast(int, s[u][2 * s2][0]), false);
         lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2][2], s[u][2 * s2][3], lo, true);
-        int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2 + 1][0], s[u][2 * s2 + 1][1], 0, false);
+        int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2 + 1][0], s[u][2 * s2 + 1][1],
+                                                 __builtin_bit_cast(int, s[u][2 * s2 + 1][0]), false);
         hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[u][2 * s2 + 1][2], s[u][2 * s2 + 1][3], hi, true);
         pf[u][s2] = (long)(uint32_t)lo | ((long)hi << 32);
       }
@@ -799,7 +810,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(U == 2 ? 4 
           oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(vfr[s2][dt], pf[u][s2], oacc[u][dt], 0, 0, 0);
       }
     }
-  }
+  };
+  int kt = 0;
+  for (; kt + NS <= nkt; kt += NS) static_for<NS>([&](auto sc) { tile(kt + decltype(sc)::value, sc); });
+  static_for<NS - 1>([&](auto sc) {
+    if (kt + decltype(sc)::value < nkt) tile(kt + decltype(sc)::value, sc);
+  });
   wait_vmcnt<0>();
   // e4m3 copy of O for the e4m3 output projection: from the bf16-rounded
   // values (what quantising the bf16 O gives), wave amax -> one atomic
@@ -2562,12 +2578,11 @@ int fwd_fp8_ns() {
   return v;
 }
 }  // namespace
-// u: queries per wave / 16 (1 or 2; 0 = by shape); ring depth NS from
-// TDG_ATTN_FWD8_NS (3, 4 or 6)
-extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, int u, hipStream_t st) {
+// ring depth NS from TDG_ATTN_FWD8_NS (3, 4 or 6: measured equal, 3 kept).
+// (32 queries per wave, U = 2, measured 3-5 % slower at seq 512 and is not
+// instantiated: profiles/r5/attn_fwd8_u_rows.txt)
+extern "C" int tdg_attn_fwd_fp8(const AttnArgs* a, int hd, hipStream_t st) {
   if (hd != 64) return -1;
-  if (u <= 0) u = 1;
-  if (u == 2) return fwd_fp8_u<3, 2>(*a, st);
   switch (fwd_fp8_ns()) {
     case 4: return fwd_fp8_u<4, 1>(*a, st);
     case 6: return fwd_fp8_u<6, 1>(*a, st);

@@ -362,16 +362,15 @@ def attn_fwd_fp8_ok(Lq: int, Lk: int, hd: int) -> bool:
 
 
 def attn_fwd_fp8(q8, k8, v8, sq, sk, sv, kv_len, scale: float, causal: bool, o8=None, so8=None,
-                 amax8=None, u: int = 0):
+                 amax8=None):
     """Attention forward on e4m3 copies q8 = e4m3(q * sq) etc. (per-tensor
     scales, one-element device tensors): O (bf16) and the log2-domain LSE, as
     attn_fwd. o8 ([B, Lq, H, hd] e4m3, with its scale so8 and amax slot
-    amax8): also O's e4m3 copy from the epilogue (= quantising the bf16 O).
-    u: 16-query subtiles per wave (1 or 2; 0 = TDG_ATTN_FWD8_U, else 1)."""
+    amax8): also O's e4m3 copy from the epilogue (= quantising the bf16 O)."""
     B, Lq, H, hd = q8.shape
     out = torch.empty(B, Lq, H, hd, dtype=torch.bfloat16, device=q8.device)
     lse = torch.empty(B, H, Lq, dtype=torch.float32, device=q8.device)
-    C().attn_fwd_fp8(q8, k8, v8, out, lse, kv_len, sq, sk, sv, scale, causal, o8, so8, amax8, u)
+    C().attn_fwd_fp8(q8, k8, v8, out, lse, kv_len, sq, sk, sv, scale, causal, o8, so8, amax8)
     return out, lse
 
 
