@@ -295,12 +295,17 @@ __device__ __forceinline__ void softmax_max(f32x4 (&s)[NT16], float& m, float& l
                                             bool masked, int k0, int klim, bool causal, int qrow,
                                             int g, float c) {
   if (masked) {
+    // key = lane base + a constant per (t, r): valid iff the constant <= the
+    // lane's limit (last valid key, the causal diagonal) minus the base --
+    // one compare against an inline constant per element
+    const int kb = k0 + (KPERM ? 8 * g : 4 * g);
+    const int lim = (causal ? min(klim - 1, qrow) : klim - 1) - kb;
 #pragma unroll
     for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = KPERM ? k0 + 32 * (t >> 1) + 8 * g + 4 * (t & 1) + r : k0 + 16 * t + 4 * g + r;
-        s[t][r] = key < klim && (!causal || key <= qrow) ? s[t][r] * c : -INFINITY;
+        const int off = KPERM ? 32 * (t >> 1) + 4 * (t & 1) + r : 16 * t + r;
+        s[t][r] = off <= lim ? s[t][r] * c : -INFINITY;
       }
   }
   // (asm max3 chain: no canonicalising moves on the MFMA results)
