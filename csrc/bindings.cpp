@@ -24,6 +24,7 @@ int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
 int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
+int tdg_fp8_set_persist(int on);
 int tdg_attn_bwd_f8(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_ln_fwd(const void* x, const void* s, const float* gamma, const float* beta, void* y,
                void* hsave, float* mean, float* rstd, int M, int D, float p, uint64_t seed,
@@ -1523,6 +1524,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_fwd_fp8", &attn_fwd_fp8);
+  m.def("fp8_set_persist", [](int64_t on) { return (int64_t)tdg_fp8_set_persist((int)on); },
+        "persistent 128x128 fp8 GEMM on (1) / off (0) / query (-1); returns the previous state");
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_g8", &attn_bwd_g8);
   m.def("attn_bwd_f8", &attn_bwd_f8);

@@ -28,6 +28,7 @@
 #include "tdg_reduce.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace tdg {
@@ -168,11 +169,16 @@ struct F8Extra {
 // PRE_OK: prefetch the ReLU mask / old C of every chunk before the image is
 // written (off for the 256x256 one-wave tiles: 32 chunks per lane would not
 // fit in registers; those load per chunk instead)
+// (wimg_at / red_at: this wave's image and the amax scratch at given LDS
+// addresses instead of smem + wid * image bytes / after the images -- the
+// persistent kernel places them around the stage holding the next tile's
+// first K step)
 template <int BM, int BN, int WM, int WN, int EPI, int CF = 0, bool PRE_OK = true>
 struct F8Epi {
   static constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int SROW = WTN * 2 + 16;
+  static constexpr int WIMG = WTM * SROW;  // bytes of one wave's image
   static constexpr int CPR = WTN / 8;
   static constexpr int LDS = NW * WTM * SROW + 64;  // images + amax scratch
   // the ReLU mask / old C of every chunk a lane stores, loaded into registers
@@ -185,18 +191,33 @@ struct F8Epi {
   static constexpr bool PRE = DR && PRE_OK;
   // (the old C of a beta != 0 ReLU-backward GEMM is loaded in the epilogue:
   // kept out of the prefetch so the kernel stays at two waves per SIMD)
+  // bias of the lane's TN columns (the 16x16 path, run()): loaded with the
+  // other prefetches ahead of the first DMA -- read in the epilogue, its
+  // vmcnt wait also waited for every younger DMA (the persistent kernel's
+  // next-tile stage issued before the epilogue)
+  static constexpr bool HASB = (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) && PRE_OK;
   struct Pre {
     int4 aux[PRE && !A8 ? ITER : 1];  // bf16 mask chunk
     uint2 aux8[PRE && A8 ? ITER : 1];  // 8 mask bytes
+    float bn[HASB ? TN : 1];
   };
   static __device__ __forceinline__ bool vec_ok(int ldc, const F8Extra& ex) {
     return (ldc & 7) == 0 && (!DR || (ex.ldaux & 7) == 0);
   }
   // (the bf16 mask is prefetched at the start of the epilogue instead: 32
   // more registers across the main loop would cost the second wave per SIMD)
+  template <bool LOADB = true>
   static __device__ __forceinline__ void prefetch(Pre& pre, const bf16_t* __restrict__ C, int M, int N,
                                                   int ldc, int m0, int n0, int wid, int lane,
-                                                  const F8Extra& ex) {
+                                                  const F8Extra& ex, const float* __restrict__ bias) {
+    if constexpr (HASB && LOADB) {
+      const int wn = wid % WN, cl = lane & 15;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WTN + 16 * j + cl;
+        pre.bn[j] = bias[n < N ? n : N - 1];
+      }
+    }
     if constexpr (PRE && A8) {
       const int wm = wid / WN, wn = wid % WN;
       const bool vok = vec_ok(ldc, ex);
@@ -225,7 +246,8 @@ struct F8Epi {
                                              const float* __restrict__ sc8,
                                              unsigned* __restrict__ amax_out, int M, int N, int ldc,
                                              int ldc8, int m0, int n0, int wid, int lane, int tid,
-                                             const F8Extra& ex, const Pre& pre) {
+                                             const F8Extra& ex, const Pre& pre, float* red_at = nullptr,
+                                             char* wimg_at = nullptr) {
     const int g = lane >> 4, cl = lane & 15, wn = wid % WN;
     run_w(
         [&](char* wimg, float alpha) {
@@ -233,7 +255,8 @@ struct F8Epi {
           for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn * WTN + 16 * j + cl;
             float bn = 0.f;
-            if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
+            if constexpr (HASB) bn = pre.bn[j];
+            else if constexpr (EPI == F8_EPI_BIAS || EPI == F8_EPI_BIAS_RELU) bn = bias[n < N ? n : N - 1];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -244,7 +267,8 @@ struct F8Epi {
               }
           }
         },
-        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre);
+        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre, red_at,
+        wimg_at);
   }
   // the 32x32 MFMA accumulators (acc[i][j]: rows 32 i .., columns 32 j .. of the wave's tile)
   static __device__ __forceinline__ void run32(char* smem, const f32x16 (&acc)[WTM / 32][WTN / 32],
@@ -254,7 +278,7 @@ struct F8Epi {
                                                const float* __restrict__ sc8,
                                                unsigned* __restrict__ amax_out, int M, int N, int ldc,
                                                int ldc8, int m0, int n0, int wid, int lane, int tid,
-                                               const F8Extra& ex, const Pre& pre) {
+                                               const F8Extra& ex, const Pre& pre, float* red_at = nullptr) {
     const int h = lane >> 5, cl = lane & 31, wn = wid % WN;
     run_w(
         [&](char* wimg, float alpha) {
@@ -274,7 +298,8 @@ struct F8Epi {
               }
           }
         },
-        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre);
+        smem, C, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex, pre, red_at,
+        nullptr);
   }
   // write_img(wimg, alpha): the wave's dequantised (bias, ReLU) bf16 tile into its image
   template <class W>
@@ -284,11 +309,12 @@ struct F8Epi {
                                                const float* __restrict__ sc8,
                                                unsigned* __restrict__ amax_out, int M, int N, int ldc,
                                                int ldc8, int m0, int n0, int wid, int lane, int tid,
-                                               const F8Extra& ex, const Pre& pre) {
+                                               const F8Extra& ex, const Pre& pre, float* red_at,
+                                               char* wimg_at) {
     const int wm = wid / WN, wn = wid % WN;
     const float alpha = 1.f / (sa[0] * sb[0]);
     const float s8 = C8 ? sc8[0] : 0.f;
-    char* wimg = smem + wid * (WTM * SROW);
+    char* wimg = wimg_at ? wimg_at : smem + wid * WIMG;
     static_assert(64 % CPR == 0, "a lane keeps its column chunk across iterations");
     short8_t pre_aux[PRE && !A8 ? ITER : 1];
     const bool vec_ok = F8Epi::vec_ok(ldc, ex);
@@ -427,7 +453,7 @@ struct F8Epi {
     }
     if (C8 && amax_out) {  // one atomic per workgroup, spread over AMAX_SPREAD words
       amax = wave_max(amax);
-      float* red = reinterpret_cast<float*>(smem + NW * WTM * SROW);
+      float* red = red_at ? red_at : reinterpret_cast<float*>(smem + NW * WTM * SROW);
       if (lane == 0) red[wid] = amax;
       __syncthreads();
       if (tid == 0) {
@@ -534,7 +560,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
 
   using Epi = F8Epi<BM, BN, WM, WN, EPI, CF>;
   typename Epi::Pre pre;
-  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex);  // (older than every DMA)
+  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex, bias);  // (older than every DMA)
   GA ga;
   GB gb;
   ga.init(wid, lane);
@@ -617,6 +643,163 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_fp8_kernel(
   f8::lds_barrier();
   Epi::run(smem, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
            pre);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent form of the 128x128 / 2x2-wave / 2-stage tile above: two
+// workgroups per CU walk the tiles (dispatch positions blockIdx.x, + gridDim.x,
+// ...; each position's tile -- and so its XCD -- as in the one-shot grid). At
+// K = 1024 a tile round of the one-shot kernel is ~40 % fixed cost: the first
+// stage's fill latency and the epilogue, with the MFMAs idle
+// (scripts/fp8_ksweep.py: 5.5-7 us per round against 1.08 us per 128-deep K
+// step). Here the next tile's K step 0 is issued into the stage the
+// last-but-one K step vacated, the epilogue writes its swizzled, unpadded
+// images into the stage the last K step
+// vacated (waves 0-2; wave 3's image in a 9 KiB region past the stages: the
+// padded images are 36 KiB), and the next tile's K step 1 goes there once
+// the images are stored: the next tile's fill runs under this tile's epilogue.
+template <int EPI, int AF = 0, int CF = 0, bool BT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gemm_fp8_pk_kernel(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, bf16_t* __restrict__ C,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sb,
+    uint8_t* __restrict__ C8, const float* __restrict__ sc8, unsigned* __restrict__ amax_out,
+    int M, int N, int K, int lda, int ldb, int ldc, int ldc8, F8Extra ex) {
+  constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NW = 4, TM = 4, TN = 4;
+  constexpr int A_BYTES = BM * BK8, B_BYTES = BN * BK8, SB = A_BYTES + B_BYTES;
+  using GA = f8::Stage<BM, NW>;
+  using GB = typename std::conditional<BT, StageT<NW>, f8::Stage<BN, NW>>::type;
+  constexpr int PT = GA::P + GB::P;
+  using Epi = F8Epi<BM, BN, WM, WN, EPI, CF>;
+  static_assert(3 * Epi::WIMG <= SB, "three wave images fit in a stage");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem + 2 * SB + Epi::WIMG);  // amax scratch
+
+  const int tid = threadIdx.x;
+  int lane = tid & 63;  // (re-defined opaquely per tile: see the loop head)
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN), tiles = tiles_m * tiles_n;
+  const int nk = K / BK8;  // host: K % 128 == 0, nk >= 2
+  auto coords = [&](int pos, int& m0_, int& n0_) {
+    const int t = xcd_remap(pos, tiles);
+    int tm, tn;
+    if (tiles_n <= tiles_m) {
+      tn = t % tiles_n;
+      tm = t / tiles_n;
+    } else {
+      tm = t % tiles_m;
+      tn = t / tiles_m;
+    }
+    m0_ = tm * BM;
+    n0_ = tn * BN;
+  };
+  int pos = blockIdx.x;
+  int m0, n0;
+  coords(pos, m0, n0);
+  GA ga;
+  ga.init(wid, lane);
+  GB gb, gbn;  // (BT: the B offsets carry n0 -- the next tile's set in gbn)
+  if constexpr (BT) gb.init(wid, lane, n0, N, ldb);
+  else gb.init(wid, lane);
+  auto issue = [&](const GB& g_, int m0_, int n0_, int k, char* dst) {
+    ga.issue(A, lda, M, m0_, k * BK8, dst, wid);
+    if constexpr (BT) g_.issue(B, ldb, k * BK8, dst + A_BYTES, wid);
+    else g_.issue(B, ldb, N, n0_, k * BK8, dst + A_BYTES, wid);
+  };
+  auto frag_b = [&](const char* img, int base) {
+    if constexpr (BT) return wf8::frag(img, base, lane);
+    else return f8::frag(img, base, lane);
+  };
+  const int abase = wm * (BM / WM), bbase = wn * (BN / WN);
+
+  typename Epi::Pre pre;
+  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex, bias);  // (older than every DMA)
+  issue(gb, m0, n0, 0, smem);
+  issue(gb, m0, n0, 1, smem + SB);
+  int sl0 = 0;  // stage of the current tile's K step 0
+  for (;;) {
+    // lane-derived addresses (epilogue image / store offsets, fragment
+    // reads) are recomputed per tile: hoisted out of the tile loop they held
+    // ~150 more registers across it and cost the second workgroup per CU
+    asm volatile("" : "+v"(lane));
+    const int posn = pos + (int)gridDim.x;
+    const bool more = posn < tiles;  // (workgroup-uniform)
+    int m0n = 0, n0n = 0;
+    if (more) {
+      coords(posn, m0n, n0n);
+      if constexpr (BT) gbn.init(wid, lane, n0n, N, ldb);
+      else gbn = gb;
+    }
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K step 0 landed (younger: K step 1 -- and nothing else outstanding
+    // is younger than step 0 but the epilogue stores / prefetch, waited too)
+    f8::wait_vmcnt<PT>();
+    f8::lds_barrier();
+    i32x8 fa[TM], fb[TN];
+    {
+      const char* st0 = smem + sl0 * SB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = f8::frag(st0, abase + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag_b(st0 + A_BYTES, bbase + 16 * j);
+    }
+    // MODE 2: step kt + 2 exists (issue it into the vacated stage); 1: the
+    // last-but-one step (issue the next tile's step 0 there); 0: the last
+    auto kstep = [&](int kt, auto modec) {
+      constexpr int MODE = decltype(modec)::value;
+      tdg::lgkm_wait<0>();
+#pragma unroll
+      for (int i = 0; i < TM; ++i) tdg::tie(fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) tdg::tie(fb[j]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], AF,
+                                                                       0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (MODE >= 1) {
+        f8::wait_vmcnt<0>();
+        f8::lds_barrier();
+        char* cur = smem + ((kt + sl0) & 1) * SB;
+        if constexpr (MODE == 2) issue(gb, m0, n0, kt + 2, cur);
+        else if (more) issue(gbn, m0n, n0n, 0, cur);
+        const char* nx = smem + ((kt + 1 + sl0) & 1) * SB;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = f8::frag(nx, abase + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag_b(nx + A_BYTES, bbase + 16 * j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) kstep(kt, std::integral_constant<int, 2>{});
+    kstep(kt++, std::integral_constant<int, 1>{});
+    kstep(kt, std::integral_constant<int, 0>{});
+
+    // epilogue images in the stage of the last K step (every wave's reads of
+    // it completed before its last MFMAs; the barrier makes that all waves)
+    char* img = smem + ((nk - 1 + sl0) & 1) * SB;
+    f8::lds_barrier();
+    Epi::run(img, acc, C, bias, sa, sb, C8, sc8, amax_out, M, N, ldc, ldc8, m0, n0, wid, lane, tid, ex,
+             pre, red, wid < 3 ? img + wid * Epi::WIMG : smem + 2 * SB);
+    if (!more) break;
+    f8::lds_barrier();  // every wave's image reads done
+    Epi::prefetch(pre, C, M, N, ldc, m0n, n0n, wid, lane, ex, bias);
+    issue(gbn, m0n, n0n, 1, img);
+    sl0 = (nk + sl0) & 1;
+    pos = posn;
+    m0 = m0n;
+    n0 = n0n;
+    gb = gbn;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -735,7 +918,8 @@ __global__ __launch_bounds__(256) void gemm_fp8_ring_kernel(
 
   using Epi = F8Epi<128, 128, 2, 2, EPI, CF>;
   typename Epi::Pre pre;
-  Epi::prefetch(pre, C, M, N, ldc, m0, n0, wid, lane, ex);  // (older than every DMA)
+  // (run32 reads the bias itself)
+  Epi::template prefetch<false>(pre, C, M, N, ldc, m0, n0, wid, lane, ex, bias);  // (older than every DMA)
   f8r::StageK ga;
   ga.init(wid, lane, m0, M, lda);
   f8r::StageK gbk;
@@ -1524,6 +1708,41 @@ __global__ void fp8_dequant_kernel(const uint8_t* __restrict__ x8, float* __rest
 using namespace tdg;
 
 namespace {
+// compute units of the current device (cached per process)
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+// persistent 128x128 fp8 GEMM (gemm_fp8_pk_kernel) per epilogue id: a bit
+// mask over F8_EPI_* (TDG_FP8_PERSIST: 0 = off, "all", or a comma list of
+// epilogue ids; default: the ReLU forward and the 8-bit-mask ReLU backward,
+// the two measured faster in the step); tdg_fp8_set_persist overrides (tests
+// compare both forms in one process)
+int g_fp8_persist = -1;
+int fp8_persist_mask() {
+  if (g_fp8_persist < 0) {
+    const char* e = getenv("TDG_FP8_PERSIST");
+    int m = (1 << F8_EPI_BIAS_RELU) | (1 << F8_EPI_DRELU8);
+    if (e && *e) {
+      if (e[0] == 'a') {
+        m = 0xff;
+      } else {  // "0": off; "2,4": those epilogue ids
+        m = 0;
+        for (const char* c = e; *c; ++c)
+          if (*c >= '1' && *c <= '7' && (c == e || c[-1] == ',')) m |= 1 << (*c - '0');
+      }
+    }
+    g_fp8_persist = m;
+  }
+  return g_fp8_persist;
+}
+bool fp8_persist(int epi) { return (fp8_persist_mask() >> epi) & 1; }
 template <int BM, int BN, int WM, int WN, int ST, int EPI, int AF = 0, int CF = 0, bool BT = false>
 int launch_f8(const void* A, const void* B, void* C, const float* bias, const float* sa,
               const float* sb, void* C8, const float* sc8, unsigned* amax, int M, int N, int K,
@@ -1537,6 +1756,24 @@ int launch_f8(const void* A, const void* B, void* C, const float* bias, const fl
     attr = true;
   }
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  // persistent walk when there is more than one round of tiles (K >= 256;
+  // not the bf16-mask ReLU backward, whose epilogue would spill in the loop)
+  if constexpr (BM == 128 && BN == 128 && WM == 2 && WN == 2 && ST == 2 && EPI != F8_EPI_DRELU) {
+    const int grid = 2 * cu_count();
+    if (fp8_persist(EPI) && K >= 2 * BK8 && tiles > grid) {
+      constexpr int plds = 2 * (BM + BN) * BK8 + (BM / 2) * (BN + 16) + 64;  // stages, wave-3 image, scratch
+      static bool pattr = false;
+      if (!pattr) {
+        hipFuncSetAttribute((const void*)gemm_fp8_pk_kernel<EPI, AF, CF, BT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        pattr = true;
+      }
+      hipLaunchKernelGGL((gemm_fp8_pk_kernel<EPI, AF, CF, BT>), dim3(grid), dim3(256), plds, st,
+                         (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C, bias, sa, sb,
+                         (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((gemm_fp8_kernel<BM, BN, WM, WN, ST, EPI, AF, CF, BT>), dim3(tiles),
                      dim3(WM * WN * 64), lds, st, (const uint8_t*)A, (const uint8_t*)B, (bf16_t*)C,
                      bias, sa, sb, (uint8_t*)C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex);
@@ -1708,6 +1945,13 @@ static int tdg_gemm_fp8_body(const void* A, const void* B, void* C, const float*
       return launch_f8<128, 128, 2, 2, 2, F8_EPI_NONE, 1, 1>(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, ex, st);
   }
   return -1;
+}
+
+// on: an F8_EPI_* bit mask (0 off, 0xff all); < 0 queries. Returns the old mask.
+extern "C" int tdg_fp8_set_persist(int on) {
+  const int old = fp8_persist_mask();
+  if (on >= 0) g_fp8_persist = on;
+  return old;
 }
 
 extern "C" int tdg_fp8_quant(const void* x, void* y8, long long n, const float* scale,

@@ -726,3 +726,57 @@ def test_adam_chunk_kernel_matches_grid_adam_and_quant_multi():
         want = F.quantize(sh[off:off + n], meta, slot, record=False)
         assert torch.equal(y8.view(torch.uint8), want.view(torch.uint8))
         assert meta.amax_values()[slot].item() == sh[off:off + n].float().abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(8192, 4096, 1024), (3000, 1536, 384), (4096, 1024, 2048),
+                                     (1100, 1280, 256)])
+def test_fp8_gemm_persistent_matches_oneshot(M, N, Kd):
+    """The persistent 128x128 fp8 GEMM (fp8.hip gemm_fp8_pk_kernel: tiles
+    walked by 2 workgroups per CU, the next tile's first K step in flight
+    under the epilogue) writes bitwise what the one-shot grid writes: forward
+    bias (+ReLU, e4m3 copy, amax) and the e5m2 dgrads (plain-weight transposing
+    read; ReLU backward from the 8-bit mask with the fused column sums)."""
+    from tensorflow_distributed_on_gke_amd.ops._ext import C as _C
+    C = _C()
+    torch.manual_seed(11)
+    meta, gm = F.Fp8Meta(DEV), F.Fp8Meta(DEV, fmt=1)
+    ia, ib, io = meta.slot("a"), meta.slot("b"), meta.slot("o")
+    ig, igo = gm.slot("g"), gm.slot("go")
+    meta.scale[io] = 8.0
+    gm.scale[igo] = 256.0
+    a8 = (torch.randn(M, Kd, device=DEV) * 4).to(F.FP8)
+    b8 = (torch.randn(N, Kd, device=DEV) * 4).to(F.FP8)
+    g8 = (torch.randn(M, Kd, device=DEV) * 4).to(F.BF8)
+    w8 = (torch.randn(Kd, N, device=DEV) * 4).to(F.FP8)  # plain weight [out=K][in=N]
+    bias = torch.randn(N, device=DEV)
+    mask8 = torch.relu(torch.randn(M, N, device=DEV)).to(F.FP8)
+
+    def run():
+        outs = []
+        y, y8 = F.gemm_fp8(a8, b8, bias, meta, ia, ib, relu=True, out8_slot=io, cfg=0)
+        outs += [y, y8.view(torch.uint8)]
+        y2, _ = F.gemm_fp8(a8, b8, bias, meta, ia, ib, cfg=0)
+        outs.append(y2)
+        d = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        d8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, meta, ib, d, out8_slot=igo, cfg=0, w_plain=True)
+        outs += [d, d8.view(torch.uint8)]
+        cs = torch.zeros(N, device=DEV)
+        r8 = F.gemm_bf8_dgrad(g8, gm, ig, w8, meta, ib, None,
+                              out8_slot=igo, cfg=0, relu_aux8=mask8, colsum_out=cs, w_plain=True)
+        outs += [r8.view(torch.uint8), cs]
+        torch.cuda.synchronize()
+        am = torch.cat([meta.amax_values()[io:io + 1], gm.amax_values()[igo:igo + 1]])
+        return outs, am
+
+    old = C.fp8_set_persist(0)
+    try:
+        ref, am_ref = run()
+        meta.amax.zero_()
+        gm.amax.zero_()
+        C.fp8_set_persist(0xff)
+        got, am_got = run()
+    finally:
+        C.fp8_set_persist(old)
+    for i, (r, g) in enumerate(zip(ref, got)):
+        assert torch.equal(r, g), (i, (r.float() - g.float()).abs().max().item())
+    assert torch.equal(am_ref, am_got)
