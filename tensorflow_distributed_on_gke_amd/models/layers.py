@@ -1180,7 +1180,9 @@ class FFNBlockFn(torch.autograd.Function):
                 fp8.gemm_bf8_dgrad(dpre8, st.gmeta, gh, w1t8, st.meta, s1t, dh.view(M, d), beta=1.0,
                                    w_plain=wp)
                 return (dh.view(B, L, d),) + (None,) * 8
-            if w2.compute_t is not None:  # NT layout against W2^T (ParamStore.add_transposed)
+            if w2.compute_t is not None and not w2.compute_t_stale:
+                # NT layout against W2^T (ParamStore.add_transposed; stale while
+                # an fp8 backward had the re-transposes paused: NN below)
                 dpre = K.linear_dgrad_t(ds2, w2.compute_t, relu_aux=h)
             else:
                 dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)

@@ -55,6 +55,7 @@ class Param:
     grad: Optional[torch.Tensor] = None
     compute: Optional[torch.Tensor] = None  # bf16 shadow (GPU) / master (CPU)
     compute_t: Optional[torch.Tensor] = None  # transposed bf16 copy (ParamStore.add_transposed)
+    compute_t_stale: bool = False  # compute_t lags the compute copy (re-transposes paused)
 
     def __repr__(self) -> str:  # pragma: no cover
         return f"Param({self.name}, {self.shape}, off={self.offset})"
@@ -109,6 +110,11 @@ class ParamStore:
         self._release_hooks: List[Callable[[], None]] = []
         self._sync_hooks: List[Callable[[], None]] = []
         self.transposed: List[Param] = []  # weights with a transposed compute copy
+        # paused: nothing reads the transposed copies (the fp8 FFN backward
+        # runs on the e4m3 weights), so the optimizer skips re-transposing
+        # them and marks them stale (Param.compute_t_stale) -- a bf16 FFN
+        # backward then takes the untransposed (NN) dgrad
+        self.transposed_paused = False
         # autograd anchor: gives layers whose only inputs are token ids a
         # tensor that requires grad, so backward reaches them.
         self.anchor = torch.zeros((), requires_grad=True)
@@ -178,6 +184,10 @@ class ParamStore:
         """Re-transpose the registered weights lying in flat[start:end]."""
         if not self.transposed:
             return
+        if self.transposed_paused:
+            for p in self.transposed:
+                p.compute_t_stale = True
+            return
         end = self.total if end is None else end
         todo = [p for p in self.transposed if p.offset >= start and p.offset + p.numel <= end]
         groups: Dict[tuple, List[Param]] = {}
@@ -187,6 +197,8 @@ class ParamStore:
 
         for ps in groups.values():
             K.transpose_grouped([p.compute for p in ps], [p.compute_t for p in ps])
+        for p in todo:
+            p.compute_t_stale = False
 
     # ------------------------------------------------------------------ grads
     def on_grad_ready(self, fn: Callable[[Param], None]) -> None:

@@ -499,6 +499,11 @@ class Fp8State:
             feeder = layer.ln1 if hasattr(layer, "qkv") else layer.ln2  # encoder / decoder
             self.ln_slots[id(feeder.gamma)] = xs
             if backward:
+                # every FFN backward now runs on the e4m3 weights: the bf16
+                # W2^T copies (ParamStore.add_transposed) are not read, and the
+                # optimizer stops re-transposing them (0.07 ms per big step)
+                if getattr(model, "store", None) is not None:
+                    model.store.transposed_paused = True
                 if not DGRAD_PLAIN_W:
                     self.weights.add(layer.ff1.w, transposed=True)
                     self.weights.add(layer.ff2.w, transposed=True)
