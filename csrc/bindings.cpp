@@ -1110,7 +1110,9 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const optional<Tensor>& C, const
               "gemm_fp8: N-contiguous B runs the e5m2 backward 128x128 configs (cfg 0, 10) only");
   if (bias.has_value()) check_f32(*bias, "bias");
   const int64_t epi_id = epi & 15;  // (flag 16: C = dequant(C8))
-  TORCH_CHECK((epi & ~int64_t(63)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
+  // (flag 64: the column-sum partials stay in ws, folded by the caller)
+  TORCH_CHECK((epi & ~int64_t(127)) == 0 && epi_id <= 3, "gemm_fp8: epilogue id");
+  TORCH_CHECK(!(epi & 64) || colsum_out.has_value(), "gemm_fp8: deferred column sums need colsum_out");
   TORCH_CHECK(!(epi & 16) || C8.has_value(), "gemm_fp8: C = dequant(C8) needs C8");
   TORCH_CHECK(epi_id == 0 || epi_id == 3 || bias.has_value(), "gemm_fp8: epilogue needs bias");
   TORCH_CHECK(epi_id != 3 || aux.has_value() != aux8.has_value(),

@@ -145,6 +145,9 @@ constexpr int F8_EPI_CDEQ = 16;
 // host-side flag of tdg_gemm_fp8's epi: B is N-contiguous ([K][ldb], e.g. a
 // weight [out][in] as the B operand of its dgrad; 128x128 tile only)
 constexpr int F8_B_NCONTIG = 32;
+// host-side flag: leave the column-sum partials (colsum_out) in ws unfolded
+// -- the caller folds them later with other deferred reductions
+constexpr int F8_CS_DEFER = 64;
 
 // Backward-GEMM extras: the ReLU mask operand (F8_EPI_DRELU: out = 0 where
 // aux <= 0) and C = alpha A B^T + beta C.
@@ -1869,7 +1872,8 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
   if (K % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -2;
   const int cdeq = (epi & F8_EPI_CDEQ) != 0;
   const bool bt = (epi & F8_B_NCONTIG) != 0;
-  epi &= ~(F8_EPI_CDEQ | F8_B_NCONTIG);
+  const bool csdefer = (epi & F8_CS_DEFER) != 0;
+  epi &= ~(F8_EPI_CDEQ | F8_B_NCONTIG | F8_CS_DEFER);
   if (bt && ((cfg != 0 && cfg != 10) || N % 16 != 0 || ldb < N || afmt != 1 || cfmt != 1)) return -6;
   if (cdeq && !C8) return -2;
   if (!C && (beta != 0.f || cdeq)) return -2;
@@ -1880,7 +1884,7 @@ extern "C" int tdg_gemm_fp8(const void* A, const void* B, void* C, const float* 
     const int rc = tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc,
                                      ldc8, epi, cfg, afmt, cfmt, ex, st, bt);
     if (rc) return rc;
-    launch_reduce_partials(ws, colsum_out, N, cdiv(M, 128) * 2, colsum_beta, st);
+    if (!csdefer) launch_reduce_partials(ws, colsum_out, N, cdiv(M, 128) * 2, colsum_beta, st);
     return 0;
   }
   return tdg_gemm_fp8_body(A, B, C, bias, sa, sb, C8, sc8, amax, M, N, K, lda, ldb, ldc, ldc8, epi,

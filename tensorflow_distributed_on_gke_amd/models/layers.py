@@ -1165,11 +1165,14 @@ class FFNBlockFn(torch.autograd.Function):
                     # inputs (FFN1 input x8, hidden h8), token-major
                     x8, h8 = ctx.f8
                     xs, hs = st.ffn_slots[id(w1)]
+                    q = rt.wgrad
+                    # (b1's column-sum fold deferred to the wgrad flush with
+                    # the LayerNorm folds: one launch instead of one per layer)
                     dpre8 = fp8.gemm_bf8_dgrad(ds8, st.gmeta, gs, w2t8, st.meta, s2t, None,
                                                relu_aux8=h8.view(M, ff), out8_slot=gh,
-                                               colsum_out=b1.grad, colsum_beta=bt, w_plain=wp)
-                    _ready(rt, b1)
-                    q = rt.wgrad
+                                               colsum_out=b1.grad, colsum_beta=bt, w_plain=wp,
+                                               defer=q.reductions)
+                    q.reduced_params.append((rt, b1))
                     q.add_fp8(ds8.view(M, d), st.gmeta.s(gs), h8.view(M, ff), st.meta.s(hs), w2, bt, rt)
                     q.add_fp8(dpre8.view(M, ff), st.gmeta.s(gh), x8.view(M, d), st.meta.s(xs), w1, bt, rt)
                 else:

@@ -233,7 +233,8 @@ def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
                    out: Optional[torch.Tensor], relu_aux: Optional[torch.Tensor] = None,
                    beta: float = 0.0, out8_slot: Optional[int] = None, cfg: Optional[int] = None,
                    relu_aux8: Optional[torch.Tensor] = None, colsum_out: Optional[torch.Tensor] = None,
-                   colsum_beta: float = 0.0, w_plain: bool = False) -> Optional[torch.Tensor]:
+                   colsum_beta: float = 0.0, w_plain: bool = False,
+                   defer: Optional[list] = None) -> Optional[torch.Tensor]:
     """Backward GEMM on the block-scaled MFMA: out[M,N] (=|+= beta) dequant(
     g8[M,K] (e5m2 gradient) @ W), bf16, where W[K,N] is the e4m3 weight:
     w_plain: w8 IS that weight ([out=K][in=N], the forward's copy; the kernel
@@ -244,7 +245,9 @@ def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
     recorded); colsum_out[N] (=|+= colsum_beta): the column sums of the
     (bf16-rounded) output -- a bias gradient -- from the epilogue (128x128
     tiles). out may be None (nothing but the e5m2 copy and the sums is
-    written)."""
+    written). defer (a list): the column sums' partials stay in a workspace
+    of colsum_out's own and their fold is appended to defer
+    (kernels.reduce_partials_multi, with the other deferred reductions)."""
     M, Kd = g8.shape
     N = w8.shape[1] if w_plain else w8.shape[0]
     o8 = torch.empty(M, N, dtype=BF8, device=g8.device) if out8_slot is not None else None
@@ -253,9 +256,15 @@ def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
     ws = None
     if (colsum_out is not None or w_plain) and c not in (0, 10):
         c = BWD_CFG_128
+    nparts = math.ceil(M / 128) * 2
     if colsum_out is not None:
-        ws = K.workspace("fp8_colsum", math.ceil(M / 128) * 2 * N, g8.device)
+        # (deferred: the partials must survive until the fold -- a workspace
+        # per output)
+        key = "fp8_colsum" if defer is None else f"fp8_colsum_{colsum_out.data_ptr()}"
+        ws = K.workspace(key, nparts * N, g8.device)
     epi = (3 if aux is not None else 0) | (32 if w_plain else 0)
+    if colsum_out is not None and defer is not None:
+        epi |= 64
     C().gemm_fp8(g8, w8, out, None, gmeta.s(ig), wmeta.s(iw), o8,
                  gmeta.s(out8_slot) if o8 is not None else None,
                  gmeta.a(out8_slot) if o8 is not None else None,
@@ -263,6 +272,8 @@ def gemm_bf8_dgrad(g8, gmeta: Fp8Meta, ig: int, w8, wmeta: Fp8Meta, iw: int,
                  epi, c, 1, 1, relu_aux,
                  aux.stride(0) if aux is not None else 0, beta, aux8=relu_aux8,
                  colsum_out=colsum_out, colsum_beta=colsum_beta, ws=ws)
+    if colsum_out is not None and defer is not None:
+        defer.append((ws[:nparts * N], colsum_out, nparts, N, colsum_beta))
     return o8
 
 
