@@ -38,6 +38,11 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 // is AMAX_SPREAD words; producers pick one by block id so the atomics of a
 // large grid do not serialise on one address)
 constexpr int BK8 = 128;  // K elements (= bytes) per tile row
+// fp8 GEMM epilogue stores write-through (sc1): see F8Epi::run_w
+#ifndef TDG_F8_EPI_SC1
+#define TDG_F8_EPI_SC1 1
+#endif
+constexpr bool F8_EPI_SC1 = TDG_F8_EPI_SC1 != 0;
 
 namespace f8 {
 
@@ -321,6 +326,11 @@ struct F8Epi {
     static_assert(64 % CPR == 0, "a lane keeps its column chunk across iterations");
     short8_t pre_aux[PRE && !A8 ? ITER : 1];
     const bool vec_ok = F8Epi::vec_ok(ldc, ex);
+    // write-through (sc1) output stores: nothing left dirty in the XCD's L2
+    // for the kernel-end write-back (as the bf16 GEMM epilogue, tdg_gemm.h)
+    const WtBuf wc(C ? (const void*)C : (const void*)C8,
+                   C ? ((size_t)(M - 1) * ldc + N) * sizeof(bf16_t) : 16);
+    const WtBuf wc8(C8 ? (const void*)C8 : (const void*)C, C8 ? (size_t)(M - 1) * ldc8 + N : 16);
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (PRE) {
 #pragma unroll
@@ -426,14 +436,16 @@ struct F8Epi {
       }
       if (C) {
         if (n + 8 <= N) {
-          *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
+          if constexpr (F8_EPI_SC1) wc.st16(C + (size_t)m * ldc + n, v);
+          else *reinterpret_cast<short8_t*>(C + (size_t)m * ldc + n) = v;
         } else {
           for (int e = 0; e < 8 && n + e < N; ++e) C[(size_t)m * ldc + n + e] = (bf16_t)v[e];
         }
       }
       if (C8) {
         if (n + 8 <= N) {
-          *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
+          if constexpr (F8_EPI_SC1) wc8.st8(C8 + (size_t)m * ldc8 + n, make_int2(lo, hi));
+          else *reinterpret_cast<int2*>(C8 + (size_t)m * ldc8 + n) = make_int2(lo, hi);
         } else {
           // (bytes by shifts: taking &lo / &hi put them in scratch memory)
           for (int e = 0; e < 8 && n + e < N; ++e)
