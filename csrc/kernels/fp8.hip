@@ -1447,6 +1447,8 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
   const int mw = m0 + wm * 128, nw = n0 + wn * 128;
   const int cl16 = lane & 15, g4 = 4 * (lane >> 4);
   const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(Cp) & 15) == 0;
+  // write-through (sc1): the gradients are read by Adam, not by this XCD
+  const WtBuf wc(Cp, ((size_t)(M - 1) * ldc + N) * sizeof(float));
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = mw + 16 * i + cl16;
@@ -1458,7 +1460,7 @@ __global__ __launch_bounds__(256) void wgrad_fp8_kernel(const WF8Args args, int 
       f32x4 v = acc[i][j] * alpha;
       if (vec && n + 4 <= N) {
         if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(c);
-        *reinterpret_cast<f32x4*>(c) = v;
+        wc.st16(c, v);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)

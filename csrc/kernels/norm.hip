@@ -22,9 +22,10 @@ namespace tdg {
 // fp8 GEMM; the row's |y| max folded into am.
 // FMT 0: e4m3 (a LayerNorm output for an fp8 forward GEMM), 1: e5m2 (the
 // backward's sublayer gradient ds for an fp8 dgrad / weight gradient)
+// (stored write-through: wt is y8's WtBuf)
 template <int D, int FMT = 0>
 __device__ __forceinline__ void ln_row_y8(const RowVec<D / 64>& o, float s8, uint8_t* __restrict__ y8,
-                                          size_t rbase, int lane, float& am) {
+                                          size_t rbase, int lane, float& am, const WtBuf& wt) {
   constexpr int VEC = D / 64;
   int w[(VEC + 3) / 4];
 #pragma unroll
@@ -45,11 +46,10 @@ __device__ __forceinline__ void ln_row_y8(const RowVec<D / 64>& o, float s8, uin
   if constexpr (VEC == 2) {
     *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(w[0] & 0xffff);
   } else if constexpr (VEC == 4) {
-    *reinterpret_cast<int*>(dst) = w[0];
+    wt.st4(dst, (uint32_t)w[0]);
   } else {
 #pragma unroll
-    for (int i = 0; i < VEC / 8; ++i)
-      *reinterpret_cast<int2*>(dst + 512 * i) = make_int2(w[2 * i], w[2 * i + 1]);
+    for (int i = 0; i < VEC / 8; ++i) wt.st8(dst + 512 * i, make_int2(w[2 * i], w[2 * i + 1]));
   }
 }
 
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     RowVec<VEC> o;
     ln_row_fwd<D>(h[k], t[k], s != nullptr, rbase, row, lane, gamma, beta, y, hsave, mean_out,
                   rstd_out, p, thresh, seed, ctr, site, eps, o, (size_t)M * D * sizeof(bf16_t), kbits);
-    if (y8) ln_row_y8<D>(o, s8p[0], y8, rbase, lane, am);
+    if (y8) ln_row_y8<D>(o, s8p[0], y8, rbase, lane, am, WtBuf(y8, (size_t)M * D));
   }
   if (y8) ln_amax_flush(am, red8, amax8);
 }
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(NWV * 64) void ln_bwd_kernel(
     }
     if (ds_out || ds8) {
       if (ds_out) ds.store_row(ds_out + rbase, lane, wds);
-      if (ds8) ln_row_y8<D, 1>(ds, s8p[0], ds8, rbase, lane, am8);
+      if (ds8) ln_row_y8<D, 1>(ds, s8p[0], ds8, rbase, lane, am8, WtBuf(ds8, (size_t)M * D));
 #pragma unroll
       for (int i = 0; i < VEC; ++i) as[i] += ds.v[i];
     }
