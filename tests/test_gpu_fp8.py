@@ -729,15 +729,16 @@ def test_adam_chunk_kernel_matches_grid_adam_and_quant_multi():
 
 
 @pytest.mark.parametrize("M,N,Kd", [(8192, 4096, 1024), (3000, 3072, 384), (8192, 1536, 256),
-                                     (1100, 1280, 256)])
+                                     (8192, 1040, 256), (1100, 1280, 256)])
 def test_fp8_gemm_persistent_matches_oneshot(M, N, Kd):
     """The persistent 128x128 fp8 GEMM (fp8.hip gemm_fp8_pk_kernel: tiles
     walked by 2 workgroups per CU, the next tile's first K step in flight
     under the epilogue) writes bitwise what the one-shot grid writes: forward
     bias (+ReLU, e4m3 copy, amax) and the e5m2 dgrads (plain-weight transposing
     read; ReLU backward from the 8-bit mask with the fused column sums).
-    Shapes with more tiles than two per CU (ragged M, the two-K-step
-    minimum) take the persistent path; the last one stays one-shot."""
+    Shapes with more tiles than two per CU (ragged M, a partial last column
+    tile, the two-K-step minimum) take the persistent path; the last one
+    stays one-shot."""
     from tensorflow_distributed_on_gke_amd.ops._ext import C as _C
     C = _C()
     torch.manual_seed(11)
