@@ -125,6 +125,9 @@ def main() -> None:
     ap.add_argument("--save-tuned", default=None, help="write the autotuned GEMM table (JSON) here")
     ap.add_argument("--force-dp", type=int, default=0,
                     help="1: run the RCCL data-parallel path even with one rank (testing)")
+    ap.add_argument("--verify-replicas", type=int, default=0,
+                    help="1: after the timed steps (outside the timing), check that every rank's "
+                         "weights are bitwise equal (DataParallel.verify_replicas; exits non-zero if not)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -204,6 +207,10 @@ def main() -> None:
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
+    verified = None
+    if args.verify_replicas and ddp is not None and world > 1:
+        ddp.verify_replicas()  # raises on divergence
+        verified = True
     ms = elapsed / args.steps * 1000.0
     global_batch = args.local_batch * world
     tokens = global_batch * (S + T) * args.steps
@@ -239,6 +246,7 @@ def main() -> None:
                 "defer_wgrad": step.rt.wgrad is not None,
                 "bucket_mb": args.bucket_mb,
                 "last_loss": round(loss, 4),
+                **({"replicas_verified": verified} if verified is not None else {}),
             },
         }), flush=True)
     if args.save_tuned and info.rank == 0:

@@ -93,16 +93,6 @@ int tdg_adam_chunks(float* p, float* g, float* m, float* v, void* shadow, long l
                     float weight_decay, int sched, int zero_grad, int inc_step,
                     const float* scale8, unsigned* amax8, hipStream_t st);
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
-int tdg_gemm_ln_fwd(const void* A, const void* W, const float* bias, const void* x,
-                    const float* gamma, const float* beta, void* y, void* hsave, float* mean,
-                    float* rstd, int M, int N, int K, int lda, int ldw, float p, uint64_t seed,
-                    const long long* ctr, uint64_t site, float eps, void* kbits, void* xch,
-                    unsigned* band_ctr, unsigned* err, int stages, int ablate, hipStream_t st);
-int tdg_gemm_ln_bwd(const void* A, const void* W, const void* C, const void* h, const float* mean,
-                    const float* rstd, const float* gamma, void* dh, void* ds, float* part, int M,
-                    int N, int K, int lda, int ldw, float beta, float p, uint64_t seed,
-                    const long long* ctr, uint64_t site, const void* kbits, void* xch,
-                    unsigned* band_ctr, unsigned* err, int stages, int ablate, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
 }
@@ -202,19 +192,7 @@ void gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tens
   check_err(rc, "tdg gemm");
 }
 
-// ---------------------------------------------------------------- GEMM + LayerNorm
-// The band-exchange state shared by every fused launch of a device (one
-// stream): xch f32 [>= bands * 128 * 4 * 2], counters int32 [>= bands], err
-// int32 [1] (ops/kernels.py _ln_xch).
-void check_ln_xch(const Tensor& xch, const Tensor& band_ctr, const Tensor& err, int64_t M) {
-  const int64_t bands = (M + 127) / 128;
-  check_f32(xch, "xch");
-  TORCH_CHECK(xch.numel() >= bands * 128 * 4 * 2, "gemm_ln: exchange buffer too small");
-  TORCH_CHECK(band_ctr.is_cuda() && band_ctr.scalar_type() == at::kInt && band_ctr.numel() >= bands,
-              "gemm_ln: band counters int32 [>= bands]");
-  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "gemm_ln: err int32");
-}
-
+// ---------------------------------------------------------------- LayerNorm helpers
 // dropout keep-bit bitmap of a [M, D] LayerNorm: uint8 [M, D / 8]
 void check_kbits(const optional<Tensor>& kbits, int64_t M, int64_t D) {
   if (!kbits.has_value()) return;
@@ -222,107 +200,6 @@ void check_kbits(const optional<Tensor>& kbits, int64_t M, int64_t D) {
                   kbits->numel() == M * D / 8 &&
                   (reinterpret_cast<uintptr_t>(kbits->data_ptr()) % 4) == 0,
               "kbits: uint8 [M, D / 8], 4-byte aligned");
-}
-
-int64_t ln_stages(int64_t stages, int64_t K) {
-  if (stages == 3 || stages == 4) return stages;
-  return K <= 512 ? 3 : 4;
-}
-
-// y, h, mean, rstd = LN(x + dropout(A @ W^T + bias)) for D = 512 (N of the GEMM)
-void gemm_ln_fwd(const Tensor& A, const Tensor& W, const Tensor& bias, const Tensor& x,
-                 const Tensor& gamma, const Tensor& beta, const Tensor& y, const Tensor& h,
-                 const Tensor& mean, const Tensor& rstd, double p, int64_t seed,
-                 const optional<Tensor>& ctr, int64_t site, double eps,
-                 const optional<Tensor>& kbits, const Tensor& xch, const Tensor& band_ctr,
-                 const Tensor& err, int64_t stages, int64_t ablate) {
-  check_bf16(A, "A");
-  check_bf16(W, "W");
-  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "gemm_ln_fwd: A [M,K], W [N,K]");
-  const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
-  TORCH_CHECK(N == 512, "gemm_ln_fwd: d_model 512 only (4 column tiles per band)");
-  TORCH_CHECK(A.stride(1) == 1 && W.is_contiguous() && A.stride(0) % 8 == 0 && K % 8 == 0,
-              "gemm_ln_fwd: K-contiguous operands, rows 16-byte aligned");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0, "gemm_ln_fwd: A alignment");
-  for (auto* t : {&x, &y, &h}) {
-    check_bf16(*t, "x/y/h");
-    check_contig(*t, "x/y/h");
-    TORCH_CHECK(t->numel() == M * N, "gemm_ln_fwd: x / y / h must be [M, 512]");
-  }
-  for (auto* t : {&bias, &gamma, &beta}) {
-    check_f32(*t, "bias/gamma/beta");
-    TORCH_CHECK(t->numel() == N && t->is_contiguous(), "gemm_ln_fwd: bias / gamma / beta [512]");
-  }
-  for (auto* t : {&mean, &rstd}) {
-    check_f32(*t, "mean/rstd");
-    TORCH_CHECK(t->numel() >= M, "gemm_ln_fwd: mean / rstd [M]");
-  }
-  check_ln_xch(xch, band_ctr, err, M);
-  check_kbits(kbits, M, N);
-  const long long* cp = ctr.has_value() ? reinterpret_cast<const long long*>(ctr->data_ptr<int64_t>()) : nullptr;
-  c10::DeviceGuard g(A.device());
-  check_err(tdg_gemm_ln_fwd(A.data_ptr(), W.data_ptr(), bias.data_ptr<float>(), x.data_ptr(),
-                            gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
-                            h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)M,
-                            (int)N, (int)K, (int)A.stride(0), (int)K, (float)p, (uint64_t)seed, cp,
-                            (uint64_t)site, (float)eps,
-                            kbits.has_value() ? kbits->data_ptr() : nullptr, xch.data_ptr(),
-                            reinterpret_cast<unsigned*>(band_ctr.data_ptr()),
-                            reinterpret_cast<unsigned*>(err.data_ptr()), (int)ln_stages(stages, K),
-                            (int)ablate, stream_of(A)),
-            "tdg gemm_ln_fwd");
-}
-
-// dh, ds, column partials = LayerNorm backward of dy = dY @ W (+ C) for D = 512
-// (W [Kd, 512]: the GEMM's N = 512, K = Kd); part f32 [3][bands][512]
-void gemm_ln_bwd(const Tensor& A, const Tensor& W, const optional<Tensor>& C, const Tensor& h,
-                 const Tensor& mean, const Tensor& rstd, const Tensor& gamma, const Tensor& dh,
-                 const optional<Tensor>& ds, const Tensor& part, double p, int64_t seed,
-                 const optional<Tensor>& ctr, int64_t site, const optional<Tensor>& kbits,
-                 const Tensor& xch, const Tensor& band_ctr, const Tensor& err, int64_t stages,
-                 int64_t ablate) {
-  check_bf16(A, "A");
-  check_bf16(W, "W");
-  TORCH_CHECK(A.dim() == 2 && W.dim() == 2, "gemm_ln_bwd: A [M,K], W [K,N]");
-  const int64_t M = A.size(0), K = W.size(0), N = W.size(1);
-  TORCH_CHECK(N == 512, "gemm_ln_bwd: d_model 512 only (4 column tiles per band)");
-  TORCH_CHECK(A.size(1) >= K && A.stride(1) == 1 && A.stride(0) % 8 == 0 &&
-                  A.stride(0) >= (K + 7) / 8 * 8 && W.is_contiguous(),
-              "gemm_ln_bwd: dY K-contiguous (ld >= round8(K)), W contiguous");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) % 16) == 0, "gemm_ln_bwd: A alignment");
-  check_extent(A, M, A.stride(0), (K + 7) / 8 * 8, "A");
-  std::vector<const Tensor*> outs = {&h, &dh};
-  if (C.has_value()) outs.push_back(&*C);
-  if (ds.has_value()) outs.push_back(&*ds);
-  for (auto* t : outs) {
-    check_bf16(*t, "h/dh/ds/C");
-    check_contig(*t, "h/dh/ds/C");
-    TORCH_CHECK(t->numel() == M * N, "gemm_ln_bwd: h / dh / ds / C must be [M, 512]");
-  }
-  check_f32(gamma, "gamma");
-  TORCH_CHECK(gamma.numel() == N, "gemm_ln_bwd: gamma [512]");
-  for (auto* t : {&mean, &rstd}) {
-    check_f32(*t, "mean/rstd");
-    TORCH_CHECK(t->numel() >= M, "gemm_ln_bwd: mean / rstd [M]");
-  }
-  check_f32(part, "part");
-  TORCH_CHECK(part.numel() >= 3 * ((M + 127) / 128) * N, "gemm_ln_bwd: partials [3][bands][512]");
-  check_ln_xch(xch, band_ctr, err, M);
-  check_kbits(kbits, M, N);
-  const long long* cp = ctr.has_value() ? reinterpret_cast<const long long*>(ctr->data_ptr<int64_t>()) : nullptr;
-  c10::DeviceGuard g(A.device());
-  check_err(tdg_gemm_ln_bwd(A.data_ptr(), W.data_ptr(), C.has_value() ? C->data_ptr() : nullptr,
-                            h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                            gamma.data_ptr<float>(), dh.data_ptr(),
-                            ds.has_value() ? ds->data_ptr() : nullptr, part.data_ptr<float>(),
-                            (int)M, (int)N, (int)K, (int)A.stride(0), (int)N,
-                            C.has_value() ? 1.f : 0.f, (float)p, (uint64_t)seed, cp,
-                            (uint64_t)site, kbits.has_value() ? kbits->data_ptr() : nullptr,
-                            xch.data_ptr(),
-                            reinterpret_cast<unsigned*>(band_ctr.data_ptr()),
-                            reinterpret_cast<unsigned*>(err.data_ptr()), (int)ln_stages(stages, K),
-                            (int)ablate, stream_of(A)),
-            "tdg gemm_ln_bwd");
 }
 
 void colsum(const Tensor& X, const Tensor& out, const Tensor& part, int64_t M, int64_t N,
@@ -1503,8 +1380,6 @@ void to_bf16(const Tensor& p, const Tensor& o) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
-  m.def("gemm_ln_fwd", &gemm_ln_fwd);
-  m.def("gemm_ln_bwd", &gemm_ln_bwd);
   m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),

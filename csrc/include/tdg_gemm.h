@@ -1,4 +1,4 @@
-// Shared pieces of the MFMA GEMM kernels (gemm.hip, gemm_ln.hip): LDS tile
+// Shared pieces of the MFMA GEMM kernels (gemm.hip, fp8.hip): LDS tile
 // image layout (XOR-swizzled), the LDS-DMA operand stager, counted waits and
 // MFMA fragment reads.
 #pragma once

@@ -125,8 +125,8 @@ __device__ __forceinline__ void ln_row_fwd(RowVec<D / 64>& h, RowVec<D / 64>& t,
       const uint32_t km = keep_bits<VEC>(seed, ctr, site, rbase, lane, thresh);
       if constexpr (VEC >= 8) {
         // the keep bits as a row-major bitmap (bit c % 8 of byte c / 8 of the
-        // row = column c): the fused LayerNorm backward reads them instead of
-        // regenerating the mask (tdg_gemm_ln.h)
+        // row = column c): the LayerNorm backward reads them instead of
+        // regenerating the mask (ln_bwd_kernel)
         if (kbits) {
 #pragma unroll
           for (int c = 0; c < RowMap<VEC>::CH; ++c)

@@ -26,7 +26,6 @@
 #include "tdg_gemm.h"
 #include "tdg_reduce.h"
 #include "gemm_pipe.h"
-#include "tdg_gemm_ln.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -51,12 +50,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
     const float* __restrict__ bias, const bf16_t* __restrict__ aux, int M, int N, int K, int lda,
     int ldb, int ldc, int ldaux, float alpha, float beta, int k_per_split, long long split_stride,
-    const GemmGroup grp, const LnEpiArgs lnx) {
-  // EPI_LNF / EPI_LNB: the post-LN block tail fused into the epilogue
-  // (tdg_gemm_ln.h; 128x128 tiles on 2 x 4 waves, N = D = 512, bf16 out)
-  constexpr bool LNF = EPI == EPI_LNF, LNB = EPI == EPI_LNB;
-  static_assert(!(LNF || LNB) || (BM == 128 && BN == 128 && WM == 2 && WN == 4 && A_KC && !OUT_F32),
-                "fused LayerNorm epilogues: 128x128 tiles, 2x4 waves, bf16 out");
+    const GemmGroup grp) {
   if (gridDim.y > 1) {
     A = grp.A[blockIdx.y];
     B = grp.B[blockIdx.y];
@@ -116,8 +110,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   using OutT = typename std::conditional<OUT_F32, float, bf16_t>::type;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RPASS = OUT_F32 ? (WTM < 32 ? WTM : 32) : WTM;
-  constexpr int EPI_ST = (LNF || LNB) ? EPI_NONE : EPI;
-  using Epi = EpiLds<EPI_ST, OUT_F32, TM, TN, RPASS>;
+  using Epi = EpiLds<EPI, OUT_F32, TM, TN, RPASS>;
   using EpiF = EpiLds<EPI_NONE, true, TM, TN, (WTM < 32 ? WTM : 32)>;  // split-K slabs
   static_assert(NW * Epi::BYTES <= STAGES * (BM + BN) * BK * 2 &&
                     NW * EpiF::BYTES <= STAGES * (BM + BN) * BK * 2,
@@ -137,43 +130,6 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
     if (pre_aux && in) aux_r[t] = *reinterpret_cast<const int4*>(aux + (size_t)m * ldaux + n);
     if (pre_c && in)
       c_r[t] = *reinterpret_cast<const int4*>(reinterpret_cast<const OutT*>(Cv) + (size_t)m * ldc + n);
-  }
-
-  // fused LayerNorm tails: their per-element operands in the accumulator
-  // layout (lane: rows 16i + (lane & 15), 4 consecutive columns per 16-column
-  // sub-tile), loaded before the main loop like the epilogue operands above
-  constexpr int LT = (LNF || LNB) ? 4 : 1, LJ = (LNF || LNB) ? 2 : 1;
-  int2 ln_a[LT][LJ], ln_b[LT][LJ];
-  float ln_m[LT], ln_r[LT];
-  uint32_t ln_k[LT];
-  f32x4 ln_bias[LJ];
-  if constexpr (LNF || LNB) {
-    const int g = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = min(m0 + wm * WTM + 16 * i + (lane & 15), M - 1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const size_t o = (size_t)m * N + n0 + wn * WTN + 16 * j + 4 * g;
-        if constexpr (LNF) {
-          ln_a[i][j] = *reinterpret_cast<const int2*>(lnx.x + o);
-        } else {
-          ln_a[i][j] = beta != 0.f ? *reinterpret_cast<const int2*>(reinterpret_cast<const bf16_t*>(Cv) + o)
-                                   : make_int2(0, 0);
-          ln_b[i][j] = *reinterpret_cast<const int2*>(lnx.h_in + o);
-        }
-      }
-      if constexpr (LNB) {
-        ln_m[i] = lnx.mean_in[m];
-        ln_r[i] = lnx.rstd_in[m];
-        ln_k[i] = lnx.kbits ? lnx.kbits[(size_t)m * (N / 32) + (n0 + wn * WTN) / 32] : 0u;
-      }
-    }
-    if constexpr (LNF) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        ln_bias[j] = *reinterpret_cast<const f32x4*>(bias + n0 + wn * WTN + 16 * j + 4 * g);
-    }
   }
 
   f32x4 acc[TM][TN];
@@ -289,26 +245,6 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(
   // (EpiLds, tdg_gemm.h). Split-K partial products go unscaled into the f32
   // slab of split z.
   lds_barrier();  // all waves done with the pipeline stages
-  if constexpr (LNF || LNB) {
-    if constexpr (LNF) {
-      // s = bf16(acc + bias), exactly the value the unfused GEMM stores
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][e] = bf2f(f2bf(alpha * acc[i][j][e] + ln_bias[j][e]));
-      ln_fwd_epilogue(smem, acc, lane, wid, wm, wn, m0, n0, tm, tn, M, N, lnx, ln_a);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] *= alpha;
-      ln_bwd_epilogue(smem, acc, lane, wid, wm, wn, m0, n0, tm, tn, M, N, lnx, beta != 0.f, ln_a,
-                      ln_b, ln_m, ln_r, ln_k);
-    }
-    return;
-  }
   const int mw0 = m0 + wm * WTM, nw0 = n0 + wn * WTN;
   if (split) {
     float* Cs = reinterpret_cast<float*>(Cv) + (size_t)blockIdx.z * split_stride;
@@ -750,12 +686,9 @@ namespace {
 template <int BM, int BN, int WM, int WN, int ST, bool AK, bool BKc, int EPI, bool F32>
 void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, const bf16_t* aux,
                 int M, int N, int K, int lda, int ldb, int ldc, int ldaux, float alpha, float beta,
-                int splits, float* ws, hipStream_t st, const GemmGroup* grp = nullptr, int G = 1,
-                const LnEpiArgs* ln = nullptr) {
+                int splits, float* ws, hipStream_t st, const GemmGroup* grp = nullptr, int G = 1) {
   static const GemmGroup kNoGroup{};
-  static const LnEpiArgs kNoLn{};
   const GemmGroup& gr = grp ? *grp : kNoGroup;
-  const LnEpiArgs& lx = ln ? *ln : kNoLn;
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   const int lds = ST * (BM + BN) * BK * 2;  // pipeline stages only (register epilogue)
   static bool attr_set = false;  // >64 KiB dynamic LDS needs the opt-in
@@ -769,14 +702,14 @@ void launch_cfg(const bf16_t* A, const bf16_t* B, void* C, const float* bias, co
   if (splits <= 1 || G > 1) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI, F32>), dim3(tiles, G, 1),
                        dim3(WM * WN * 64), lds, st, A, B, C, bias, aux, M, N, K, lda, ldb, ldc,
-                       ldaux, alpha, beta, K, 0LL, gr, lx);
+                       ldaux, alpha, beta, K, 0LL, gr);
   } else {
     int kps = cdiv(cdiv(K, splits), BK) * BK;
     splits = cdiv(K, kps);
     const long long stride = (long long)M * ldc;
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, ST, AK, BKc, EPI_NONE, true>),
                        dim3(tiles, 1, splits), dim3(WM * WN * 64), lds, st, A, B, (void*)ws, bias,
-                       aux, M, N, K, lda, ldb, ldc, ldaux, 1.f, 0.f, kps, stride, gr, lx);
+                       aux, M, N, K, lda, ldb, ldc, ldaux, 1.f, 0.f, kps, stride, gr);
     const long long total = (long long)M * N;
     const int blocks = (int)std::min<long long>(4096, (total + 255) / 256);
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, F32>), dim3(blocks), dim3(256), 0, st, ws, C,
@@ -980,24 +913,6 @@ int dispatch_epi(int epi, bool f32, int tile_cfg, const bf16_t* A, const bf16_t*
 }
 
 }  // namespace
-
-// Fused post-LN GEMM (EPI_LNF: forward NT with bias; EPI_LNB: dgrad NN,
-// beta = 0 or 1 onto C): 128x128 tiles, 8 waves (2 x 4), `stages` 3 or 4.
-template <bool BKc, int EPI>
-int launch_ln(const bf16_t* A, const bf16_t* B, void* C, const float* bias, int M, int N, int K,
-              int lda, int ldb, int ldc, float beta, int stages, const LnEpiArgs& ln,
-              hipStream_t st) {
-  if (N != 128 * LN_BAND_TILES || ldc != N || K <= 0) return -2;
-  if (stages == 3)
-    launch_cfg<128, 128, 2, 4, 3, true, BKc, EPI, false>(A, B, C, bias, nullptr, M, N, K, lda, ldb,
-                                                        ldc, 0, 1.f, beta, 1, nullptr, st, nullptr,
-                                                        1, &ln);
-  else
-    launch_cfg<128, 128, 2, 4, 4, true, BKc, EPI, false>(A, B, C, bias, nullptr, M, N, K, lda, ldb,
-                                                        ldc, 0, 1.f, beta, 1, nullptr, st, nullptr,
-                                                        1, &ln);
-  return 0;
-}
 
 // Per-layout entry points: each operand layout's instantiations are
 // compiled in a translation unit of their own (gemm_<layout>.hip), so the

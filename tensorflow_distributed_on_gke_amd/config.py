@@ -77,6 +77,13 @@ class Settings:
     bucket_mb: float = 64.0
     grad_comm_dtype: str = "fp32"  # fp32 | bf16 (gradient all-reduce payload)
     hip_graph: bool = False
+    # variable-length (text) batches under hip_graph: each batch's source and
+    # target-input lengths are padded up to a multiple of graph_bucket (capped
+    # at max_len; semantically neutral -- attention, loss and LayerNorm are
+    # length-masked) and one captured step per (source, target) bucket is kept,
+    # at most graph_cache of them (least recently used evicted)
+    graph_bucket: int = 32
+    graph_cache: int = 64
     idle_after_train: bool = False  # reference __main__.py:183-186 keeps the pod alive
     check_replicas_every: int = 0  # debug: assert bitwise-identical replicas every N steps
     metrics_file: Optional[str] = None  # JSONL metrics sink (rank 0)

@@ -23,6 +23,10 @@ Here (no TensorFlow, no network):
   batch), each global batch right-padded with PAD to its longest sequence
   (`.to_tensor()`). Pairs longer than max_len tokens are dropped (the
   reference would fail on them: positional tables of length 1000).
+  `bucket` > 1 pads further, to the next multiple of `bucket` (source) and
+  of `bucket` + the one shifted token (target), capped at max_len, so the
+  batch shapes fall into few buckets and the HIP-graph step cache
+  (train/step.py) replays a captured step for most batches.
 """
 from __future__ import annotations
 
@@ -106,6 +110,18 @@ def pad_rows(rows: Sequence[Sequence[int]], length: Optional[int] = None) -> tor
     return out
 
 
+def bucket_lengths(S: int, T: int, bucket: int, max_len: int) -> Tuple[int, int]:
+    """Padded (source, target) lengths of a batch whose longest rows are S
+    and T tokens: the source to a multiple of `bucket`, the target so that
+    the teacher-forced decoder input (T - 1 tokens) is one; both capped at
+    max_len (longer pairs were dropped, so the cap never cuts a row)."""
+    if bucket <= 1:
+        return S, T
+    Sb = min(-(-S // bucket) * bucket, max(S, max_len))
+    Tb = min(-(-(T - 1) // bucket) * bucket + 1, max(T, max_len))
+    return Sb, Tb
+
+
 def read_pairs(path: str) -> List[Tuple[str, str]]:
     """`source<TAB>target` lines (blank lines and lines without a tab skipped)."""
     pairs = []
@@ -161,7 +177,7 @@ class TextPairs:
 
     def __init__(self, path: str, src_tok, tgt_tok, local_batch: int, rank: int = 0, world: int = 1,
                  seed: int = 0, shuffle_buffer: int = 20000, shuffle: bool = True,
-                 max_len: int = 1000, pin: bool = False):
+                 max_len: int = 1000, pin: bool = False, bucket: int = 1):
         pairs = read_pairs(path)
         src_ids = src_tok.encode_batch([p[0] for p in pairs])
         tgt_ids = tgt_tok.encode_batch([p[1] for p in pairs])
@@ -175,6 +191,7 @@ class TextPairs:
             raise ValueError(f"{path}: {len(self.src)} pairs, fewer than one global batch "
                              f"({self.global_batch})")
         self.seed, self.shuffle_buffer, self.shuffle = seed, shuffle_buffer, shuffle
+        self.bucket, self.max_len = max(1, int(bucket)), max_len
         self.pin = pin and torch.cuda.is_available()
         # full global batches per epoch (the tail that does not fill one is skipped
         # so every rank runs the same number of synchronous steps)
@@ -200,8 +217,8 @@ class TextPairs:
         epoch, i = divmod(step, self.steps_per_epoch)
         order = self._epoch_order(epoch)
         g = order[i * self.global_batch:(i + 1) * self.global_batch]
-        S = max(len(self.src[j]) for j in g)
-        T = max(len(self.tgt[j]) for j in g)
+        S, T = bucket_lengths(max(len(self.src[j]) for j in g), max(len(self.tgt[j]) for j in g),
+                              self.bucket, self.max_len)
         mine = g[self.rank * self.local_batch:(self.rank + 1) * self.local_batch]
         src = pad_rows([self.src[j] for j in mine], S)
         tgt = pad_rows([self.tgt[j] for j in mine], T)

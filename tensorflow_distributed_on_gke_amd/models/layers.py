@@ -65,9 +65,6 @@ class RunCtx:
     fp8: Optional[object] = None
     # WgradQueue: weight gradients deferred to the end of backward (grouped)
     wgrad: Optional["WgradQueue"] = None
-    # the last post-LN block output whose LayerNorm backward may be fused
-    # into its consumer's dgrad (LnLink), until a consumer claims it
-    ln_out: Optional["LnLink"] = None
 
     @property
     def p(self) -> float:
@@ -97,73 +94,12 @@ class KVGrad:
     wkv: Optional["Param"] = None  # the batched K|V projection (its e5m2 gradient slot)
 
 
-@dataclass(eq=False)
-class LnLink:
-    """A post-LN block output y whose LayerNorm BACKWARD runs in the epilogue
-    of the dgrad that produces y's gradient -- the consumer's last GEMM (the
-    next block's input-projection / FFN1 dgrad, the batched cross K|V dgrad,
-    the vocabulary projection's dgrad; ops.kernels.dgrad_ln_bwd).
-
-    The producing block's forward publishes it (rt.ln_out); the consuming
-    block's forward claims it when its input IS y. In backward the consumer
-    computes (dh, ds) of the producer's LayerNorm and hands them over in
-    `fused`; the producer's backward then skips its own LayerNorm backward
-    (the gradient autograd passes it is that dh). Only on the GPU, bf16,
-    d_model 512, with the deferred weight-gradient queue (whose column-sum
-    folds it joins)."""
-    y: torch.Tensor
-    saved: tuple
-    gamma: Param
-    beta: Param
-    sub_bias: Param
-    site: int
-    fused: Optional[tuple] = None
-
-
-def _ln_linkable(rt: RunCtx, x: torch.Tensor) -> bool:
-    """This LayerNorm's backward will be fused into its consumer's dgrad (its
-    forward then also saves the dropout keep bits)."""
-    return (x.is_cuda and rt.training and rt.wgrad is not None and rt.fp8 is None
-            and K.ln_fused_ok(x.shape[-1]))
-
-
-def _publish_ln(rt: RunCtx, y: torch.Tensor, saved, gamma: Param, beta: Param, sub_bias: Param,
-                site: int) -> Optional[LnLink]:
-    if not (_ln_linkable(rt, y) and saved[3] is None):
-        rt.ln_out = None
-        return None
-    rt.ln_out = LnLink(y, saved, gamma, beta, sub_bias, site)
-    return rt.ln_out
-
-
-def _claim_ln(rt: RunCtx, x: torch.Tensor) -> Optional[LnLink]:
-    link = rt.ln_out
-    if link is not None and link.y is x:
-        rt.ln_out = None
-        return link
-    return None
-
-
-def _dgrad_ln(dy2: torch.Tensor, w: Param, N: int, dres: Optional[torch.Tensor],
-              link: Optional[LnLink], rt: RunCtx) -> torch.Tensor:
-    """The consumer's last dgrad: dx = dy2 @ w (+ dres, the residual gradient
-    already in dx). With a claimed link, the producer's LayerNorm backward
-    runs in the same launch: returns its dh (what autograd passes on as dx)
-    and leaves (dh, ds) in link.fused."""
-    if link is None:
-        if dres is None:
-            return K.linear_dgrad(dy2, w.compute, N)
-        return _dgrad_into(dy2, w, N, dres)
-    q = rt.wgrad
-    h, mean, rstd, _, kbits = link.saved
-    M, D = dy2.shape[0], w.shape[1]
-    dh, ds = K.dgrad_ln_bwd(dy2, w.compute, dres, h, mean, rstd, link.gamma.master, link.gamma.grad,
-                            link.beta.grad, link.sub_bias.grad, rt.p, rt.seed, rt.ctr, link.site,
-                            q.reductions, accumulate=rt.accumulate,
-                            stages=3 if N <= 512 else 4, kbits=kbits)
-    q.reduced_params += [(rt, link.gamma), (rt, link.beta), (rt, link.sub_bias)]
-    link.fused = (dh, ds)
-    return dh.view(M, D)
+def _dgrad_res(dy2: torch.Tensor, w: Param, N: int, dres: Optional[torch.Tensor]) -> torch.Tensor:
+    """A block's input gradient dx = dy2 @ w (+ dres, the residual gradient
+    already in dx: accumulated by the GEMM's beta = 1 epilogue)."""
+    if dres is None:
+        return K.linear_dgrad(dy2, w.compute, N)
+    return _dgrad_into(dy2, w, N, dres)
 
 
 def _keep_scale(rt: RunCtx, site: int, shape, device) -> Optional[torch.Tensor]:
@@ -476,22 +412,17 @@ def _attn_f8_bwd(ctx, Lq: int, Lk: int, hd: int) -> bool:
 def _proj_ln_fwd(a2, w: Param, b: Param, x, gamma: Param, beta: Param, site: int, rt: RunCtx):
     """GPU block tail y = LN(x + dropout(a2 @ w^T + b)) -> (y, saved): the
     output-projection GEMM (bias fused) then the fused dropout + residual +
-    LayerNorm kernel. (A single fused GEMM + LayerNorm launch measured slower
-    on MI355X: every workgroup then streams all of W; csrc/lab/gemm_ln.hip.)"""
-    if x.is_cuda and rt.fp8 is None and K.ln_fused_fwd_ok(x.shape[-1]):
-        # one launch: the LayerNorm runs in the GEMM's epilogue
-        kbits = _kbits(rt, x)
-        y, h, mean, rstd = K.linear_ln_fwd(a2, w.compute, b.master, x.contiguous(), gamma.master,
-                                           beta.master, rt.p, rt.seed, rt.ctr, site, eps=LN_EPS,
-                                           stages=3, kbits=kbits)
-        return y.view(x.shape), (h.view(x.shape), mean, rstd, None, kbits)
+    LayerNorm kernel. (GEMM + LayerNorm in one launch measured slower on
+    MI355X, both as full-row tiles -- every workgroup streams all of W,
+    csrc/lab/gemm_ln.hip -- and as 128-column tiles exchanging row partials
+    across workgroups: profiles/r5/ln_fused_ab.txt.)"""
     s = K.linear_fwd(a2, w.compute, b.master)
     return _ln_fwd(x, s.view(x.shape), gamma, beta, site, rt)
 
 
 # the training forward's LayerNorms save their dropout keep bits (1 bit per
 # element) for the backward, which reads them instead of regenerating the
-# Philox mask (ln_bwd / dgrad_ln_bwd kbits)
+# Philox mask (ln_bwd kbits)
 LN_KEEP_BITS = os.environ.get("TDG_LN_KEEP_BITS", "1") != "0"
 
 
@@ -525,18 +456,12 @@ def _ln_fwd(x, s, gamma: Param, beta: Param, site: int, rt: RunCtx):
 
 
 def _ln_bwd(dy, saved, gamma: Param, beta: Param, sub_bias: Param, site: int, rt: RunCtx,
-            ds8_slot: Optional[int] = None, link: Optional[LnLink] = None):
+            ds8_slot: Optional[int] = None):
     """Returns (dh, ds): dh = dL/d(residual input) (fresh, writable), ds =
     dL/d(sublayer output). Also writes dgamma, dbeta and the sublayer's output
     bias gradient (sum of ds over rows). ds8_slot (GPU, fp8 backward): ds is
     returned as its e5m2 copy only (scale slot ds8_slot of rt.fp8.gmeta,
     amax recorded), the bf16 ds is not written."""
-    if link is not None and link.fused is not None:
-        # already computed by the consumer's dgrad epilogue (_dgrad_ln); its
-        # column-sum folds are queued and the parameters reported there
-        dh, ds = link.fused
-        link.fused = None
-        return dh.view(dy.shape), ds.view(dy.shape)
     h, mean, rstd, ks = saved[:4]
     if dy.is_cuda:
         q = rt.wgrad
@@ -653,7 +578,6 @@ class SelfAttnBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(hd)
         ctx.p = (wqkv, bqkv, wo, bo, gamma, beta)
         ctx.meta = (heads, causal, scale, site, rt)
-        ctx.in_link = _claim_ln(rt, x)
         x2 = x.reshape(B * L, d)
         ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * L, wqkv, wo, d)
         kx = [] if lean else None
@@ -696,7 +620,6 @@ class SelfAttnBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(o.view(B * L, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, L, d), gamma, beta, site, rt)
-        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, bo, site)
         ctx.save_for_backward(x2, qkv, o, aux, kv_len)
         return y
 
@@ -711,7 +634,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
         bt = _beta(rt)
         if ctx.lean:
             return SelfAttnBlockFn._backward_fp8(ctx, dy)
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, link=ctx.out_link)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         q5 = qkv.view(B, L, 3, heads, hd)
         if dy.is_cuda:
@@ -722,7 +645,7 @@ class SelfAttnBlockFn(torch.autograd.Function):
             K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
                        g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
             _wgrad(rt, dqkv, x2, 3 * d, wqkv, bqkv)
-            dx = _dgrad_ln(dqkv, wqkv, 3 * d, dh, ctx.in_link, rt)
+            dx = _dgrad_res(dqkv, wqkv, 3 * d, dh)
             if rt.wgrad is not None:
                 rt.wgrad.layer_end()  # self-attention is a layer's first block
             return (dx.view(B, L, d),) + (None,) * 11
@@ -812,6 +735,14 @@ class SelfAttnBlockFn(torch.autograd.Function):
 
 
 # =============================================================================== cross-attention
+def _take_dkv(dkv_in, kvh: KVGrad, rows: int) -> torch.Tensor:
+    """The batched d(K|V) [rows, layers * 2d] the decoder layers filled (layer
+    0 also hands it to autograd, which delivers it as dkv_in)."""
+    dkv = (dkv_in if dkv_in is not None else kvh.buf).reshape(rows, -1)
+    kvh.buf = None
+    return dkv
+
+
 class CrossKVFn(torch.autograd.Function):
     """kv_all[B, S, layers*2*d] = enc @ Wkv_all^T + b: the K and V projections
     of the encoder output for every decoder layer in one GEMM."""
@@ -822,7 +753,6 @@ class CrossKVFn(torch.autograd.Function):
         e2 = enc.reshape(B * S, d)
         ctx.p = (wkv, bkv)
         ctx.kvh, ctx.rt, ctx.shape = kvh, rt, (B, S, d)
-        ctx.in_link = _claim_ln(rt, enc)
         ctx.save_for_backward(e2)
         ctx.lean = lean = enc.is_cuda and _attn_lean(rt, B * S, wkv, None, d)
         kx = [] if lean else None
@@ -842,8 +772,10 @@ class CrossKVFn(torch.autograd.Function):
                 if r is not None:  # its e4m3 copy feeds the decoders' e4m3 attention
                     kv = r[0]
                     rt.fp8.kv8 = (r[1].view(B, S, -1), r[2])
-                    if kvh.f8b:  # (autograd needs the output tensor; its values are never read)
-                        kv = torch.empty(B * S, r[1].shape[1], dtype=torch.bfloat16, device=enc.device)
+                    if kvh.f8b:  # (autograd needs an output of this shape; nothing reads
+                        # it: a zero-stride placeholder, not a bf16 K|V image)
+                        kv = torch.zeros(1, dtype=torch.bfloat16, device=enc.device).expand(
+                            B * S, r[1].shape[1])
             if kv is None:
                 kv = K.linear_fwd(e2.contiguous(), wkv.compute, bkv.master)
         else:
@@ -859,8 +791,6 @@ class CrossKVFn(torch.autograd.Function):
         # filled slice-by-slice by every CrossAttnBlockFn.backward (layer 0
         # also hands it to autograd, which delivers it here as dkv_in)
         kvh = ctx.kvh
-        dkv = (dkv_in if dkv_in is not None else kvh.buf).reshape(B * S, -1)
-        kvh.buf = None
         N = wkv.shape[0]
         bt = _beta(rt)
         if e2.is_cuda and ctx.f8a is not None:
@@ -869,24 +799,26 @@ class CrossKVFn(torch.autograd.Function):
             st = rt.fp8
             x8, xs = ctx.f8a
             gk = st.proj_bwd[id(wkv)]
-            if kvh.f8b:  # written by the layers' fp8 attention backward (e5m2 + bias sums)
+            if kvh.f8b:  # written by the layers' fp8 attention backward (e5m2 + bias sums;
+                # dkv_in is the layers' zero-stride placeholder)
                 dkv8 = kvh.buf8.reshape(B * S, -1)
                 _fold_bias_later(rt, kvh.part, B, N, bkv)
                 kvh.buf8 = kvh.part = None
             else:
-                dkv8 = _fp8_grad_bias(dkv.contiguous(), gk, bkv, rt, "kv")
+                dkv8 = _fp8_grad_bias(_take_dkv(dkv_in, kvh, B * S).contiguous(), gk, bkv, rt, "kv")
             rt.wgrad.add_fp8(dkv8, st.gmeta.s(gk), x8, st.meta.s(xs), wkv, bt, rt)
             rt.wgrad.boundary()
-            denc = torch.empty(B * S, d, dtype=torch.bfloat16, device=dkv.device)
+            denc = torch.empty(B * S, d, dtype=torch.bfloat16, device=e2.device)
             _fp8_dgrad_into(dkv8, gk, wkv, denc, rt, 0.0)
             if rt.store is not None:
                 rt.store.release_point()
             return denc.view(B, S, d), None, None, None, None
+        dkv = _take_dkv(dkv_in, kvh, B * S)
         if e2.is_cuda:
             _wgrad(rt, dkv, e2, N, wkv, bkv)
             if rt.wgrad is not None:
                 rt.wgrad.boundary()  # every decoder layer's backward is done
-            denc = _dgrad_ln(dkv, wkv, N, None, ctx.in_link, rt)
+            denc = _dgrad_res(dkv, wkv, N, None)
         else:
             _write_grad(wkv, dkv.t() @ e2, rt)
             _write_grad(bkv, dkv.sum(0), rt)
@@ -912,12 +844,12 @@ class CrossAttnBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(hd)
         ctx.p = (wq, bq, wo, bo, gamma, beta)
         ctx.meta = (heads, scale, site, rt, layer, kvh)
-        ctx.in_link = _claim_ln(rt, x)
         x2 = x.reshape(B * T, d)
-        kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd) \
-            if kv_all.is_contiguous() else None
-        if kv5 is None:
-            raise ValueError("kv_all must be contiguous")
+        kv5 = None  # (kvh.f8b: kv_all is a placeholder, the e4m3 K|V are read)
+        if not kvh.f8b:
+            if not kv_all.is_contiguous():
+                raise ValueError("kv_all must be contiguous")
+            kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
         ctx.lean = lean = x.is_cuda and _attn_lean(rt, B * T, wq, wo, d)
         kx = [] if lean else None
         if x.is_cuda:
@@ -965,7 +897,6 @@ class CrossAttnBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(o.view(B * T, d), wo, bo, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, s.view(B, T, d), gamma, beta, site, rt)
-        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, bo, site)
         ctx.save_for_backward(x2, kv_all, q, o, aux, kv_len)
         return y
 
@@ -979,11 +910,16 @@ class CrossAttnBlockFn(torch.autograd.Function):
         hd = d // heads
         bt = _beta(rt)
         M = B * T
-        if kvh.buf is None:
-            kvh.buf = torch.empty(B * S, kv_all.shape[2], dtype=kv_all.dtype, device=dy.device)
-        dkv_all = kvh.buf.view(B, S, -1)
-        kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
-        g5 = dkv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+        if kvh.f8b:
+            # every layer's d(K|V) goes to kvh.buf8 as e5m2: autograd gets a
+            # zero-stride placeholder of the right shape, no bf16 buffer
+            dkv_all = kv5 = g5 = None
+        else:
+            if kvh.buf is None:
+                kvh.buf = torch.empty(B * S, kv_all.shape[2], dtype=kv_all.dtype, device=dy.device)
+            dkv_all = kvh.buf.view(B, S, -1)
+            kv5 = kv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
+            g5 = dkv_all[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, S, 2, heads, hd)
         if ctx.lean:
             st = rt.fp8
             x8, xs, o8 = ctx.f8a
@@ -992,8 +928,9 @@ class CrossAttnBlockFn(torch.autograd.Function):
             ds8 = ds8.view(M, d)
             gq = st.proj_bwd[id(wq)]
             if _attn_f8_bwd(ctx, T, S, hd):
-                # fp8 attention backward: e5m2 dQ (+ amax, bias sums), bf16
-                # dK / dV into the batched cross K|V gradient
+                # fp8 attention backward: e5m2 dQ (+ amax, bias sums); dK / dV
+                # as e5m2 into kvh.buf8 (kvh.f8b) or bf16 into the batched
+                # cross K|V gradient
                 gdo, gds = st.attn_bwd8[id(wo)]
                 do8 = _fp8_dgrad8(ds8, go, wo, gdo, rt)
                 q8, qs, kv85, kvs = ctx.q8
@@ -1024,7 +961,10 @@ class CrossAttnBlockFn(torch.autograd.Function):
                 _fp8_dgrad_into(dq8, gq, wq, dh.view(M, d), rt, 1.0)
                 rt.wgrad.add_fp8(ds8, st.gmeta.s(go), o8, st.meta.s(os_), wo, bt, rt)
                 rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)
-                dkv_ret = dkv_all if layer == 0 else None
+                dkv_ret = None
+                if layer == 0:
+                    dkv_ret = dkv_all if dkv_all is not None else torch.zeros(
+                        1, dtype=kv_all.dtype, device=dy.device).expand(kv_all.shape)
                 return (dh.view(B, T, d), dkv_ret) + (None,) * 12
             do = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
             _fp8_dgrad_into(ds8, go, wo, do, rt, 0.0)
@@ -1051,7 +991,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             rt.wgrad.add_fp8(dq8, st.gmeta.s(gq), x8, st.meta.s(xs), wq, bt, rt)
             dkv_ret = dkv_all if layer == 0 else None
             return (dh.view(B, T, d), dkv_ret) + (None,) * 12
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt, link=ctx.out_link)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, bo, site, rt)
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:
             _wgrad(rt, ds2, o.view(M, d), d, wo)
@@ -1073,7 +1013,7 @@ class CrossAttnBlockFn(torch.autograd.Function):
             _write_grad(wq, dq.t() @ x2, rt)
             _write_grad(bq, dq.sum(0), rt)
             _ready(rt, wq, bq)  # (GPU: reported by _wgrad / the deferred flush)
-        dx = _dgrad_ln(dq, wq, d, dh, ctx.in_link, rt)
+        dx = _dgrad_res(dq, wq, d, dh)
         # Only layer 0 hands the (by then complete) shared buffer to autograd;
         # the other layers contribute through the side channel, so no adds.
         dkv_ret = dkv_all if layer == 0 else None
@@ -1091,7 +1031,6 @@ class FFNBlockFn(torch.autograd.Function):
         x2 = x.reshape(B * L, d)
         ctx.p = (w1, b1, w2, b2, gamma, beta)
         ctx.meta = (site, rt)
-        ctx.in_link = _claim_ln(rt, x)
         ctx.f8 = None
         ctx.lean = False
         if x.is_cuda and rt.fp8 is not None:
@@ -1124,7 +1063,6 @@ class FFNBlockFn(torch.autograd.Function):
             y, ctx.ln = _proj_ln_fwd(h, w2, b2, x, gamma, beta, site, rt)
         else:
             y, ctx.ln = _ln_fwd(x, f.view(B, L, d), gamma, beta, site, rt)
-        ctx.out_link = _publish_ln(rt, y, ctx.ln, gamma, beta, b2, site)
         ctx.save_for_backward(x2, h if h is not None else x2)  # (lean: h unused)
         return y
 
@@ -1139,8 +1077,7 @@ class FFNBlockFn(torch.autograd.Function):
         f8w = ctx.lean
         bw = rt.fp8.ffn_bwd_slots.get(id(w1)) if (dy.is_cuda and rt.fp8 is not None) else None
         # lean fp8 backward: the LayerNorm backward emits ds directly in e5m2
-        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt, ds8_slot=bw[0] if f8w else None,
-                         link=ctx.out_link)
+        dh, ds = _ln_bwd(dy, ctx.ln, gamma, beta, b2, site, rt, ds8_slot=bw[0] if f8w else None)
         ds2 = ds.reshape(B * L, d)
         if dy.is_cuda:
             if not f8w:
@@ -1190,7 +1127,7 @@ class FFNBlockFn(torch.autograd.Function):
             else:
                 dpre = K.linear_dgrad(ds2, w2.compute, d, relu_aux=h)
             _wgrad(rt, dpre, x2, ff, w1, b1)
-            dx = _dgrad_ln(dpre, w1, ff, dh, ctx.in_link, rt)
+            dx = _dgrad_res(dpre, w1, ff, dh)
             return (dx.view(B, L, d),) + (None,) * 8
         else:
             _write_grad(w2, ds2.t() @ h, rt)

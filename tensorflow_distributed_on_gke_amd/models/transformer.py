@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from tensorflow_distributed_on_gke_amd.models.layers import (_claim_ln, _dgrad_ln, _wgrad,
+from tensorflow_distributed_on_gke_amd.models.layers import (_dgrad_res, _wgrad,
                                                               CrossAttnBlockFn, CrossKVFn, EmbedFn,
                                                               FFNBlockFn, KVGrad, RunCtx,
                                                               SelfAttnBlockFn)
@@ -263,7 +263,6 @@ class Transformer:
 
     def features(self, src, tgt_in, rt: RunCtx, lengths=None):
         src_len, tgt_len = lengths if lengths is not None else (seq_lengths(src), seq_lengths(tgt_in))
-        rt.ln_out = None  # (a link of a previous forward is never claimed by this one)
         enc = self.encode(src, src_len, rt)
         return self.decode(tgt_in, enc, src_len, tgt_len, rt)
 
@@ -320,9 +319,6 @@ class Transformer:
         grad_ctx = torch.enable_grad() if backward else torch.no_grad()
         with grad_ctx:
             dec = self.features(src, tgt_in, rt, lengths)
-        # the decoder's last LayerNorm: its backward may run in the vocabulary
-        # projection's dgrad epilogue (layers.LnLink)
-        dec_link = _claim_ln(rt, dec) if backward else None
         dec2 = dec.detach().reshape(M, cfg.d_model)
         if dev.type == "cuda":
             logits = self.project(dec.detach())
@@ -338,7 +334,7 @@ class Transformer:
             beta = 1.0 if rt.accumulate else 0.0
             dl = logits  # now holds dlogits (pad columns zeroed)
             _wgrad(rt, dl, dec2.contiguous(), cfg.tgt_vocab, self.final.w, self.final.b)
-            ddec = _dgrad_ln(dl, self.final.w, cfg.tgt_vocab, None, dec_link, rt)
+            ddec = _dgrad_res(dl, self.final.w, cfg.tgt_vocab, None)
         else:
             lg = self.project(dec.detach())
             lab = labels.reshape(-1)

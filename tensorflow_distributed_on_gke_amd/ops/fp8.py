@@ -84,8 +84,10 @@ def precision_map() -> Dict[str, str]:
 # the fp8 MFMAs, every key of a (batch, head) in one workgroup (P and dS once)
 ATTN_BWD_F8 = os.environ.get("TDG_ATTN_BWD_F8", "1") != "0"
 _ATTN_BWD_F8_STR = ("e4m3 Q/K/V/P x e5m2 dO/dS on fp8 MFMA (v_mfma_f32_16x16x32 fp8/bf8), f32 "
-                    "softmax from the forward LSE (seq 129-512); e5m2 dQ|dK|dV out (cross-attention "
-                    "dK/dV bf16 into the batched K|V gradient)")
+                    "softmax from the forward LSE (seq 129-512; longer: the bf16 backward below); "
+                    "e5m2 dQ|dK|dV out -- cross-attention dK/dV as e5m2 straight into the batched "
+                    "K|V gradient (its own scale slot) when every decoder layer runs this kernel, "
+                    "else bf16 into it")
 _ATTN_BWD_BF16_STR = "bf16 MFMA on the dequantised e4m3 Q/K/V, bf16 dO (e5m2 dQ|dK|dV out)"
 
 

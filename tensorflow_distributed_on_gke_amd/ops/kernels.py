@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -20,6 +20,7 @@ NUM_CU = 256
 
 # ------------------------------------------------------------------ workspace
 _WS: Dict[Tuple[int, int, str], torch.Tensor] = {}
+_WS_RETIRED: List[torch.Tensor] = []
 
 
 def workspace(name: str, numel: int, device, dtype=torch.float32, zero: bool = False) -> torch.Tensor:
@@ -32,6 +33,11 @@ def workspace(name: str, numel: int, device, dtype=torch.float32, zero: bool = F
     key = (dev.index or 0, sid, name)
     t = _WS.get(key)
     if t is None or t.numel() < numel or t.dtype != dtype:
+        if t is not None:
+            # a captured HIP graph may still address the smaller buffer (the
+            # step cache keeps one graph per batch shape, train/step.py):
+            # never hand its memory to another tensor
+            _WS_RETIRED.append(t)
         t = (torch.zeros if zero else torch.empty)(max(numel, 1), dtype=dtype, device=dev)
         _WS[key] = t
     return t
@@ -39,6 +45,7 @@ def workspace(name: str, numel: int, device, dtype=torch.float32, zero: bool = F
 
 def reset_workspace() -> None:
     _WS.clear()
+    _WS_RETIRED.clear()
 
 
 # ------------------------------------------------------------------ GEMM
@@ -500,109 +507,6 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site, w
             defer.append((ws[i * nb * D:(i + 1) * nb * D], o, nb, D, 1.0 if accumulate else 0.0))
     if ds is None:
         ds = dh
-    return dh, ds
-
-
-# Post-LN block tails fused into the d_model-wide GEMMs (csrc/include/tdg_gemm_ln.h):
-# the forward LayerNorm in the epilogue of the output projection / FFN2, the
-# LayerNorm backward in the epilogue of the dgrad that produces its input
-# gradient -- no separate ln_fwd / ln_bwd launch and no round trip of the
-# pre-LN sum / the LayerNorm input gradient through memory. d_model 512.
-# "0" (default): neither -- measured on MI355X, the fused tails cost more in
-# the GEMM epilogue (band-exchange latency, dropout mask, the second output
-# store, all serialised behind the main loop at 8 waves per CU) than the
-# separate LayerNorm launches they remove: headline step 4.84-4.86 ms
-# unfused vs 4.88-4.90 backward-fused vs 5.06-5.08 both (scripts/ln_fused_lab.py,
-# profiles/r5/ln_fused_ab.txt). "bwd": the backward only; "all": both.
-LN_FUSED = os.environ.get("TDG_LN_FUSED", "0")
-LN_FUSED_D = 512
-# lab only (scripts/ln_fused_lab.py): epilogue parts switched off (tdg_gemm_ln.h)
-LN_ABLATE = int(os.environ.get("TDG_LN_ABLATE", "0"))
-
-
-def _ln_mode() -> str:
-    v = LN_FUSED
-    if v is True or v == "1":
-        return "all"
-    if v is False or v is None:
-        return "0"
-    return str(v)
-
-
-def ln_fused_ok(D: int) -> bool:
-    """The LayerNorm backward of a d_model-D block runs in its consumer's dgrad."""
-    return _ln_mode() in ("bwd", "all") and D == LN_FUSED_D
-
-
-def ln_fused_fwd_ok(D: int) -> bool:
-    """The LayerNorm forward runs in the producing GEMM's epilogue."""
-    return _ln_mode() == "all" and D == LN_FUSED_D
-
-
-def _ln_xch(M: int, device):
-    """Band-exchange state of the fused launches: per-row partial pairs,
-    per-band arrival counters (monotonic, never reset: they must stay at a
-    multiple of 4 between launches, so they are allocated zeroed once and
-    only ever grown by reallocation) and the spin-failure flag."""
-    bands = -(-M // 128)
-    xch = workspace("ln_xch", bands * 128 * 4 * 2, device)
-    dev = torch.device(device)
-    key = (dev.index or 0, "ln_xch_state")
-    st = _WS.get(key)
-    if st is None or st[0].numel() < bands:
-        st = (torch.zeros(max(bands, 256), dtype=torch.int32, device=dev),
-              torch.zeros(1, dtype=torch.int32, device=dev))
-        _WS[key] = st
-    return xch, st[0], st[1]
-
-
-def ln_xch_check() -> None:
-    """Raise if a fused LayerNorm launch ever gave up waiting for a band
-    partner (bounded spin; its outputs were then wrong). Reads device flags: a
-    host sync -- tests and log points only."""
-    for k, v in list(_WS.items()):
-        if isinstance(k, tuple) and len(k) == 2 and k[1] == "ln_xch_state":
-            if int(v[1].item()):
-                raise RuntimeError("fused LayerNorm: a band exchange timed out (outputs invalid)")
-
-
-def linear_ln_fwd(a2, w, bias, x, gamma, beta, p, seed, ctr, site, eps=1e-6, stages=0, kbits=None):
-    """y, h, mean, rstd of y = LN(x + dropout(a2 @ w^T + bias)) in ONE launch
-    (the GEMM's epilogue; bitwise the unfused GEMM's bf16 s, the LayerNorm
-    statistics combined from per-tile partials)."""
-    M = a2.shape[0]
-    D = w.shape[0]
-    y = torch.empty(M, D, dtype=torch.bfloat16, device=a2.device)
-    h = torch.empty_like(y)
-    mean = torch.empty(M, dtype=torch.float32, device=a2.device)
-    rstd = torch.empty_like(mean)
-    xch, bctr, err = _ln_xch(M, a2.device)
-    C().gemm_ln_fwd(a2, w, bias, x.reshape(M, D), gamma, beta, y, h, mean, rstd, p, seed, ctr, site,
-                    eps, kbits, xch, bctr, err, stages, LN_ABLATE)
-    return y, h, mean, rstd
-
-
-def dgrad_ln_bwd(dy2, w, c, h, mean, rstd, gamma, dgamma, dbeta, dbias, p, seed, ctr, site,
-                 defer, accumulate=False, stages=0, kbits=None):
-    """LayerNorm backward fused into the dgrad that produces its input
-    gradient dy = dy2 @ w (+ c, the residual gradient): returns (dh, ds).
-    The dgamma / dbeta / dbias column partials go to a per-site workspace
-    and their folds are appended to `defer` (reduce_partials_multi)."""
-    M = dy2.shape[0]
-    D = w.shape[1]
-    dh = torch.empty(M, D, dtype=torch.bfloat16, device=dy2.device)
-    # ds is its own tensor even without dropout: the caller accumulates the
-    # next dgrad into dh while deferred weight gradients still read ds
-    ds = torch.empty_like(dh)
-    nb = -(-M // 128)
-    part = workspace(f"ln_fbwd_part_{site}", 3 * nb * D, dy2.device)
-    xch, bctr, err = _ln_xch(M, dy2.device)
-    C().gemm_ln_bwd(dy2, w, c.reshape(M, D) if c is not None else None, h.reshape(M, D), mean, rstd,
-                    gamma, dh, ds, part, p, seed, ctr, site, kbits, xch, bctr, err, stages,
-                    LN_ABLATE)
-    b = 1.0 if accumulate else 0.0
-    for i, o in enumerate((dgamma, dbeta, dbias)):
-        defer.append((part[i * nb * D:(i + 1) * nb * D], o, nb, D, b))
     return dh, ds
 
 

@@ -47,13 +47,14 @@ from tensorflow_distributed_on_gke_amd.parallel.dist import PG_TIMEOUT_S
 # Issue the gradient collectives from a host thread (CommThread) instead of
 # making the communication stream wait on the compute stream.
 #   "auto" (default): both issue paths are kept ready; TrainStep.choose_dp_mode
-#          times them on the node the job runs on (segmented HIP graph with the
-#          thread vs with the process group's own stream handoff), checks that
-#          the replicas stay bitwise equal after each (verify_replicas) and keeps
-#          the faster verified one. Without that start-up measurement the
-#          process group's handoff is used -- the thread is never the default
-#          on evidence from another machine (round-4 one-rank A/B: 5.10-5.12 ms
-#          with the thread vs 5.33-5.35 without, profiles/r4/ab_dp_comm_thread.txt).
+#          times them on the node the job runs on (segmented HIP graph and eager
+#          step, each with the thread and with the process group's own stream
+#          handoff), checks that the replicas stay bitwise equal after each
+#          (verify_replicas) and keeps the faster verified one. Where no
+#          start-up measurement runs (uncaptured step, autoselect off) the
+#          thread is used: it won the one-rank RCCL A/B on MI355X (5.10-5.12 ms
+#          vs 5.33-5.35 without, profiles/r4/ab_dp_comm_thread.txt). The
+#          choice and its reason go into the bench record.
 #   "1":   thread on RCCL (no measurement);  "0": never;
 #   "force": thread also over gloo (GPU tensors: the multi-rank rehearsals on
 #          one GPU, tests/test_gpu_dp.py; CPU tensors: tests/test_parallel_cpu.py).
@@ -204,8 +205,8 @@ class DataParallel:
             nccl = store.flat.is_cuda and dist.get_backend(group) == "nccl"
             if nccl or COMM_THREAD == "force":
                 self._comm = CommThread(store.flat.device)
-                if COMM_THREAD in ("1", "force"):
-                    self._thread = self._comm
+                # (auto: on until TrainStep.choose_dp_mode measures otherwise)
+                self._thread = self._comm
         # how the issue path was chosen (introspection / the bench record)
         self.comm_choice = "thread" if self._thread is not None else "pg"
         # collectives issued but not yet waited for (any issue path): a

@@ -34,9 +34,10 @@ import torch
 
 
 class SegmentedGraph:
-    def __init__(self, stream: Optional[torch.cuda.Stream] = None):
+    def __init__(self, stream: Optional[torch.cuda.Stream] = None, pool=None):
         self.stream = stream
-        self.pool = None
+        # (a pool shared with other captured steps: train/step.py's shape cache)
+        self.pool = pool
         self.items: List[Tuple[str, object]] = []
         self._cur: Optional[torch.cuda.CUDAGraph] = None
         self.capturing = False

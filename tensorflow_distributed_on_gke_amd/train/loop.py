@@ -114,9 +114,11 @@ class Trainer:
         if self.tokenizers is not None:
             from tensorflow_distributed_on_gke_amd.data.text import TextPairs
             st, tt = self.tokenizers
+            # (hip_graph: batches padded to length buckets, one captured step each)
+            bucket = s.graph_bucket if s.hip_graph and info.device.type == "cuda" else 1
             self.train_data = TextPairs(s.train_file, st, tt, s.local_batch_size, info.rank, info.world,
                                         seed=s.seed, shuffle_buffer=s.shuffle_buffer, max_len=s.max_len,
-                                        pin=info.device.type == "cuda")
+                                        pin=info.device.type == "cuda", bucket=bucket)
             self.val_data = TextPairs(s.validation_file or s.train_file, st, tt, s.local_batch_size,
                                       info.rank, info.world, seed=s.seed, shuffle=False,
                                       max_len=s.max_len)
@@ -271,10 +273,14 @@ class Trainer:
             for batch in range(steps):
                 src, tgt = self._to_dev(self.train_data.next())
                 epoch_tokens += (src.shape[1] + tgt.shape[1] - 1) * src.shape[0] * info.world
-                if s.hip_graph and s.data == "synthetic" and info.device.type == "cuda" and not captured \
+                if s.hip_graph and info.device.type == "cuda" and not captured \
                         and not self._backward_fault_armed:
                     # capture() restores the state its warm-up steps changed,
-                    # so this batch is still trained exactly once (below)
+                    # so this batch is still trained exactly once (below).
+                    # Text data: every new (bucketed) batch shape is captured
+                    # the same way when it first arrives (TrainStep._select)
+                    self.step_fn.bucketed = s.data == "text"
+                    self.step_fn.graph_cache = s.graph_cache
                     if self.ddp is not None and self.ddp.active:
                         sel = self.step_fn.choose_dp_mode(src, tgt)
                         if info.chief:
@@ -308,6 +314,11 @@ class Trainer:
                     if info.chief:
                         self.log(f"Epoch {epoch + 1} Batch {batch} Loss {float(a[0]) / n:.4f} "
                                  f"Accuracy {float(a[1]) / (n * self._acc_div):.4f}")
+                        if self.step_fn.bucketed and self.step_fn.captured:
+                            gs = self.step_fn.graph_stats
+                            self.log(f"graph cache: {self.step_fn.cached_shapes} batch shapes captured "
+                                     f"(captures {gs['captures']}, evictions {gs['evictions']}, "
+                                     f"replays {gs['replays']})")
                         self.metrics.write(kind="train", epoch=epoch + 1, batch=batch, step=self.global_step,
                                            loss=float(a[0]) / n, accuracy=float(a[1]) / (n * self._acc_div),
                                            **st)

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import time
+from collections import OrderedDict
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -110,6 +111,23 @@ class TrainStep:
         self.graph = None
         self.segments: Optional[SegmentedGraph] = None
         self._static: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+        # Variable-length batches (text data, the reference's padded-to-the-
+        # batch-max shapes: english_portugese_dataset.py:44-46, __main__.py:127
+        # experimental_relax_shapes): with `bucketed` set, a batch of a shape
+        # not captured yet is captured on the spot (warm-up, restore, capture:
+        # it still trains once) and kept in an LRU cache of at most
+        # `graph_cache` captured steps keyed by (source, target) shape. All of
+        # them allocate from ONE memory pool: each replay is a whole step, so
+        # the intermediates of different shapes may share memory (workspaces,
+        # which persist, are never reused: ops.kernels.workspace).
+        self.bucketed = False
+        self.graph_cache = 64
+        self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self._key: Optional[tuple] = None
+        self._pool = None
+        self._cap_stream: Optional[torch.cuda.Stream] = None
+        self._warm_stream: Optional[torch.cuda.Stream] = None
+        self.graph_stats = {"captures": 0, "replays": 0, "evictions": 0}
 
     @property
     def captured(self) -> bool:
@@ -187,6 +205,8 @@ class TrainStep:
         mode = self.capture_mode()
         if mode == "0":
             return False
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
         if (self._static is not None and self._static[0].shape == src.shape
                 and self._static[1].shape == tgt.shape):
             # (choose_dp_mode captures more than one arm: every captured graph
@@ -196,7 +216,12 @@ class TrainStep:
         else:
             self._static = (src.clone(), tgt.clone())
         saved = self.snapshot()
-        s = torch.cuda.Stream()
+        if self._cap_stream is None:
+            # one warm-up and one capture stream for every captured shape: the
+            # workspaces (keyed by stream) are shared by all of them
+            self._warm_stream = torch.cuda.Stream()
+            self._cap_stream = torch.cuda.Stream()
+        s = self._warm_stream
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
@@ -213,9 +238,9 @@ class TrainStep:
             torch.cuda.synchronize()
         if mode == "seg":
             prepare_capture()
-            cap = torch.cuda.Stream()
+            cap = self._cap_stream
             cap.wait_stream(torch.cuda.current_stream())
-            rec = SegmentedGraph(cap)
+            rec = SegmentedGraph(cap, pool=self._pool)
             self.ddp.recorder = rec
             try:
                 with torch.cuda.stream(cap):
@@ -229,12 +254,53 @@ class TrainStep:
                 self.ddp.recorder = None
             torch.cuda.current_stream().wait_stream(cap)
             self.segments = rec
+            self._register()
             return True
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, pool=self._pool, stream=self._cap_stream):
             self.eager(*self._static)
         self.graph = g
+        self._register()
         return True
+
+    # ------------------------------------------------------------------ shape cache
+    def _register(self) -> None:
+        """The just-captured step becomes the cache entry of its shape."""
+        self._key = (tuple(self._static[0].shape), tuple(self._static[1].shape))
+        self._graphs[self._key] = (self.graph, self.segments, self._static)
+        self._graphs.move_to_end(self._key)
+        self.graph_stats["captures"] += 1
+
+    @property
+    def cached_shapes(self) -> int:
+        return len(self._graphs)
+
+    def _select(self, src: torch.Tensor, tgt: torch.Tensor) -> None:
+        """Make the captured step of this batch shape current: a cache hit,
+        or (bucketed) a capture of the new shape, evicting the least recently
+        used one when the cache is full. Every rank sees the same global-batch
+        shapes in the same order, so every rank captures and evicts alike."""
+        key = (tuple(src.shape), tuple(tgt.shape))
+        if key == self._key:
+            return
+        ent = self._graphs.get(key)
+        if ent is not None:
+            self._graphs.move_to_end(key)
+            self.graph, self.segments, self._static = ent
+            self._key = key
+            return
+        if not self.bucketed:
+            raise ValueError(f"captured step takes {tuple(self._static[0].shape)} / "
+                             f"{tuple(self._static[1].shape)} batches, got {tuple(src.shape)} / "
+                             f"{tuple(tgt.shape)}")
+        while len(self._graphs) >= max(1, self.graph_cache):
+            self._graphs.popitem(last=False)
+            self.graph_stats["evictions"] += 1
+        self.graph = self.segments = None
+        self._static = None
+        self._key = None
+        if not self.capture(src, tgt, warmup=1):
+            raise RuntimeError("bucketed step: capture of a new batch shape failed")
 
     def choose_dp_mode(self, src: torch.Tensor, tgt: torch.Tensor, steps: int = 8,
                        rounds: int = 3, margin: float = 0.03) -> Dict[str, object]:
@@ -242,9 +308,9 @@ class TrainStep:
 
         Arms: the segmented graph (collectives issued between graph segments)
         and the eager step; and, where a comm thread exists
-        (ddp.COMM_THREAD "auto"), the segmented graph once more with the
-        collectives issued by the host comm thread instead of the process
-        group's own stream handoff. Each arm is timed in interleaved rounds
+        (ddp.COMM_THREAD "auto"), both once more with the collectives issued
+        by the host comm thread instead of the process group's own stream
+        handoff. Each arm is timed in interleaved rounds
         (median per arm, MAX over ranks, so every rank takes the same
         decision) and, after its timed steps, the replicas must be bitwise
         equal (DataParallel.verify_replicas raises otherwise: an issue path
@@ -252,17 +318,32 @@ class TrainStep:
         segmented graph wins when the host is the bottleneck (eight ranks
         sharing a node's CPUs); the eager step when the host keeps ahead. The
         training state is restored afterwards, so this trains nothing.
-        Returns {"mode": "seg" | "0", "comm_thread": bool, "<arm>_ms": ..}."""
+        Without a measurement (the step is not captured, DP_AUTOSELECT off)
+        an available comm thread is used. Returns {"mode": "seg" | "0",
+        "comm_thread": bool, "reason": "measured" | "unmeasured",
+        "<arm>_ms": .., "select_s": seconds this selection took}."""
         ddp = self.ddp
+        t_start = time.perf_counter()
         auto_thread = (ddp is not None and ddp.active and ddp.can_thread
                        and _ddp_mod.COMM_THREAD == "auto")
         if auto_thread:
             ddp.use_thread(False)
+
+        def unmeasured(mode: str) -> Dict[str, object]:
+            # no start-up measurement: with a comm thread available ("auto")
+            # the thread issues the collectives -- it won the one-rank RCCL A/B
+            # on MI355X for the eager and the segmented step alike (5.11 vs
+            # 5.34 ms, profiles/r4/ab_dp_comm_thread.txt)
+            if auto_thread:
+                ddp.use_thread(True)
+            th = ddp is not None and ddp._thread is not None
+            return {"mode": mode, "comm_thread": th, "reason": "unmeasured",
+                    "select_s": round(time.perf_counter() - t_start, 3)}
+
         if not self.capture(src, tgt):
-            return {"mode": self.capture_mode(), "comm_thread": ddp is not None and ddp._thread is not None}
+            return unmeasured(self.capture_mode())
         if not (ddp is not None and ddp.active and self.segments is not None) or not DP_AUTOSELECT:
-            return {"mode": "seg" if self.segments is not None else self.capture_mode(),
-                    "comm_thread": ddp is not None and ddp._thread is not None}
+            return unmeasured("seg" if self.segments is not None else self.capture_mode())
         arms = {"seg": (self.segments, ddp._thread is not None)}
         if auto_thread:
             self.segments = None
@@ -295,13 +376,17 @@ class TrainStep:
                 self(src, tgt)
             return run, th
 
-        names = list(arms) + ["0"]
+        # eager arms: the process group's handoff, and (auto) the comm thread
+        eager_arms = {"0": False}
+        if auto_thread:
+            eager_arms["0_thread"] = True
+        names = list(arms) + list(eager_arms)
         runs = {k: [] for k in names}
         for _ in range(rounds):
             for k in names:
-                if k == "0":
+                if k in eager_arms:
                     self.segments = None
-                    ddp.use_thread(False)
+                    ddp.use_thread(eager_arms[k])
                     runs[k].append(timed(lambda: self.eager(src, tgt)))
                 else:
                     run, th = seg_run(k)
@@ -315,29 +400,36 @@ class TrainStep:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ddp.group)
         ms = {k: float(v) for k, v in zip(names, t.tolist())}
         self.restore(saved)
-        best_seg = min((k for k in names if k != "0"), key=lambda k: ms[k])
-        if ms["0"] < ms[best_seg] * (1.0 - margin):
+        best_seg = min((k for k in names if k not in eager_arms), key=lambda k: ms[k])
+        best_eager = min(eager_arms, key=lambda k: ms[k])
+        if ms[best_eager] < ms[best_seg] * (1.0 - margin):
             self.segments = None
             self._static = None
-            ddp.use_thread(False)
-            mode, th = "0", False
+            th = eager_arms[best_eager]
+            ddp.use_thread(th)
+            mode = "0"
         else:
             self.segments, th = arms[best_seg]
             ddp.use_thread(th)
             mode = "seg"
-        arms.clear()  # the other captures' graphs and pools are released
+        arms.clear()  # the other captures' graphs are released
+        self._graphs.clear()
+        self._key = None
+        if self.segments is not None:
+            self._register()
         torch.cuda.synchronize()
-        out = {"mode": mode, "comm_thread": th}
-        out.update({f"{'eager' if k == '0' else k}_ms": round(v * 1e3, 3) for k, v in ms.items()})
+        out = {"mode": mode, "comm_thread": th, "reason": "measured"}
+        out.update({f"{k.replace('0', 'eager', 1) if k.startswith('0') else k}_ms": round(v * 1e3, 3)
+                    for k, v in ms.items()})
+        out["select_s"] = round(time.perf_counter() - t_start, 3)
         return out
 
     def __call__(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         if not self.captured:
             return self.eager(src, tgt)
         if src.shape != self._static[0].shape or tgt.shape != self._static[1].shape:
-            raise ValueError(f"captured step takes {tuple(self._static[0].shape)} / "
-                             f"{tuple(self._static[1].shape)} batches, got {tuple(src.shape)} / "
-                             f"{tuple(tgt.shape)}")
+            self._select(src, tgt)
+        self.graph_stats["replays"] += 1
         self._static[0].copy_(src, non_blocking=True)
         self._static[1].copy_(tgt, non_blocking=True)
         if self.segments is not None:

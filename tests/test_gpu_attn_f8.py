@@ -139,3 +139,61 @@ def test_attn_bwd_f8_only_e5m2_dq_bf16_dkdv():
     assert torch.equal(dk, dk2) and torch.equal(dv, dv2)
     assert torch.equal(dq8.view(torch.uint8), dq82.view(torch.uint8))
     assert torch.allclose(part, dq.float().sum(1).reshape(B, -1), rtol=1e-4, atol=1e-5)
+
+
+def test_attn_bwd_f8_cross_kv_own_slot_and_column_sums():
+    """The form the fp8 step runs for cross-attention by default (KVGrad.f8b):
+    e5m2 dQ in the Q-projection gradient slot (sg8 / amaxg8, column sums at
+    cs_q of cs_part) and e5m2 dK / dV written straight into a layer's slice of
+    the batched cross K|V gradient [B, Lk, layers * 2d] in that projection's
+    own slot (sgkv8 / amaxgkv8, a different scale), their column sums at the
+    layer's offsets cs_k / cs_v of the wider cs_part2. Every output is checked
+    against the bf16 gradients of the same call."""
+    B, H, hd, Lq, Lk = 2, 3, 64, 300, 400
+    d = H * hd
+    layers, layer = 3, 1
+    NKV = layers * 2 * d
+    (kk, meta, gmeta, slots, x8, deq, kv_len, scale, o, lse, gs, do8,
+     _) = _setup(B, H, Lq, Lk, False, 9, True)
+    ido, ids, ig = gs
+    ikv = gmeta.slot("gkv")
+    gmeta.scale[ig] = 2.0 ** 10
+    gmeta.scale[ikv] = 2.0 ** 13  # != sg8: a wrong slot shows in every byte
+    dq = torch.empty(B, Lq, H, hd, dtype=torch.bfloat16, device=DEV)
+    # (the bf16 and e5m2 outputs share strides: both batched [B, Lk, NKV])
+    bufb = torch.zeros(B, Lk, NKV, dtype=torch.bfloat16, device=DEV)
+    gb5 = bufb[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, Lk, 2, H, hd)
+    dk, dv = gb5[:, :, 0], gb5[:, :, 1]
+    dq8 = torch.empty(B, Lq, H, hd, dtype=torch.float8_e5m2, device=DEV)
+    buf8 = torch.zeros(B, Lk, NKV, dtype=torch.float8_e5m2, device=DEV)
+    g85 = buf8[:, :, layer * 2 * d:(layer + 1) * 2 * d].view(B, Lk, 2, H, hd)
+    part = torch.full((B, d), float("nan"), device=DEV)
+    part2 = torch.full((B, NKV), float("nan"), device=DEV)
+    n = kk.attn_bwd_f8(x8[0], x8[1], x8[2], meta.s(slots[0]), meta.s(slots[1]), meta.s(slots[2]),
+                       o, do8, gmeta.s(ido), lse, kv_len, scale, False, gmeta.s(ids), gmeta.a(ids),
+                       dq=dq, dk=dk, dv=dv, dq8=dq8, dk8=g85[:, :, 0], dv8=g85[:, :, 1],
+                       sg8=gmeta.s(ig), amaxg8=gmeta.a(ig), cs_part=part, cs_ld=d, cs_q=0,
+                       sgkv8=gmeta.s(ikv), amaxgkv8=gmeta.a(ikv), cs_part2=part2, cs_ld2=NKV,
+                       cs_k=layer * 2 * d, cs_v=layer * 2 * d + d)
+    assert n == B
+    torch.cuda.synchronize()
+
+    def e5(x, s):
+        return (x.float() * s).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+
+    assert torch.equal(dq8.view(torch.uint8), e5(dq, 2.0 ** 10))
+    assert torch.equal(g85[:, :, 0].contiguous().view(torch.uint8), e5(dk, 2.0 ** 13))
+    assert torch.equal(g85[:, :, 1].contiguous().view(torch.uint8), e5(dv, 2.0 ** 13))
+    # the other layers' slices of the batched buffer are untouched
+    other = torch.cat([buf8[:, :, :layer * 2 * d], buf8[:, :, (layer + 1) * 2 * d:]], -1)
+    assert int(other.view(torch.uint8).count_nonzero()) == 0
+    # separate amax slots
+    am = gmeta.amax_values()
+    assert am[ig].item() == pytest.approx(dq.float().abs().max().item(), rel=1e-6)
+    assert am[ikv].item() == pytest.approx(max(dk.float().abs().max().item(),
+                                               dv.float().abs().max().item()), rel=1e-6)
+    # column sums: dQ's in cs_part, dK / dV's at the layer's offsets of cs_part2
+    assert torch.allclose(part, dq.float().sum(1).reshape(B, d), rtol=1e-4, atol=1e-5)
+    for off, g in ((layer * 2 * d, dk), (layer * 2 * d + d, dv)):
+        want = g.float().sum(1).reshape(B, d)
+        assert torch.allclose(part2[:, off:off + d], want, rtol=1e-4, atol=1e-4 * want.abs().max().item())

@@ -122,7 +122,8 @@ def _dp_worker(rank, port, out, mode):
         assert st.selected["seg_ms"] > 0 and st.selected["eager_ms"] > 0
         # RCCL (one rank): the host comm-thread arm is measured (and its
         # replicas verified) too, and the choice is recorded
-        assert st.selected["seg_thread_ms"] > 0, st.selected
+        assert st.selected["seg_thread_ms"] > 0 and st.selected["eager_thread_ms"] > 0, st.selected
+        assert st.selected["reason"] == "measured" and st.selected["select_s"] > 0
         assert st.selected["comm_thread"] == (st.ddp._thread is not None)
         res[name] = (f, l)
     torch.save({"ef": res["eager"][0], "el": res["eager"][1], "gf": res["graph"][0], "gl": res["graph"][1],

@@ -138,3 +138,30 @@ def test_train_cli_on_text_data_two_ranks(tmp_path):
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
     assert t.returncode == 0, t.stdout + t.stderr
     assert "'o gato é grande .' ->" in t.stdout and "attention maps" in t.stdout
+
+
+def test_bucketed_batches_pad_to_length_buckets(tmp_path):
+    """bucket > 1 (hip_graph text runs): every batch is padded further, the
+    source to a multiple of the bucket and the target so that the decoder
+    input (target minus the shifted token) is one, never past max_len, and
+    the extra columns are PAD only (the rows are the unbucketed ones)."""
+    from tensorflow_distributed_on_gke_amd.data.text import bucket_lengths
+    assert bucket_lengths(5, 9, 1, 1000) == (5, 9)
+    assert bucket_lengths(5, 9, 32, 1000) == (32, 33)
+    assert bucket_lengths(32, 33, 32, 1000) == (32, 33)
+    assert bucket_lengths(33, 34, 32, 1000) == (64, 65)
+    assert bucket_lengths(990, 1000, 32, 1000) == (992, 1000)  # capped at max_len
+    assert bucket_lengths(999, 990, 32, 1000) == (1000, 993)
+    p = _corpus(tmp_path / "c.tsv")
+    tok_s = WordPieceTokenizer.train((s for s, _ in read_pairs(str(p))), vocab_size=200)
+    tok_t = WordPieceTokenizer.train((t for _, t in read_pairs(str(p))), vocab_size=200)
+    plain = TextPairs(str(p), tok_s, tok_t, local_batch=8, seed=1)
+    bk = TextPairs(str(p), tok_s, tok_t, local_batch=8, seed=1, bucket=16)
+    shapes = set()
+    for i in range(plain.steps_per_epoch):
+        (s0, t0), (s1, t1) = plain.batch(i), bk.batch(i)
+        assert s1.shape[1] % 16 == 0 and (t1.shape[1] - 1) % 16 == 0
+        assert torch.equal(s1[:, :s0.shape[1]], s0) and bool((s1[:, s0.shape[1]:] == PAD).all())
+        assert torch.equal(t1[:, :t0.shape[1]], t0) and bool((t1[:, t0.shape[1]:] == PAD).all())
+        shapes.add((tuple(s1.shape), tuple(t1.shape)))
+    assert len(shapes) < plain.steps_per_epoch
