@@ -300,7 +300,16 @@ struct R256Args {
   int ncls;
 };
 
-template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+// DEEP: every half-tile slot is refilled with the K-tile TWO steps ahead as
+// soon as the phase after its last read has passed its barrier (A-half0 /
+// B-half0 in phase 1, B-half1 in phase 2, A-half1 in phase 0 of the next
+// step), instead of with the next K-tile one whole step later: the same
+// 128 KiB of LDS keep 5-7 half-tiles (80-112 KiB) in flight instead of
+// 2-4, and each half is issued 6-7 phases before its use instead of 3-4.
+// Counted waits (per wave, 2 LDS-DMA instructions per half; issue order A1 of
+// kt+1 | A0 B0 of kt+2 | B1 of kt+2 per step):
+//   steady (kt+2 exists) 10 / 10 / 12, kt+1 last 10 / 10 / 8, last 4 / 2 / 0.
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, bool DEEP>
 __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
                                                       const float* __restrict__ bias,
                                                       const bf16_t* __restrict__ aux, int K,
@@ -360,47 +369,60 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
   //   A-half hA: (x / 64) * 128 + hA * 64 + x % 64
   //   B-half hB: (x / 32) * 64 + hB * 32 + x % 32
   // (KC images remap rows, MC images remap 8-element column chunks.)
-  int a_mn[2][2], b_mn[2][2], a_k[2], b_k[2];
+  // LDS-DMA through buffer resources: per lane and piece of every half-tile a
+  // byte offset fixed for the whole K loop (VGPR), per K-tile one scalar
+  // offset (k0 * 2 K-contiguous, k0 * ld * 2 MN-contiguous) -- no per-lane
+  // 64-bit address is ever formed (as global_load_lds addresses, the
+  // compiler strength-reduced them into eight loop-carried 64-bit pointers
+  // and spilled). launch_256 checks every extent is below 2^31 bytes. Rows /
+  // columns past the operand are clamped (KC: the last row, MC: column 0;
+  // never stored).
+  uint32_t a_off[2][2], b_off[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int xa = A_KC ? ga.row[i] : ga.col[i];
     const int xb = B_KC ? gb.row[i] : gb.col[i];
-    a_k[i] = A_KC ? ga.col[i] : ga.row[i];
-    b_k[i] = B_KC ? gb.col[i] : gb.row[i];
+    const int ka = A_KC ? ga.col[i] : ga.row[i];
+    const int kb = B_KC ? gb.col[i] : gb.row[i];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      a_mn[hh][i] = (xa >> 6) * 128 + hh * 64 + (xa & 63);
-      b_mn[hh][i] = (xb >> 5) * 64 + hh * 32 + (xb & 31);
+      int ma = m0 + (xa >> 6) * 128 + hh * 64 + (xa & 63);
+      int nb = n0 + (xb >> 5) * 64 + hh * 32 + (xb & 31);
+      if (A_KC) {
+        ma = ma < M ? ma : M - 1;
+        a_off[hh][i] = 2u * (uint32_t)(ma * lda + ka);
+      } else {
+        ma = ma < M ? ma : 0;
+        a_off[hh][i] = 2u * (uint32_t)(ka * lda + ma);
+      }
+      if (B_KC) {
+        nb = nb < N ? nb : N - 1;
+        b_off[hh][i] = 2u * (uint32_t)(nb * ldb + kb);
+      } else {
+        nb = nb < N ? nb : 0;
+        b_off[hh][i] = 2u * (uint32_t)(kb * ldb + nb);
+      }
     }
   }
-  auto issue = [&](auto kc, const bf16_t* X, int ld, int len, int base, const int* mns,
-                   const int* ks, int k0, char* dst) {
+  const int nrec_a = 2 * (A_KC ? (M - 1) * lda + K : (K - 1) * lda + M);
+  const int nrec_b = 2 * (B_KC ? (N - 1) * ldb + K : (K - 1) * ldb + N);
+  const uint32_t kstep_a = A_KC ? BK * 2u : (uint32_t)BK * (uint32_t)lda * 2u;
+  const uint32_t kstep_b = B_KC ? BK * 2u : (uint32_t)BK * (uint32_t)ldb * 2u;
+  auto issue = [&](const bf16_t* X, int nrec, const uint32_t* offs, uint32_t soff, char* dst) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int mn = base + mns[i];
-      long long off;
-      if constexpr (decltype(kc)::value) {
-        mn = mn < len ? mn : len - 1;
-        off = (long long)mn * ld + k0 + ks[i];
-      } else {
-        mn = mn < len ? mn : 0;  // never stored
-        off = (long long)(k0 + ks[i]) * ld + mn;
-      }
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(X + off),
-          (__attribute__((address_space(3))) void*)(dst + (wid * 2 + i) * 1024), 16, 0, 0);
-    }
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), (short)0, nrec, 0x00020000),
+          (__attribute__((address_space(3))) void*)(dst + (wid * 2 + i) * 1024), 16, offs[i],
+          (int)soff, 0, 0);
   };
-  using AKC = std::integral_constant<bool, A_KC>;
-  using BKC = std::integral_constant<bool, B_KC>;
   // half h of K-tile kt: 0 = A-half0, 1 = B-half0, 2 = B-half1, 3 = A-half1
   auto issue_half = [&](int kt, int h) {
     char* st = smem + (kt & 1) * SB;
-    const int k0 = kt * BK;
-    if (h == 0) issue(AKC{}, A, lda, M, m0, a_mn[0], a_k, k0, st + 0 * HB);
-    else if (h == 1) issue(BKC{}, B, ldb, N, n0, b_mn[0], b_k, k0, st + 2 * HB);
-    else if (h == 2) issue(BKC{}, B, ldb, N, n0, b_mn[1], b_k, k0, st + 3 * HB);
-    else issue(AKC{}, A, lda, M, m0, a_mn[1], a_k, k0, st + 1 * HB);
+    if (h == 0) issue(A, nrec_a, a_off[0], kstep_a * (uint32_t)kt, st + 0 * HB);
+    else if (h == 1) issue(B, nrec_b, b_off[0], kstep_b * (uint32_t)kt, st + 2 * HB);
+    else if (h == 2) issue(B, nrec_b, b_off[1], kstep_b * (uint32_t)kt, st + 3 * HB);
+    else issue(A, nrec_a, a_off[1], kstep_a * (uint32_t)kt, st + 1 * HB);
   };
 
   f32x4 acc[8][4];
@@ -431,6 +453,93 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     if (ph == 0) bsum0 = bs;
     else bsum1 = bs;
   };
+  if constexpr (DEEP) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue_half(0, h);
+    if (nk > 1) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) issue_half(1, h);
+    }
+    // MODE 3: K-tiles kt+1 and kt+2 exist; 2: kt+1 is the last; 1: kt is
+    auto kstep_deep = [&](int kt, auto modec) {
+      constexpr int MODE = decltype(modec)::value;
+      const char* st = smem + (kt & 1) * SB;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        if (ph < 3) {
+          if (ph == 0) wait_vmcnt<MODE == 1 ? 4 : 10>();
+          else if (ph == 1) wait_vmcnt<MODE == 1 ? 2 : 10>();
+          else wait_vmcnt<MODE == 3 ? 12 : (MODE == 2 ? 8 : 0)>();
+          lds_barrier();
+          if (kt == 0 && ph == 0) TDG_STAMP(1);
+        }
+        if (ph == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<A_KC, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<B_KC, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
+        } else if (ph == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<B_KC, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
+        } else if (ph == 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
+        }
+        // refills: the slot read in the previous phase (every wave's reads of
+        // it completed before this phase's barrier) takes K-tile kt + 2
+        if constexpr (MODE >= 2) {
+          if (ph == 0) issue_half(kt + 1, 3);
+        }
+        if constexpr (MODE == 3) {
+          if (ph == 1) {
+            issue_half(kt + 2, 0);
+            issue_half(kt + 2, 1);
+          } else if (ph == 2) {
+            issue_half(kt + 2, 2);
+          }
+        }
+        if (ph < 3) {
+          lgkm_wait<0>();
+          if (ph == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tie_all(fa[i]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) tie_all(fb[j]);
+          } else if (ph == 1) {
+#pragma unroll
+            for (int j = 2; j < 4; ++j) tie_all(fb[j]);
+          } else {
+#pragma unroll
+            for (int i = 4; i < 8; ++i) tie_all(fa[i]);
+          }
+        }
+        const int i0 = (ph < 2) ? 0 : 4;
+        const int j0 = (ph == 0 || ph == 3) ? 0 : 2;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i0 + i][j0 + j] = mfma16(fb[j0 + j][s2], fa[i0 + i][s2], acc[i0 + i][j0 + j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (do_bsum && (ph == 0 || ph == 2)) bias_sum(ph);
+      }
+    };
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) kstep_deep(kt, std::integral_constant<int, 3>{});
+    if (kt + 1 < nk) kstep_deep(kt++, std::integral_constant<int, 2>{});
+    kstep_deep(kt, std::integral_constant<int, 1>{});
+  } else {
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue_half(0, h);
   // MORE: K-tile kt + 1 exists (steady state, branch-free); the last tile is
@@ -504,6 +613,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
   int kt = 0;
   for (; kt + 1 < nk; ++kt) kstep(kt, std::true_type{});
   kstep(kt, std::false_type{});
+  }
   if (do_bsum) {  // lanes l, l+16, l+32, l+48 hold disjoint K subsets of row l&15
     bsum0 += __shfl_xor(bsum0, 16, 64);
     bsum0 += __shfl_xor(bsum0, 32, 64);
@@ -729,6 +839,28 @@ constexpr bool has_256() {
   return false;
 }
 
+// gemm256_kernel addresses its operands through buffer resources (32-bit
+// byte offsets): every class's operand extents must stay below 2^31 bytes
+inline bool r256_offsets_ok(const R256Args& a, bool akc, bool bkc, int K) {
+  for (int c = 0; c < a.ncls; ++c) {
+    const R256Class& k = a.cls[c];
+    const long long ea = akc ? (long long)(k.M - 1) * k.lda + K : (long long)(K - 1) * k.lda + k.M;
+    const long long eb = bkc ? (long long)(k.N - 1) * k.ldb + K : (long long)(K - 1) * k.ldb + k.N;
+    if (ea * 2 >= 0x7fffffffLL || eb * 2 >= 0x7fffffffLL) return false;
+  }
+  return true;
+}
+
+// 256x256 main loop refilling half-tile slots two K-tiles ahead
+// (gemm256_kernel DEEP); TDG_G256_DEEP=0 selects the one-step-ahead refill
+inline bool g256_deep() {
+  static const bool v = [] {
+    const char* e = std::getenv("TDG_G256_DEEP");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 template <bool AK, bool BKc, int EPI, bool F32>
 int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t* aux, int K,
                int ldaux, float alpha, float beta, hipStream_t st) {
@@ -736,15 +868,22 @@ int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t*
     return -4;
   } else {
     if (K % BK != 0 || tiles <= 0) return -3;
+    if (!r256_offsets_ok(args, AK, BKc, K)) return -9;
     constexpr int lds = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32>,
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds, st, args,
-                       bias, aux, K, ldaux, alpha, beta);
+    if (g256_deep())
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, true>), dim3(tiles), dim3(512), lds, st,
+                         args, bias, aux, K, ldaux, alpha, beta);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, false>), dim3(tiles), dim3(512), lds, st,
+                         args, bias, aux, K, ldaux, alpha, beta);
     return 0;
   }
 }
