@@ -300,16 +300,21 @@ struct R256Args {
   int ncls;
 };
 
-// DEEP: every half-tile slot is refilled with the K-tile TWO steps ahead as
-// soon as the phase after its last read has passed its barrier (A-half0 /
-// B-half0 in phase 1, B-half1 in phase 2, A-half1 in phase 0 of the next
-// step), instead of with the next K-tile one whole step later: the same
-// 128 KiB of LDS keep 5-7 half-tiles (80-112 KiB) in flight instead of
-// 2-4, and each half is issued 6-7 phases before its use instead of 3-4.
-// Counted waits (per wave, 2 LDS-DMA instructions per half; issue order A1 of
-// kt+1 | A0 B0 of kt+2 | B1 of kt+2 per step):
+// Main-loop refill: every half-tile slot is refilled with the K-tile TWO
+// steps ahead as soon as the phase after its last read has passed its
+// barrier (A-half0 / B-half0 in phase 1, B-half1 in phase 2, A-half1 in
+// phase 0 of the next step), not with the next K-tile one whole step later:
+// the same 128 KiB of LDS keep 5-7 half-tiles (80-112 KiB) in flight instead
+// of 2-4, each half issued 6-7 phases before its use instead of 3-4 (round 6:
+// weight-gradient L2 hit rate 54 -> 65 %, profiles/r6/). Counted waits (per
+// wave, 2 LDS-DMA instructions per half; issue order A1 of kt+1 | A0 B0 of
+// kt+2 | B1 of kt+2 per step):
 //   steady (kt+2 exists) 10 / 10 / 12, kt+1 last 10 / 10 / 8, last 4 / 2 / 0.
-template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, bool DEEP>
+// (Measured and not kept, docs/PERF.md "Round 6": reading each phase's
+// fragments behind the previous phase's MFMAs -- equal on the NT forwards,
+// and with MN-contiguous operands, whose fragments are two transposing reads
+// joined into one register quad, it spills inside the loop.)
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
                                                       const float* __restrict__ bias,
                                                       const bf16_t* __restrict__ aux, int K,
@@ -453,7 +458,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     if (ph == 0) bsum0 = bs;
     else bsum1 = bs;
   };
-  if constexpr (DEEP) {
+  {
 #pragma unroll
     for (int h = 0; h < 4; ++h) issue_half(0, h);
     if (nk > 1) {
@@ -539,80 +544,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
     for (; kt + 2 < nk; ++kt) kstep_deep(kt, std::integral_constant<int, 3>{});
     if (kt + 1 < nk) kstep_deep(kt++, std::integral_constant<int, 2>{});
     kstep_deep(kt, std::integral_constant<int, 1>{});
-  } else {
-#pragma unroll
-  for (int h = 0; h < 4; ++h) issue_half(0, h);
-  // MORE: K-tile kt + 1 exists (steady state, branch-free); the last tile is
-  // its own instantiation (tail branches inside one loop body invite the
-  // compiler to move MFMAs out of their phases: docs/PERF.md "Round 4")
-  auto kstep = [&](int kt, auto morec) {
-    constexpr bool more = decltype(morec)::value;
-    const char* st = smem + (kt & 1) * SB;
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      if (ph < 3) {
-        if constexpr (more) wait_vmcnt<4>();
-        else wait_vmcnt<0>();
-        lds_barrier();
-        if (kt == 0 && ph == 0) TDG_STAMP(1);
-      }
-      if (ph == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<A_KC, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<B_KC, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
-      } else if (ph == 1) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<B_KC, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
-      } else if (ph == 2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
-      }
-      if constexpr (more) issue_half(kt + 1, ph);
-      // this phase's fragment reads (untracked transposing reads included)
-      if (ph < 3) {
-        lgkm_wait<0>();
-        if (ph == 0) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) tie_all(fa[i]);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) tie_all(fb[j]);
-        } else if (ph == 1) {
-#pragma unroll
-          for (int j = 2; j < 4; ++j) tie_all(fb[j]);
-        } else {
-#pragma unroll
-          for (int i = 4; i < 8; ++i) tie_all(fa[i]);
-        }
-      }
-      const int i0 = (ph < 2) ? 0 : 4;
-      const int j0 = (ph == 0 || ph == 3) ? 0 : 2;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i0 + i][j0 + j] = mfma16(fb[j0 + j][s2], fa[i0 + i][s2], acc[i0 + i][j0 + j]);
-      __builtin_amdgcn_s_setprio(0);
-      // bias-gradient row sums: constant fragment indices only (a
-      // wave-uniform branch per candidate): a runtime index would move fa[]
-      // to scratch
-      if (do_bsum && (ph == 0 || ph == 2)) bias_sum(ph);
-    }
-  };
-  int kt = 0;
-  for (; kt + 1 < nk; ++kt) kstep(kt, std::true_type{});
-  kstep(kt, std::false_type{});
   }
   if (do_bsum) {  // lanes l, l+16, l+32, l+48 hold disjoint K subsets of row l&15
     bsum0 += __shfl_xor(bsum0, 16, 64);
@@ -851,16 +782,6 @@ inline bool r256_offsets_ok(const R256Args& a, bool akc, bool bkc, int K) {
   return true;
 }
 
-// 256x256 main loop refilling half-tile slots two K-tiles ahead
-// (gemm256_kernel DEEP); TDG_G256_DEEP=0 selects the one-step-ahead refill
-inline bool g256_deep() {
-  static const bool v = [] {
-    const char* e = std::getenv("TDG_G256_DEEP");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
 template <bool AK, bool BKc, int EPI, bool F32>
 int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t* aux, int K,
                int ldaux, float alpha, float beta, hipStream_t st) {
@@ -872,18 +793,12 @@ int launch_256(const R256Args& args, int tiles, const float* bias, const bf16_t*
     constexpr int lds = 2 * 4 * 128 * BK * 2;  // 128 KiB: 2 stages x 4 half-tiles
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32, true>,
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKc, EPI, F32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    if (g256_deep())
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, true>), dim3(tiles), dim3(512), lds, st,
-                         args, bias, aux, K, ldaux, alpha, beta);
-    else
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32, false>), dim3(tiles), dim3(512), lds, st,
-                         args, bias, aux, K, ldaux, alpha, beta);
+    hipLaunchKernelGGL((gemm256_kernel<AK, BKc, EPI, F32>), dim3(tiles), dim3(512), lds, st, args,
+                       bias, aux, K, ldaux, alpha, beta);
     return 0;
   }
 }

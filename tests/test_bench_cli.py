@@ -108,8 +108,9 @@ def test_visible_gpus_does_not_initialise_hip(monkeypatch):
 
 def test_fp8_precision_record_lists_every_op():
     """bench.py's dtype field for --dtype fp8 says exactly what runs in which
-    format (the output projection and the weight gradients are fp8, the
-    attention backward is not)."""
+    format: the output projection, the dgrads and the weight gradients are
+    fp8, the attention backward is the fp8-MFMA kernel up to 512 keys (the
+    bf16 backward with e5m2 outputs beyond), the vocabulary projection bf16."""
     from tensorflow_distributed_on_gke_amd.ops import fp8
 
     m = fp8.precision_map()
@@ -119,6 +120,7 @@ def test_fp8_precision_record_lists_every_op():
     assert m["attention_projection_weight_gradients"].startswith("e5m2")
     assert m["attention_projection_dgrads"].startswith("e5m2")
     assert m["attention_backward"] == fp8.ATTN_BWD_PRECISION
+    assert "512" in m["attention_backward"] and "e5m2" in m["attention_backward"]
     assert "attention_backward=" + fp8.ATTN_BWD_PRECISION in s
     assert m["vocab_projection"].startswith("bf16")
     src = open(os.path.join(ROOT, "bench.py")).read()
