@@ -15,7 +15,10 @@ export TDG_NO_AUTOBUILD=1
 TICK=$!
 trap "kill $TICK 2>/dev/null" EXIT
 echo "== 8 gloo ranks, Transformer-base"
-TDG_DIST_BACKEND=gloo timeout -k 10 900 python -u bench.py --gpus 8 --steps 6 --warmup 2 --verify-replicas 1 \
+# one hardware queue per rank: eight processes x the default 4 queues
+# oversubscribe the card's queue slots (the first attempt of this rehearsal
+# died with an illegal-instruction abort inside a PyTorch kernel)
+GPU_MAX_HW_QUEUES=1 TDG_DIST_BACKEND=gloo timeout -k 10 900 python -u bench.py --gpus 8 --steps 6 --warmup 2 --verify-replicas 1 \
   > $O/dp8.log 2>&1
 rc=$?
 grep -E "dp_mode_select|^\{" $O/dp8.log | cut -c1-900
