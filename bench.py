@@ -93,7 +93,14 @@ def self_launch(n: int) -> int:
     # the parent never initialises HIP: the ranks are fresh child processes
     # that each bind their own GPU
     assert not torch.cuda.is_initialized(), "bench.py launcher must not initialise HIP"
-    return launch.launch([os.path.abspath(__file__)] + sys.argv[1:], n, spec)
+    extra = {}
+    if 0 < ngpu < n and "GPU_MAX_HW_QUEUES" not in os.environ:
+        # several ranks share a card (gloo rehearsal): one hardware queue each,
+        # so the ranks' queues together stay within the card's queue slots (an
+        # 8-rank rehearsal with 4 queues per rank aborted once inside a PyTorch
+        # kernel with an illegal-instruction error; with 1 it ran clean)
+        extra["GPU_MAX_HW_QUEUES"] = "1"
+    return launch.launch([os.path.abspath(__file__)] + sys.argv[1:], n, spec, env_extra=extra)
 
 
 def _fp8_precision() -> str:
