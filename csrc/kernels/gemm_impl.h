@@ -465,10 +465,49 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
 #pragma unroll
       for (int h = 0; h < 3; ++h) issue_half(1, h);
     }
+    // Fragment reads at immediate DS offsets: every read of a K-step is one
+    // of six per-lane bases (+ the stage) plus a compile-time offset -- the
+    // half image, the 32-deep k-step, the 4-row group of a transposing read
+    // or the subtile row -- instead of a swizzled address computed per read
+    // (~50 VALU per K-step and wave). The swizzle terms of frag<> (lds_off)
+    // depend only on the lane there: K-contiguous images XOR the 32-byte
+    // segment 2 s + (g >> 1) with (lane >> 1) & 3, one base per k-step s;
+    // MN-contiguous images XOR the subtile's segment with (lane >> 2) & 3 |
+    // (g & 1) << 2, one base per subtile.
+    const int fg = lane >> 4, fcl = lane & 15, fq = fcl >> 2, fp = fcl & 3;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+    auto kc_base = [&](int row0, int s) -> uint32_t {
+      return lds0 + (row0 + fcl) * (BK * 2) + (((2 * s + (fg >> 1)) ^ ((fcl >> 1) & 3)) << 5) + (fg & 1) * 16;
+    };
+    auto mn_base = [&](int sub) -> uint32_t {
+      return lds0 + (8 * fg + fq) * 256 + 8 * fp + ((sub ^ (fq | ((fg & 1) << 2))) << 5);
+    };
+    uint32_t rba[4], rbb[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rba[i] = A_KC ? kc_base(arow, i & 1) : mn_base((arow >> 4) + i);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) rbb[j] = B_KC ? kc_base(brow, j) : mn_base((brow >> 4) + j);
+    // fragment (subtile I, k-step S) of the half image at H * HB; b: bases of the stage
+    auto frag_imm = [&](auto kcc, auto hc, auto ic, auto sc, const uint32_t* b) -> short8_t {
+      constexpr bool KC = decltype(kcc)::value;
+      constexpr int H = decltype(hc)::value, I = decltype(ic)::value, S = decltype(sc)::value;
+      if constexpr (KC) {
+        return lds_read_b128_at<H * HB + I * 16 * BK * 2>(b[S]);
+      } else {
+        return cat4(lds_read_tr16_at<H * HB + 8192 * S>(b[I]), lds_read_tr16_at<H * HB + 8192 * S + 1024>(b[I]));
+      }
+    };
+    using AKCc = std::integral_constant<bool, A_KC>;
+    using BKCc = std::integral_constant<bool, B_KC>;
     // MODE 3: K-tiles kt+1 and kt+2 exist; 2: kt+1 is the last; 1: kt is
     auto kstep_deep = [&](int kt, auto modec) {
       constexpr int MODE = decltype(modec)::value;
-      const char* st = smem + (kt & 1) * SB;
+      const uint32_t stg = (uint32_t)(kt & 1) * SB;
+      uint32_t ba[4], bb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ba[i] = rba[i] + stg;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bb[j] = rbb[j] + stg;
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph) {
         if (ph < 3) {
@@ -478,25 +517,29 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const R256Args args,
           lds_barrier();
           if (kt == 0 && ph == 0) TDG_STAMP(1);
         }
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using C2 = std::integral_constant<int, 2>;
+        using C3 = std::integral_constant<int, 3>;
         if (ph == 0) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) fa[i][s2] = frag<A_KC, 128>(st + 0 * HB, arow + 16 * i, s2, lane);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) fb[j][s2] = frag<B_KC, 128>(st + 2 * HB, brow + 16 * j, s2, lane);
+          static_for<4>([&](auto I) {
+            fa[I][0] = frag_imm(AKCc{}, C0{}, I, C0{}, ba);
+            fa[I][1] = frag_imm(AKCc{}, C0{}, I, C1{}, ba);
+          });
+          static_for<2>([&](auto J) {
+            fb[J][0] = frag_imm(BKCc{}, C2{}, J, C0{}, bb);
+            fb[J][1] = frag_imm(BKCc{}, C2{}, J, C1{}, bb);
+          });
         } else if (ph == 1) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) fb[2 + j][s2] = frag<B_KC, 128>(st + 3 * HB, brow + 16 * j, s2, lane);
+          static_for<2>([&](auto J) {
+            fb[2 + J][0] = frag_imm(BKCc{}, C3{}, J, C0{}, bb);
+            fb[2 + J][1] = frag_imm(BKCc{}, C3{}, J, C1{}, bb);
+          });
         } else if (ph == 2) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) fa[4 + i][s2] = frag<A_KC, 128>(st + 1 * HB, arow + 16 * i, s2, lane);
+          static_for<4>([&](auto I) {
+            fa[4 + I][0] = frag_imm(AKCc{}, C1{}, I, C0{}, ba);
+            fa[4 + I][1] = frag_imm(AKCc{}, C1{}, I, C1{}, ba);
+          });
         }
         // refills: the slot read in the previous phase (every wave's reads of
         // it completed before this phase's barrier) takes K-tile kt + 2
