@@ -40,10 +40,15 @@ int tdg_reduce_partials_multi(const float* const* parts, float* const* outs, con
                               int G, int N, float beta, hipStream_t st);
 int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe, void* out, int M,
                   int L, int D, float scale, float p, uint64_t seed, const long long* ctr,
-                  uint64_t site, hipStream_t st);
+                  uint64_t site, void* kbits, hipStream_t st);
 int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, int M, int D,
                   float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
                   hipStream_t st);
+void tdg_embed_csr_ws(int M, int V, int D, long long* n32, long long* n64);
+int tdg_embed_bwd_csr(const void* tok, int tok64, const void* dout, const void* kbits,
+                      float* dtable, int* ws32, long long* ws64, int M, int D, int V, float scale,
+                      float p, uint64_t seed, const long long* ctr, uint64_t site, float beta,
+                      hipStream_t st);
 int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable, long long* acc,
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
@@ -776,7 +781,8 @@ void reduce_partials_multi(const std::vector<Tensor>& parts, const std::vector<T
 
 // ---------------------------------------------------------------- embedding
 void embed_fwd(const Tensor& tok, const Tensor& table, const Tensor& pe, const Tensor& out,
-               double scale, double p, int64_t seed, const optional<Tensor>& ctr, int64_t site) {
+               double scale, double p, int64_t seed, const optional<Tensor>& ctr, int64_t site,
+               const optional<Tensor>& kbits) {
   TORCH_CHECK(tok.dim() == 2 && tok.is_contiguous() && tok.is_cuda(), "tok must be [B,L]");
   const bool t64 = tok.scalar_type() == at::kLong;
   TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
@@ -789,10 +795,12 @@ void embed_fwd(const Tensor& tok, const Tensor& table, const Tensor& pe, const T
   const int64_t D = table.size(1), L = tok.size(1), M = tok.numel();
   TORCH_CHECK(pe.dim() == 2 && pe.size(1) == D && pe.size(0) >= L, "pe table too short");
   TORCH_CHECK(out.numel() == M * D, "out shape");
+  check_kbits(kbits, M, D);
   c10::DeviceGuard g(tok.device());
   const int rc = tdg_embed_fwd(tok.data_ptr(), t64, table.data_ptr(), pe.data_ptr<float>(),
                                out.data_ptr(), (int)M, (int)L, (int)D, (float)scale, (float)p,
-                               (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site, stream_of(tok));
+                               (uint64_t)seed, ctr_ptr(ctr), (uint64_t)site,
+                               kbits.has_value() ? kbits->data_ptr() : nullptr, stream_of(tok));
   check_err(rc, "tdg embed_fwd");
 }
 
@@ -835,6 +843,53 @@ void embed_bwd_det(const Tensor& tok, const Tensor& dout, const Tensor& dtable, 
                                    (float)scale, (float)p, (uint64_t)seed, ctr_ptr(ctr),
                                    (uint64_t)site, accumulate ? 1.f : 0.f, stream_of(tok));
   check_err(rc, "tdg embed_bwd_det");
+}
+
+// (int32 words, int64 words) of the CSR embedding backward's workspace
+std::vector<int64_t> embed_csr_ws(int64_t M, int64_t V, int64_t D) {
+  long long n32 = 0, n64 = 0;
+  tdg_embed_csr_ws((int)M, (int)V, (int)D, &n32, &n64);
+  return {n32, n64};
+}
+
+// Deterministic CSR embedding backward (sort, per-row gather, cut-row
+// combine: embed.hip); bitwise the fixed-point atomic path's gradient.
+// Returns false (nothing launched) when V exceeds the sort's LDS histogram.
+bool embed_bwd_csr(const Tensor& tok, const Tensor& dout, const Tensor& dtable, const Tensor& ws32,
+                   const Tensor& ws64, double scale, double p, int64_t seed,
+                   const optional<Tensor>& ctr, int64_t site, bool accumulate,
+                   const optional<Tensor>& kbits) {
+  TORCH_CHECK(tok.is_contiguous() && tok.is_cuda(), "tok");
+  const bool t64 = tok.scalar_type() == at::kLong;
+  TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
+  check_bf16(dout, "dout");
+  check_contig(dout, "dout");
+  check_f32(dtable, "dtable");
+  check_contig(dtable, "dtable");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(dtable.data_ptr()) & 15) == 0, "dtable 16-byte aligned");
+  const int64_t D = dtable.size(1), M = tok.numel(), V = dtable.size(0);
+  TORCH_CHECK(dout.numel() == M * D, "dout shape");
+  TORCH_CHECK(M > 0 && M < (1LL << 30), "token count");
+  check_kbits(kbits, M, D);
+  long long n32 = 0, n64 = 0;
+  tdg_embed_csr_ws((int)M, (int)V, (int)D, &n32, &n64);
+  TORCH_CHECK(ws32.scalar_type() == at::kInt && ws32.is_cuda() && ws32.is_contiguous() &&
+                  ws32.numel() >= n32 && (reinterpret_cast<uintptr_t>(ws32.data_ptr()) & 15) == 0,
+              "embed_bwd_csr: ws32 int32 [", n32, "]");
+  TORCH_CHECK(ws64.scalar_type() == at::kLong && ws64.is_cuda() && ws64.is_contiguous() &&
+                  ws64.numel() >= n64,
+              "embed_bwd_csr: ws64 int64 [", n64, "]");
+  c10::DeviceGuard g(tok.device());
+  const int rc = tdg_embed_bwd_csr(tok.data_ptr(), t64, dout.data_ptr(),
+                                   kbits.has_value() ? kbits->data_ptr() : nullptr,
+                                   dtable.data_ptr<float>(), ws32.data_ptr<int>(),
+                                   reinterpret_cast<long long*>(ws64.data_ptr<int64_t>()), (int)M,
+                                   (int)D, (int)V, (float)scale, (float)p, (uint64_t)seed,
+                                   ctr_ptr(ctr), (uint64_t)site, accumulate ? 1.f : 0.f,
+                                   stream_of(tok));
+  if (rc == -2) return false;
+  check_err(rc, "tdg embed_bwd_csr");
+  return true;
 }
 
 // ---------------------------------------------------------------- grouped GEMM
@@ -1412,6 +1467,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("embed_bwd_det", &embed_bwd_det);
+  m.def("embed_csr_ws", &embed_csr_ws);
+  m.def("embed_bwd_csr", &embed_bwd_csr);
   m.def("count_tokens", &count_tokens);
   m.def("prep_batch", &prep_batch);
   m.def("transpose_grouped", &transpose_grouped);

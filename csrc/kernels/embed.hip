@@ -19,7 +19,7 @@ template <int D, typename TokT>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(
     const TokT* __restrict__ tok, const bf16_t* __restrict__ table, const float* __restrict__ pe,
     bf16_t* __restrict__ out, int M, int L, float scale, float p, uint32_t thresh, uint64_t seed,
-    const long long* __restrict__ ctr, uint64_t site) {
+    const long long* __restrict__ ctr, uint64_t site, uint8_t* __restrict__ kbits) {
   constexpr int VEC = D / 64;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -36,6 +36,15 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(
     const uint32_t km = keep_bits<VEC>(seed, ctr, site, (size_t)row * D, lane, thresh);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) v.v[i] = ((km >> i) & 1u) ? v.v[i] * sc : 0.f;
+    if constexpr (VEC >= 8) {
+      // the keep bits as a row-major bitmap (byte c / 8 of the row = columns
+      // c..c+7) for the CSR backward, which then draws no Philox
+      if (kbits) {
+#pragma unroll
+        for (int c = 0; c < RowMap<VEC>::CH; ++c)
+          kbits[(size_t)row * (D / 8) + 64 * c + lane] = (uint8_t)(km >> (8 * c));
+      }
+    }
   }
   v.store_row(out + (size_t)row * D, lane);
 }
@@ -174,6 +183,288 @@ __global__ __launch_bounds__(256) void embed_acc_convert_kernel(long long* __res
   }
 }
 
+// ---------------------------------------------------------------- CSR backward
+// Deterministic and free of global atomics (the fixed-point kernel above spends
+// its time on 4 M int64 atomics per table: ~28 us + 12 us conversion at 8192 x
+// 512). (1) One workgroup counting-sorts the token ids (LDS histogram, scan,
+// scatter) and cuts every vocabulary row into work items of at most ET
+// occurrences, each holding its token positions; (2) one wave per item adds
+// its rows' dropout-masked, scaled gradients as 2^-32 fixed-point int64 in
+// registers -- integer addition, so the order of the rows does not matter and
+// the sum is bitwise the fixed-point atomic kernel's -- and writes the f32
+// gradient row, or for a row cut into several items an int64 partial; (3) one
+// workgroup per such row adds its partials. Every table row is written
+// (untouched rows: 0, or beta * old).
+constexpr int ET = 8;          // occurrences per work item (their loads in flight together)
+constexpr int EVMAX = 16384;   // vocabulary rows of the LDS histogram
+constexpr int EPMAX = 16;      // token positions per sort thread (M <= 16384)
+
+struct EmbItem {
+  int v, slot, n, pad;  // row, partial slot (-1: the row's only item), occurrences
+  int pos[ET];          // token positions
+};
+struct EmbCsr {
+  EmbItem* items;   // [V + M / ET + 1]
+  int4* heavy;      // [M / ET + 1]: (row, first slot, slots, 0)
+  int* counts;      // [2]: items, cut rows
+  long long* slab;  // [2 M / ET + 2, D] int64 partials
+};
+
+__host__ __device__ inline int csr_ub_items(int M, int V) { return V + M / ET + 1; }
+__host__ __device__ inline int csr_ub_heavy(int M) { return M / ET + 1; }
+__host__ __device__ inline int csr_ub_slots(int M) { return 2 * (M / ET) + 2; }
+
+template <typename TT>
+__global__ __launch_bounds__(1024) void embed_sort_kernel(const TT* __restrict__ tok, int M, int V,
+                                                          EmbCsr cs) {
+  __shared__ int cnt[EVMAX];    // occurrences, then the scatter cursor
+  __shared__ int ibase[EVMAX];  // first item of each row
+  __shared__ int4 wtot[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int v = tid; v < V; v += 1024) cnt[v] = 0;
+  // each thread a contiguous run of <= EPMAX positions, loaded at once; equal
+  // consecutive ids are added as one count (right padding: one LDS atomic per
+  // thread instead of one per position on a single bin)
+  const int P = (M + 1023) / 1024;
+  const int i0 = min(M, tid * P), i1 = min(M, i0 + P);
+  long long tk[EPMAX];
+#pragma unroll
+  for (int u = 0; u < EPMAX; ++u) {
+    long long t = -1;
+    if (i0 + u < i1) t = (long long)tok[i0 + u];
+    tk[u] = (t >= 0 && t < V) ? t : -1;
+  }
+  __syncthreads();
+  {
+    long long cur = -1;
+    int len = 0;
+#pragma unroll
+    for (int u = 0; u < EPMAX; ++u) {
+      if (tk[u] != cur) {
+        if (cur >= 0) atomicAdd(&cnt[cur], len);
+        cur = tk[u];
+        len = 0;
+      }
+      ++len;
+    }
+    if (cur >= 0) atomicAdd(&cnt[cur], len);
+  }
+  __syncthreads();
+  // each thread a contiguous run of rows: items, partial slots, cut rows
+  const int C = (V + 1023) / 1024;
+  const int v0 = min(V, tid * C), v1 = min(V, v0 + C);
+  int4 loc = make_int4(0, 0, 0, 0);
+  for (int v = v0; v < v1; ++v) {
+    const int c = cnt[v];
+    const int n = c > ET ? (c + ET - 1) / ET : 1;
+    loc.y += n;
+    if (c > ET) {
+      loc.z += n;
+      loc.w += 1;
+    }
+  }
+  // block exclusive scan (wave scan + wave totals)
+  int4 inc = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int b = __shfl_up(inc.y, d, 64), c = __shfl_up(inc.z, d, 64), e = __shfl_up(inc.w, d, 64);
+    if (lane >= d) {
+      inc.y += b;
+      inc.z += c;
+      inc.w += e;
+    }
+  }
+  if (lane == 63) wtot[wid] = inc;
+  __syncthreads();
+  int4 o = make_int4(0, inc.y - loc.y, inc.z - loc.z, inc.w - loc.w);
+  for (int w = 0; w < wid; ++w) {
+    o.y += wtot[w].y;
+    o.z += wtot[w].z;
+    o.w += wtot[w].w;
+  }
+  for (int v = v0; v < v1; ++v) {
+    const int c = cnt[v];
+    const bool cut = c > ET;
+    const int n = cut ? (c + ET - 1) / ET : 1;
+    for (int k = 0; k < n; ++k) {
+      EmbItem* it = cs.items + o.y + k;
+      *reinterpret_cast<int4*>(it) = make_int4(v, cut ? o.z + k : -1, min(c, (k + 1) * ET) - k * ET, 0);
+    }
+    if (cut) {
+      cs.heavy[o.w] = make_int4(v, o.z, n, 0);
+      o.z += n;
+      o.w += 1;
+    }
+    ibase[v] = o.y;
+    cnt[v] = 0;  // scatter cursor
+    o.y += n;
+  }
+  if (tid == 1023) {  // (its run ends at V: its running offsets are the totals)
+    cs.counts[0] = o.y;
+    cs.counts[1] = o.w;
+  }
+  __syncthreads();
+  {
+    long long cur = -1;
+    int len = 0, r0 = i0;
+    auto scatter = [&]() {
+      const int b = atomicAdd(&cnt[cur], len);
+      const int ib = ibase[cur];
+      for (int k = 0; k < len; ++k) {
+        const int q = b + k;
+        cs.items[ib + q / ET].pos[q % ET] = r0 + k;
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < EPMAX; ++u) {
+      if (tk[u] != cur) {
+        if (cur >= 0) scatter();
+        cur = tk[u];
+        len = 0;
+        r0 = i0 + u;
+      }
+      ++len;
+    }
+    if (cur >= 0) scatter();
+  }
+}
+
+// f32 gradient row (fixed-point sums in RowMap slots) -> dtable row, beta * old
+template <int VEC>
+__device__ __forceinline__ void emb_store_row(float* __restrict__ row, const long long (&acc)[VEC],
+                                              int lane, float beta, const WtBuf& wt) {
+  using Map = RowMap<VEC>;
+#pragma unroll
+  for (int c = 0; c < Map::CH; ++c) {
+    float* p = row + c * 64 * Map::W + lane * Map::W;
+#pragma unroll
+    for (int q = 0; q < Map::W; q += 4 > Map::W ? Map::W : 4) {
+      if constexpr (Map::W >= 4) {
+        float4 o = make_float4((float)acc[c * Map::W + q] * (1.f / FX_SCALE),
+                               (float)acc[c * Map::W + q + 1] * (1.f / FX_SCALE),
+                               (float)acc[c * Map::W + q + 2] * (1.f / FX_SCALE),
+                               (float)acc[c * Map::W + q + 3] * (1.f / FX_SCALE));
+        if (beta != 0.f) {
+          const float4 b = *reinterpret_cast<const float4*>(p + q);
+          o.x += beta * b.x;
+          o.y += beta * b.y;
+          o.z += beta * b.z;
+          o.w += beta * b.w;
+        }
+        wt.st16(p + q, o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < Map::W; ++e) {
+          float o = (float)acc[c * Map::W + e] * (1.f / FX_SCALE);
+          if (beta != 0.f) o += beta * p[e];
+          p[e] = o;
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void embed_gather_kernel(const bf16_t* __restrict__ dout,
+                                                           const uint8_t* __restrict__ kbits,
+                                                           float* __restrict__ dtable, EmbCsr cs,
+                                                           int V, int nub, float sc, float p,
+                                                           uint32_t thresh, uint64_t seed,
+                                                           const long long* ctr, uint64_t site,
+                                                           float beta) {
+  constexpr int VEC = D / 64;
+  using Map = RowMap<VEC>;
+  const int lane = threadIdx.x & 63;
+  const int it = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (it >= nub) return;
+  // the item (row, slot, count and its positions) and the item count in
+  // flight together; then all its rows (and keep bytes)
+  const EmbItem* ip = cs.items + it;
+  const int4 w = *reinterpret_cast<const int4*>(ip);
+  const int4 pa = *reinterpret_cast<const int4*>(ip->pos);
+  const int4 pb = *reinterpret_cast<const int4*>(ip->pos + 4);
+  if (it >= cs.counts[0]) return;
+  const int n = w.z;
+  const int r[ET] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+  static_assert(ET == 8, "positions as two int4");
+  RowVec<VEC> g[ET];
+  uint32_t km[ET];
+#pragma unroll
+  for (int u = 0; u < ET; ++u) {
+    if (u < n) {
+      g[u].load_row(dout + (size_t)r[u] * D, lane);
+      km[u] = 0xffffffffu;
+      if constexpr (VEC >= 8) {
+        if (p > 0.f && kbits) {
+          uint32_t b = 0;
+#pragma unroll
+          for (int c = 0; c < Map::CH; ++c)
+            b |= (uint32_t)kbits[(size_t)r[u] * (D / 8) + 64 * c + lane] << (8 * c);
+          km[u] = b;
+        }
+      }
+    }
+  }
+  long long acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0;
+#pragma unroll
+  for (int u = 0; u < ET; ++u) {
+    if (u >= n) break;
+    uint32_t m = km[u];
+    if (p > 0.f && !(VEC >= 8 && kbits))
+      m = keep_bits<VEC>(seed, ctr, site, (size_t)r[u] * D, lane, thresh);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float x = g[u].v[i] * sc;  // (the fixed-point atomic kernel's arithmetic)
+      if (!((m >> i) & 1u)) x = 0.f;
+      acc[i] += (long long)rintf(x * FX_SCALE);
+    }
+  }
+  if (w.y < 0) {
+    emb_store_row<VEC>(dtable + (size_t)w.x * D, acc, lane, beta,
+                       WtBuf(dtable, (size_t)V * D * sizeof(float)));
+  } else {
+    long long* sl = cs.slab + (size_t)w.y * D;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) sl[Map::col(lane, i)] = acc[i];
+  }
+}
+
+// one 16-wave workgroup per cut row: wave w adds the row's partial slots
+// w, w + 16, ...; the 16 sums are added through LDS (integers: any order)
+template <int D>
+__global__ __launch_bounds__(1024) void embed_combine_kernel(float* __restrict__ dtable, EmbCsr cs,
+                                                             int V, int nub, float beta) {
+  constexpr int VEC = D / 64;
+  using Map = RowMap<VEC>;
+  __shared__ long long red[16][D];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int hb = blockIdx.x;
+  if (hb >= nub || hb >= cs.counts[1]) return;
+  const int4 h = cs.heavy[hb];
+  long long acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0;
+  for (int k = wid; k < h.z; k += 16) {
+    const long long* sl = cs.slab + (size_t)(h.y + k) * D;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] += sl[Map::col(lane, i)];
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) red[wid][Map::col(lane, i)] = acc[i];
+  __syncthreads();
+  float* row = dtable + (size_t)h.x * D;
+  for (int c = threadIdx.x; c < D; c += 1024) {
+    long long t = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][c];
+    float o = (float)t * (1.f / FX_SCALE);
+    if (beta != 0.f) o += beta * row[c];
+    row[c] = o;
+  }
+}
+
 }  // namespace tdg
 
 using namespace tdg;
@@ -181,11 +472,12 @@ using namespace tdg;
 namespace {
 template <int D, typename TT>
 void fwd_d(const void* tok, const void* table, const float* pe, void* out, int M, int L,
-           float scale, float p, uint64_t seed, const long long* ctr, uint64_t site, hipStream_t st) {
+           float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
+           void* kbits, hipStream_t st) {
   const uint32_t thresh = dropout_thresh(p);
   hipLaunchKernelGGL((embed_fwd_kernel<D, TT>), dim3(cdiv(M, 4)), dim3(256), 0, st,
                      (const TT*)tok, (const bf16_t*)table, pe, (bf16_t*)out, M, L, scale, p,
-                     thresh, seed, ctr, site);
+                     thresh, seed, ctr, site, (uint8_t*)kbits);
 }
 template <int D, typename TT>
 void bwd_d(const void* tok, const void* dout, float* dtable, int M, float scale, float p,
@@ -212,13 +504,15 @@ void bwd_fx_d(const void* tok, const void* dout, unsigned long long* acc, int M,
     default: return -1;                           \
   }
 
+// kbits (may be null; D >= 512): the dropout keep bits, uint8 [M, D / 8]
 extern "C" int tdg_embed_fwd(const void* tok, int tok64, const void* table, const float* pe,
                              void* out, int M, int L, int D, float scale, float p, uint64_t seed,
-                             const long long* ctr, uint64_t site, hipStream_t st) {
+                             const long long* ctr, uint64_t site, void* kbits, hipStream_t st) {
+  if (kbits && D < 512) return -3;
   if (tok64) {
-    TDG_D_SWITCH(fwd_d, long long, tok, table, pe, out, M, L, scale, p, seed, ctr, site, st)
+    TDG_D_SWITCH(fwd_d, long long, tok, table, pe, out, M, L, scale, p, seed, ctr, site, kbits, st)
   } else {
-    TDG_D_SWITCH(fwd_d, int, tok, table, pe, out, M, L, scale, p, seed, ctr, site, st)
+    TDG_D_SWITCH(fwd_d, int, tok, table, pe, out, M, L, scale, p, seed, ctr, site, kbits, st)
   }
 }
 
@@ -267,4 +561,55 @@ extern "C" int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, f
   const int blocks = (int)std::min<long long>(4096, (n / 2 + 255) / 256 + 1);
   hipLaunchKernelGGL(embed_acc_convert_kernel, dim3(blocks), dim3(256), 0, st, acc, dtable, n, beta);
   return 0;
+}
+
+// Workspace of the CSR backward: int32 words (16-byte aligned pieces) and
+// int64 partial words.
+extern "C" void tdg_embed_csr_ws(int M, int V, int D, long long* n32, long long* n64) {
+  *n32 = (long long)(sizeof(EmbItem) / 4) * csr_ub_items(M, V) + 4LL * csr_ub_heavy(M) + 4;
+  *n64 = (long long)csr_ub_slots(M) * D;
+}
+
+// Deterministic CSR embedding backward (three launches): dtable = beta *
+// dtable + sum over the rows of each token of drop(dout) * scale. ws32 / ws64
+// hold tdg_embed_csr_ws words. Returns -1 for an unsupported D, -2 for V past
+// the LDS histogram or M past the sort's registers (the caller uses the
+// fixed-point atomic path).
+extern "C" int tdg_embed_bwd_csr(const void* tok, int tok64, const void* dout, const void* kbits,
+                                 float* dtable, int* ws32, long long* ws64, int M, int D, int V,
+                                 float scale, float p, uint64_t seed, const long long* ctr,
+                                 uint64_t site, float beta, hipStream_t st) {
+  if (V > EVMAX || V <= 0 || M <= 0 || M > 1024 * EPMAX) return -2;
+  if (D != 128 && D != 256 && D != 512 && D != 1024) return -1;
+  EmbCsr cs;
+  int* w = ws32;
+  cs.items = reinterpret_cast<EmbItem*>(w);
+  w += (long long)(sizeof(EmbItem) / 4) * csr_ub_items(M, V);
+  cs.heavy = reinterpret_cast<int4*>(w);
+  w += 4LL * csr_ub_heavy(M);
+  cs.counts = w;
+  cs.slab = ws64;
+  if (tok64)
+    hipLaunchKernelGGL(embed_sort_kernel<long long>, dim3(1), dim3(1024), 0, st,
+                       (const long long*)tok, M, V, cs);
+  else
+    hipLaunchKernelGGL(embed_sort_kernel<int>, dim3(1), dim3(1024), 0, st, (const int*)tok, M, V, cs);
+  const uint32_t thresh = dropout_thresh(p);
+  const float sc = p > 0.f ? scale / (1.f - p) : scale;
+  const int ni = csr_ub_items(M, V), nh = csr_ub_heavy(M);
+#define TDG_CSR(DD)                                                                               \
+  hipLaunchKernelGGL(embed_gather_kernel<DD>, dim3(cdiv(ni, 4)), dim3(256), 0, st,                \
+                     (const bf16_t*)dout, (const uint8_t*)kbits, dtable, cs, V, ni, sc, p, thresh, \
+                     seed, ctr, site, beta);                                                      \
+  hipLaunchKernelGGL(embed_combine_kernel<DD>, dim3(nh), dim3(1024), 0, st, dtable, cs, V, nh,    \
+                     beta);                                                                       \
+  return 0;
+  switch (D) {
+    case 128: TDG_CSR(128)
+    case 256: TDG_CSR(256)
+    case 512: TDG_CSR(512)
+    case 1024: TDG_CSR(1024)
+  }
+#undef TDG_CSR
+  return -1;
 }

@@ -509,7 +509,12 @@ class EmbedFn(torch.autograd.Function):
         ctx.table, ctx.site, ctx.rt, ctx.scale = table, site, rt, scale
         ctx.save_for_backward(tok)
         if tok.is_cuda:
-            return K.embed_fwd(tok, table.compute, pe, scale, rt.p, rt.seed, rt.ctr, site)
+            # training with dropout: the keep bits for the CSR backward
+            ctx.kbits = None
+            if K.EMBED_CSR and K.DETERMINISTIC_EMBED and rt.training and rt.p > 0 and d % 512 == 0:
+                ctx.kbits = torch.empty(tok.numel(), d // 8, dtype=torch.uint8, device=tok.device)
+            return K.embed_fwd(tok, table.compute, pe, scale, rt.p, rt.seed, rt.ctr, site,
+                               kbits=ctx.kbits)
         B, L = tok.shape
         x = table.master[tok] * scale + pe[:L].unsqueeze(0)
         ks = _keep_scale(rt, site, x.shape, x.device)
@@ -523,7 +528,7 @@ class EmbedFn(torch.autograd.Function):
         if dout.is_cuda:
             dc = dout.contiguous()
             K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site,
-                        accumulate=rt.accumulate)
+                        accumulate=rt.accumulate, kbits=ctx.kbits)
             _ready(rt, table)
             return None, None, None, None, None, None
         else:

@@ -524,21 +524,40 @@ def reduce_partials_multi(items) -> None:
 
 
 # ------------------------------------------------------------------ embedding / loss / optim
-def embed_fwd(tok, table, pe, scale, p, seed, ctr, site):
+def embed_fwd(tok, table, pe, scale, p, seed, ctr, site, kbits=None):
+    """dropout(table[tok] * scale + pe); kbits (uint8 [B * L, D / 8], D >=
+    512): also the dropout keep bits, for the CSR backward."""
     B, L = tok.shape
     D = table.shape[1]
     out = torch.empty(B, L, D, dtype=torch.bfloat16, device=tok.device)
-    C().embed_fwd(tok, table, pe, out, scale, p, seed, ctr, site)
+    C().embed_fwd(tok, table, pe, out, scale, p, seed, ctr, site, kbits)
     return out
 
 
 DETERMINISTIC_EMBED = os.environ.get("TDG_DETERMINISTIC", "1") != "0"
 
 
-def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False):
+# deterministic embedding backward without global atomics: token sort, one
+# wave per vocabulary row (or cut of a frequent row), fixed-point sums in
+# registers (embed.hip "CSR backward"); else the fixed-point atomic kernel
+EMBED_CSR = os.environ.get("TDG_EMBED_CSR", "1") != "0"
+
+
+def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False, kbits=None):
     """dtable (=|+=) scatter-add of the embedding gradient. Default: the
-    deterministic fixed-point path (bitwise reproducible); TDG_DETERMINISTIC=0
-    uses plain f32 atomics (dtable must then be zero unless accumulating)."""
+    deterministic paths (bitwise reproducible and bitwise equal to each
+    other): the CSR kernels, else fixed-point int64 atomics;
+    TDG_DETERMINISTIC=0 uses plain f32 atomics (dtable must then be zero
+    unless accumulating). kbits: the forward's keep bits (CSR path; else the
+    Philox mask is regenerated)."""
+    if DETERMINISTIC_EMBED and EMBED_CSR:
+        M, V, D = tok.numel(), dtable.shape[0], dtable.shape[1]
+        n32, n64 = C().embed_csr_ws(M, V, D)
+        w32 = workspace("embed_csr32", n32, dtable.device, torch.int32)
+        w64 = workspace("embed_csr64", n64, dtable.device, torch.int64)
+        if C().embed_bwd_csr(tok, dout, dtable, w32, w64, scale, p, seed, ctr, site, accumulate,
+                             kbits):
+            return
     if DETERMINISTIC_EMBED:
         acc = workspace("embed_fx", dtable.numel(), dtable.device, torch.int64, zero=True)
         C().embed_bwd_det(tok, dout, dtable, acc, scale, p, seed, ctr, site, accumulate)
