@@ -45,10 +45,12 @@ int tdg_embed_bwd(const void* tok, int tok64, const void* dout, float* dtable, i
                   float scale, float p, uint64_t seed, const long long* ctr, uint64_t site,
                   hipStream_t st);
 void tdg_embed_csr_ws(int M, int V, int D, long long* n32, long long* n64);
-int tdg_embed_bwd_csr(const void* tok, int tok64, const void* dout, const void* kbits,
-                      float* dtable, int* ws32, long long* ws64, int M, int D, int V, float scale,
-                      float p, uint64_t seed, const long long* ctr, uint64_t site, float beta,
-                      hipStream_t st);
+int tdg_embed_csr_ok(int M, int V);
+int tdg_embed_csr_sort(int ntab, const void* const* tok, const int* tok64, const int* M,
+                       const int* V, int* const* ws32, long long* stamps, hipStream_t st);
+int tdg_embed_csr_apply(const void* dout, const void* kbits, float* dtable, int* ws32,
+                        long long* ws64, int M, int D, int V, float scale, float p, uint64_t seed,
+                        const long long* ctr, uint64_t site, float beta, hipStream_t st);
 int tdg_embed_bwd_det(const void* tok, int tok64, const void* dout, float* dtable, long long* acc,
                       int M, int D, long long V, float scale, float p, uint64_t seed,
                       const long long* ctr, uint64_t site, float beta, hipStream_t st);
@@ -852,44 +854,78 @@ std::vector<int64_t> embed_csr_ws(int64_t M, int64_t V, int64_t D) {
   return {n32, n64};
 }
 
-// Deterministic CSR embedding backward (sort, per-row gather, cut-row
-// combine: embed.hip); bitwise the fixed-point atomic path's gradient.
-// Returns false (nothing launched) when V exceeds the sort's LDS histogram.
-bool embed_bwd_csr(const Tensor& tok, const Tensor& dout, const Tensor& dtable, const Tensor& ws32,
-                   const Tensor& ws64, double scale, double p, int64_t seed,
-                   const optional<Tensor>& ctr, int64_t site, bool accumulate,
-                   const optional<Tensor>& kbits) {
-  TORCH_CHECK(tok.is_contiguous() && tok.is_cuda(), "tok");
-  const bool t64 = tok.scalar_type() == at::kLong;
-  TORCH_CHECK(t64 || tok.scalar_type() == at::kInt, "tok must be int32/int64");
+bool embed_csr_ok(int64_t M, int64_t V) { return tdg_embed_csr_ok((int)M, (int)V) != 0; }
+
+void check_csr_ws(const Tensor& ws32, int64_t M, int64_t V, int64_t D, const char* n) {
+  long long n32 = 0, n64 = 0;
+  tdg_embed_csr_ws((int)M, (int)V, (int)D, &n32, &n64);
+  TORCH_CHECK(ws32.scalar_type() == at::kInt && ws32.is_cuda() && ws32.is_contiguous() &&
+                  ws32.numel() >= n32 && (reinterpret_cast<uintptr_t>(ws32.data_ptr()) & 15) == 0,
+              n, ": int32 workspace of ", n32, " words (16-byte aligned)");
+}
+
+// Token sort of the CSR embedding backward for one or two tables (one
+// launch): toks[i] (int32/int64, any shape) over vocabularies V[i] into the
+// int32 workspaces ws32[i] (embed_csr_ws words).
+void embed_csr_sort(const std::vector<Tensor>& toks, const std::vector<int64_t>& V,
+                    const std::vector<Tensor>& ws32, const optional<Tensor>& stamps) {
+  const int n = (int)toks.size();
+  TORCH_CHECK(n >= 1 && n <= 2 && (int)V.size() == n && (int)ws32.size() == n, "embed_csr_sort: 1-2 tables");
+  const void* tp[2];
+  int t64[2], M[2], VV[2];
+  int* wp[2];
+  for (int i = 0; i < n; ++i) {
+    const Tensor& t = toks[i];
+    TORCH_CHECK(t.is_contiguous() && t.is_cuda(), "tok");
+    TORCH_CHECK(t.scalar_type() == at::kLong || t.scalar_type() == at::kInt, "tok must be int32/int64");
+    TORCH_CHECK(tdg_embed_csr_ok((int)t.numel(), (int)V[i]), "embed_csr_sort: shape past the sort");
+    check_csr_ws(ws32[i], t.numel(), V[i], 128, "embed_csr_sort");
+    tp[i] = t.data_ptr();
+    t64[i] = t.scalar_type() == at::kLong;
+    M[i] = (int)t.numel();
+    VV[i] = (int)V[i];
+    wp[i] = ws32[i].data_ptr<int>();
+  }
+  c10::DeviceGuard g(toks[0].device());
+  long long* sp = nullptr;
+  if (stamps.has_value()) {  // lab: int64 [2 * 8 * 64]
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->is_cuda() && stamps->numel() >= 1024,
+                "stamps");
+    sp = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  check_err(tdg_embed_csr_sort(n, tp, t64, M, VV, wp, sp, stream_of(toks[0])), "tdg embed_csr_sort");
+}
+
+// The embedding gradient from a sorted workspace (deterministic; bitwise the
+// fixed-point atomic path's): dtable = beta * dtable + scatter of drop(dout) *
+// scale; kbits: the forward's keep bits.
+void embed_csr_apply(const Tensor& dout, const Tensor& dtable, const Tensor& ws32,
+                     const Tensor& ws64, int64_t M, double scale, double p, int64_t seed,
+                     const optional<Tensor>& ctr, int64_t site, bool accumulate,
+                     const optional<Tensor>& kbits) {
   check_bf16(dout, "dout");
   check_contig(dout, "dout");
   check_f32(dtable, "dtable");
   check_contig(dtable, "dtable");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(dtable.data_ptr()) & 15) == 0, "dtable 16-byte aligned");
-  const int64_t D = dtable.size(1), M = tok.numel(), V = dtable.size(0);
+  const int64_t D = dtable.size(1), V = dtable.size(0);
   TORCH_CHECK(dout.numel() == M * D, "dout shape");
-  TORCH_CHECK(M > 0 && M < (1LL << 30), "token count");
+  TORCH_CHECK(tdg_embed_csr_ok((int)M, (int)V), "embed_csr_apply: shape past the sort");
   check_kbits(kbits, M, D);
+  check_csr_ws(ws32, M, V, D, "embed_csr_apply");
   long long n32 = 0, n64 = 0;
   tdg_embed_csr_ws((int)M, (int)V, (int)D, &n32, &n64);
-  TORCH_CHECK(ws32.scalar_type() == at::kInt && ws32.is_cuda() && ws32.is_contiguous() &&
-                  ws32.numel() >= n32 && (reinterpret_cast<uintptr_t>(ws32.data_ptr()) & 15) == 0,
-              "embed_bwd_csr: ws32 int32 [", n32, "]");
   TORCH_CHECK(ws64.scalar_type() == at::kLong && ws64.is_cuda() && ws64.is_contiguous() &&
                   ws64.numel() >= n64,
-              "embed_bwd_csr: ws64 int64 [", n64, "]");
-  c10::DeviceGuard g(tok.device());
-  const int rc = tdg_embed_bwd_csr(tok.data_ptr(), t64, dout.data_ptr(),
-                                   kbits.has_value() ? kbits->data_ptr() : nullptr,
-                                   dtable.data_ptr<float>(), ws32.data_ptr<int>(),
-                                   reinterpret_cast<long long*>(ws64.data_ptr<int64_t>()), (int)M,
-                                   (int)D, (int)V, (float)scale, (float)p, (uint64_t)seed,
-                                   ctr_ptr(ctr), (uint64_t)site, accumulate ? 1.f : 0.f,
-                                   stream_of(tok));
-  if (rc == -2) return false;
-  check_err(rc, "tdg embed_bwd_csr");
-  return true;
+              "embed_csr_apply: int64 workspace of ", n64, " words");
+  c10::DeviceGuard g(dout.device());
+  check_err(tdg_embed_csr_apply(dout.data_ptr(), kbits.has_value() ? kbits->data_ptr() : nullptr,
+                                dtable.data_ptr<float>(), ws32.data_ptr<int>(),
+                                reinterpret_cast<long long*>(ws64.data_ptr<int64_t>()), (int)M,
+                                (int)D, (int)V, (float)scale, (float)p, (uint64_t)seed,
+                                ctr_ptr(ctr), (uint64_t)site, accumulate ? 1.f : 0.f,
+                                stream_of(dout)),
+            "tdg embed_csr_apply");
 }
 
 // ---------------------------------------------------------------- grouped GEMM
@@ -1468,7 +1504,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("embed_bwd_det", &embed_bwd_det);
   m.def("embed_csr_ws", &embed_csr_ws);
-  m.def("embed_bwd_csr", &embed_bwd_csr);
+  m.def("embed_csr_ok", &embed_csr_ok);
+  m.def("embed_csr_sort", &embed_csr_sort);
+  m.def("embed_csr_apply", &embed_csr_apply);
   m.def("count_tokens", &count_tokens);
   m.def("prep_batch", &prep_batch);
   m.def("transpose_grouped", &transpose_grouped);

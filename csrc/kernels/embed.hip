@@ -195,9 +195,9 @@ __global__ __launch_bounds__(256) void embed_acc_convert_kernel(long long* __res
 // gradient row, or for a row cut into several items an int64 partial; (3) one
 // workgroup per such row adds its partials. Every table row is written
 // (untouched rows: 0, or beta * old).
-constexpr int ET = 8;          // occurrences per work item (their loads in flight together)
-constexpr int EVMAX = 16384;   // vocabulary rows of the LDS histogram
-constexpr int EPMAX = 16;      // token positions per sort thread (M <= 16384)
+constexpr int ET = 8;         // occurrences per work item (their loads in flight together)
+constexpr int EVMAX = 8192;   // vocabulary rows of the LDS histogram
+constexpr int EPMAX = 16;     // token positions per sort thread (M <= 16384)
 
 struct EmbItem {
   int v, slot, n, pad;  // row, partial slot (-1: the row's only item), occurrences
@@ -209,35 +209,75 @@ struct EmbCsr {
   int* counts;      // [2]: items, cut rows
   long long* slab;  // [2 M / ET + 2, D] int64 partials
 };
+// one table of a (one or two table) sort launch
+struct EmbSortTab {
+  const void* tok;
+  int tok64, M, V;
+  EmbCsr cs;
+};
+struct EmbSortArgs {
+  EmbSortTab t[2];
+  long long* stamps;  // lab only (null): s_memrealtime at the phase ends, [2][8][64]
+};
 
 __host__ __device__ inline int csr_ub_items(int M, int V) { return V + M / ET + 1; }
 __host__ __device__ inline int csr_ub_heavy(int M) { return M / ET + 1; }
 __host__ __device__ inline int csr_ub_slots(int M) { return 2 * (M / ET) + 2; }
 
-template <typename TT>
-__global__ __launch_bounds__(1024) void embed_sort_kernel(const TT* __restrict__ tok, int M, int V,
-                                                          EmbCsr cs) {
-  __shared__ int cnt[EVMAX];    // occurrences, then the scatter cursor
-  __shared__ int ibase[EVMAX];  // first item of each row
+// Workgroup barrier for LDS data only: __syncthreads() also waits for every
+// outstanding global store of the wave (vmcnt(0)), which made each of the
+// sort's per-round barriers wait for the item stores of that round (~2 us per
+// round of 1024 vocabulary rows).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One 1024-thread workgroup per table. LDS: the histogram (then the scatter
+// cursors), each row's packed (first item << 15 | first sorted position), the
+// sorted token positions and the cut rows. One block scan over per-thread
+// contiguous runs of rows gives every offset; the items are then written with
+// rows dealt to lanes in rounds of 1024, so consecutive lanes write
+// consecutive items (coalesced), and the cut rows' items one per thread.
+__global__ __launch_bounds__(1024) void embed_sort_kernel(const EmbSortArgs a) {
+  __shared__ int cnt[EVMAX];
+  __shared__ int ibst[EVMAX];
+  __shared__ int perm[1024 * EPMAX];
+  __shared__ int hrow[1024 * EPMAX / ET + 1], hslot[1024 * EPMAX / ET + 1];  // cut rows
   __shared__ int4 wtot[16];
+  const EmbSortTab tb = blockIdx.x ? a.t[1] : a.t[0];
+  const int M = tb.M, V = tb.V;
+  const EmbCsr cs = tb.cs;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // (lab stamps: wave 0 stores the clock, one slot per lane -- vector stores)
+  auto stamp = [&](int k) {
+    if (a.stamps && wid == 0)
+      a.stamps[(blockIdx.x * 8 + k) * 64 + lane] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   for (int v = tid; v < V; v += 1024) cnt[v] = 0;
-  // each thread a contiguous run of <= EPMAX positions, loaded at once; equal
-  // consecutive ids are added as one count (right padding: one LDS atomic per
-  // thread instead of one per position on a single bin)
+  // each thread a contiguous run of <= EPMAX positions, all loads in flight
+  // at once; equal consecutive ids are counted as one run (right padding:
+  // one LDS atomic per thread instead of one per position on a single bin)
   const int P = (M + 1023) / 1024;
   const int i0 = min(M, tid * P), i1 = min(M, i0 + P);
-  long long tk[EPMAX];
+  long long tl[EPMAX];
+  if (tb.tok64) {
+    const long long* t = static_cast<const long long*>(tb.tok);
 #pragma unroll
-  for (int u = 0; u < EPMAX; ++u) {
-    long long t = -1;
-    if (i0 + u < i1) t = (long long)tok[i0 + u];
-    tk[u] = (t >= 0 && t < V) ? t : -1;
+    for (int u = 0; u < EPMAX; ++u) tl[u] = i0 + u < i1 ? t[i0 + u] : -1;
+  } else {
+    const int* t = static_cast<const int*>(tb.tok);
+#pragma unroll
+    for (int u = 0; u < EPMAX; ++u) tl[u] = i0 + u < i1 ? (long long)t[i0 + u] : -1;
   }
-  __syncthreads();
+  int tk[EPMAX];
+#pragma unroll
+  for (int u = 0; u < EPMAX; ++u) tk[u] = (tl[u] >= 0 && tl[u] < V) ? (int)tl[u] : -1;
+  lds_sync();
   {
-    long long cur = -1;
-    int len = 0;
+    int cur = -1, len = 0;
 #pragma unroll
     for (int u = 0; u < EPMAX; ++u) {
       if (tk[u] != cur) {
@@ -249,84 +289,136 @@ __global__ __launch_bounds__(1024) void embed_sort_kernel(const TT* __restrict__
     }
     if (cur >= 0) atomicAdd(&cnt[cur], len);
   }
-  __syncthreads();
-  // each thread a contiguous run of rows: items, partial slots, cut rows
+  lds_sync();
+  stamp(1);
+  // offsets: each thread a contiguous run of rows, one block scan of
+  // (positions, items, partial slots, cut rows)
   const int C = (V + 1023) / 1024;
   const int v0 = min(V, tid * C), v1 = min(V, v0 + C);
   int4 loc = make_int4(0, 0, 0, 0);
   for (int v = v0; v < v1; ++v) {
     const int c = cnt[v];
     const int n = c > ET ? (c + ET - 1) / ET : 1;
+    loc.x += c;
     loc.y += n;
     if (c > ET) {
       loc.z += n;
       loc.w += 1;
     }
   }
-  // block exclusive scan (wave scan + wave totals)
   int4 inc = loc;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const int b = __shfl_up(inc.y, d, 64), c = __shfl_up(inc.z, d, 64), e = __shfl_up(inc.w, d, 64);
+    const int q0 = __shfl_up(inc.x, d, 64), q1 = __shfl_up(inc.y, d, 64);
+    const int q2 = __shfl_up(inc.z, d, 64), q3 = __shfl_up(inc.w, d, 64);
     if (lane >= d) {
-      inc.y += b;
-      inc.z += c;
-      inc.w += e;
+      inc.x += q0;
+      inc.y += q1;
+      inc.z += q2;
+      inc.w += q3;
     }
   }
   if (lane == 63) wtot[wid] = inc;
-  __syncthreads();
-  int4 o = make_int4(0, inc.y - loc.y, inc.z - loc.z, inc.w - loc.w);
-  for (int w = 0; w < wid; ++w) {
-    o.y += wtot[w].y;
-    o.z += wtot[w].z;
-    o.w += wtot[w].w;
+  lds_sync();
+  int4 o = make_int4(inc.x - loc.x, inc.y - loc.y, inc.z - loc.z, inc.w - loc.w);
+  int4 tot = make_int4(0, 0, 0, 0);
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int4 t = wtot[w];
+    if (w < wid) {
+      o.x += t.x;
+      o.y += t.y;
+      o.z += t.z;
+      o.w += t.w;
+    }
+    tot.x += t.x;
+    tot.y += t.y;
+    tot.z += t.z;
+    tot.w += t.w;
   }
   for (int v = v0; v < v1; ++v) {
     const int c = cnt[v];
     const bool cut = c > ET;
     const int n = cut ? (c + ET - 1) / ET : 1;
-    for (int k = 0; k < n; ++k) {
-      EmbItem* it = cs.items + o.y + k;
-      *reinterpret_cast<int4*>(it) = make_int4(v, cut ? o.z + k : -1, min(c, (k + 1) * ET) - k * ET, 0);
-    }
+    ibst[v] = (o.y << 15) | o.x;
+    cnt[v] = o.x;  // scatter cursor
     if (cut) {
       cs.heavy[o.w] = make_int4(v, o.z, n, 0);
+      hrow[o.w] = v;
+      hslot[o.w] = o.z;
       o.z += n;
       o.w += 1;
     }
-    ibase[v] = o.y;
-    cnt[v] = 0;  // scatter cursor
+    o.x += c;
     o.y += n;
   }
-  if (tid == 1023) {  // (its run ends at V: its running offsets are the totals)
-    cs.counts[0] = o.y;
-    cs.counts[1] = o.w;
+  if (tid == 0) {
+    cs.counts[0] = tot.y;
+    cs.counts[1] = tot.w;
   }
-  __syncthreads();
-  {
-    long long cur = -1;
-    int len = 0, r0 = i0;
-    auto scatter = [&]() {
-      const int b = atomicAdd(&cnt[cur], len);
-      const int ib = ibase[cur];
-      for (int k = 0; k < len; ++k) {
-        const int q = b + k;
-        cs.items[ib + q / ET].pos[q % ET] = r0 + k;
-      }
-    };
+  lds_sync();
+  stamp(2);
+  {  // sorted positions into LDS
+    int cur = -1, len = 0, r0 = i0;
 #pragma unroll
     for (int u = 0; u < EPMAX; ++u) {
       if (tk[u] != cur) {
-        if (cur >= 0) scatter();
+        if (cur >= 0) {
+          const int b = atomicAdd(&cnt[cur], len);
+          for (int k = 0; k < len; ++k) perm[b + k] = r0 + k;
+        }
         cur = tk[u];
         len = 0;
         r0 = i0 + u;
       }
       ++len;
     }
-    if (cur >= 0) scatter();
+    if (cur >= 0) {
+      const int b = atomicAdd(&cnt[cur], len);
+      for (int k = 0; k < len; ++k) perm[b + k] = r0 + k;
+    }
   }
+  lds_sync();
+  stamp(3);
+  // single-item rows (<= ET occurrences; untouched rows included): head and
+  // positions, rows dealt to lanes in rounds of 1024
+  for (int v = tid; v < V; v += 1024) {
+    const int ib = ibst[v] >> 15, st = ibst[v] & 0x7fff;
+    const int c = cnt[v] - st;
+    if (c > ET) continue;
+    int q[ET];
+#pragma unroll
+    for (int j = 0; j < ET; ++j) q[j] = j < c ? perm[st + j] : 0;
+    int4* it = reinterpret_cast<int4*>(cs.items + ib);
+    it[0] = make_int4(v, -1, c, 0);
+    if (c > 0) {
+      it[1] = make_int4(q[0], q[1], q[2], q[3]);
+      it[2] = make_int4(q[4], q[5], q[6], q[7]);
+    }
+  }
+  stamp(4);
+  // the cut rows' items, one thread per item: item s of the tot.z cut items
+  // belongs to the cut row h whose slot range holds it (binary search of the
+  // ascending slot bases) -- a padding id's hundreds of items, or hundreds of
+  // cut rows, are nobody's serial loop
+  for (int sidx = tid; sidx < tot.z; sidx += 1024) {
+    int lo = 0, hi = tot.w - 1;
+    while (lo < hi) {  // last h with hslot[h] <= sidx
+      const int mid = (lo + hi + 1) >> 1;
+      if (hslot[mid] <= sidx) lo = mid;
+      else hi = mid - 1;
+    }
+    const int v = hrow[lo], ib = ibst[v] >> 15, st = ibst[v] & 0x7fff;
+    const int c = cnt[v] - st, k = sidx - hslot[lo];
+    int q[ET];
+#pragma unroll
+    for (int j = 0; j < ET; ++j) q[j] = k * ET + j < c ? perm[st + k * ET + j] : 0;
+    int4* it = reinterpret_cast<int4*>(cs.items + ib + k);
+    it[0] = make_int4(v, sidx, min(c, (k + 1) * ET) - k * ET, 0);
+    it[1] = make_int4(q[0], q[1], q[2], q[3]);
+    it[2] = make_int4(q[4], q[5], q[6], q[7]);
+  }
+  stamp(5);
 }
 
 // f32 gradient row (fixed-point sums in RowMap slots) -> dtable row, beta * old
@@ -570,17 +662,8 @@ extern "C" void tdg_embed_csr_ws(int M, int V, int D, long long* n32, long long*
   *n64 = (long long)csr_ub_slots(M) * D;
 }
 
-// Deterministic CSR embedding backward (three launches): dtable = beta *
-// dtable + sum over the rows of each token of drop(dout) * scale. ws32 / ws64
-// hold tdg_embed_csr_ws words. Returns -1 for an unsupported D, -2 for V past
-// the LDS histogram or M past the sort's registers (the caller uses the
-// fixed-point atomic path).
-extern "C" int tdg_embed_bwd_csr(const void* tok, int tok64, const void* dout, const void* kbits,
-                                 float* dtable, int* ws32, long long* ws64, int M, int D, int V,
-                                 float scale, float p, uint64_t seed, const long long* ctr,
-                                 uint64_t site, float beta, hipStream_t st) {
-  if (V > EVMAX || V <= 0 || M <= 0 || M > 1024 * EPMAX) return -2;
-  if (D != 128 && D != 256 && D != 512 && D != 1024) return -1;
+namespace {
+EmbCsr csr_view(int* ws32, long long* ws64, int M, int V) {
   EmbCsr cs;
   int* w = ws32;
   cs.items = reinterpret_cast<EmbItem*>(w);
@@ -589,11 +672,46 @@ extern "C" int tdg_embed_bwd_csr(const void* tok, int tok64, const void* dout, c
   w += 4LL * csr_ub_heavy(M);
   cs.counts = w;
   cs.slab = ws64;
-  if (tok64)
-    hipLaunchKernelGGL(embed_sort_kernel<long long>, dim3(1), dim3(1024), 0, st,
-                       (const long long*)tok, M, V, cs);
-  else
-    hipLaunchKernelGGL(embed_sort_kernel<int>, dim3(1), dim3(1024), 0, st, (const int*)tok, M, V, cs);
+  return cs;
+}
+}  // namespace
+
+// Supported by the CSR path: V <= EVMAX, M <= 1024 * EPMAX (else the
+// fixed-point atomic path).
+extern "C" int tdg_embed_csr_ok(int M, int V) {
+  return V > 0 && V <= EVMAX && M > 0 && M <= 1024 * EPMAX;
+}
+
+// The token sort of one or two tables (one workgroup each, one launch): the
+// work items of the CSR backward in ws32[i] (tdg_embed_csr_ws words).
+extern "C" int tdg_embed_csr_sort(int ntab, const void* const* tok, const int* tok64, const int* M,
+                                  const int* V, int* const* ws32, long long* stamps,
+                                  hipStream_t st) {
+  if (ntab < 1 || ntab > 2) return -2;
+  EmbSortArgs a{};
+  a.stamps = stamps;
+  for (int i = 0; i < ntab; ++i) {
+    if (!tdg_embed_csr_ok(M[i], V[i])) return -2;
+    a.t[i].tok = tok[i];
+    a.t[i].tok64 = tok64[i];
+    a.t[i].M = M[i];
+    a.t[i].V = V[i];
+    a.t[i].cs = csr_view(ws32[i], nullptr, M[i], V[i]);
+  }
+  hipLaunchKernelGGL(embed_sort_kernel, dim3(ntab), dim3(1024), 0, st, a);
+  return 0;
+}
+
+// The gradient from sorted work items (tdg_embed_csr_sort): dtable = beta *
+// dtable + sum over the rows of each token of drop(dout) * scale; gather and
+// cut-row combine launches. kbits: the forward's keep bits (or null: the
+// Philox mask is regenerated).
+extern "C" int tdg_embed_csr_apply(const void* dout, const void* kbits, float* dtable, int* ws32,
+                                   long long* ws64, int M, int D, int V, float scale, float p,
+                                   uint64_t seed, const long long* ctr, uint64_t site, float beta,
+                                   hipStream_t st) {
+  if (!tdg_embed_csr_ok(M, V)) return -2;
+  const EmbCsr cs = csr_view(ws32, ws64, M, V);
   const uint32_t thresh = dropout_thresh(p);
   const float sc = p > 0.f ? scale / (1.f - p) : scale;
   const int ni = csr_ub_items(M, V), nh = csr_ub_heavy(M);

@@ -26,3 +26,16 @@ for M, V, D, pad in [(1024, 1000, 512, 0.0), (8192, 1000, 512, 0.0), (8192, 7765
             kk.embed_bwd(tok, dout, dt, math.sqrt(D), 0.1, 1, ctr, 3)
         torch.cuda.synchronize()
     print(f"M={M} V={V} D={D} pad={pad} done", flush=True)
+
+# phase clocks of the sort (s_memrealtime, 100 MHz): wave 0's view
+for M, V, pad in [(8192, 1000, 0.0), (8192, 7765, 0.0), (8192, 7765, 0.35)]:
+    g = torch.Generator().manual_seed(M + V)
+    tok = torch.randint(1, V, (M,), generator=g)
+    tok[: int(pad * M)] = 0
+    tok = tok.to(dev)
+    st = torch.zeros(1024, dtype=torch.int64, device=dev)
+    for _ in range(3):
+        kk.embed_csr_sort([(tok, V, "lab")], stamps=st)
+    torch.cuda.synchronize()
+    t = st.view(2, 8, 64)[0, :6, 0].cpu()
+    print(f"sort M={M} V={V} pad={pad}: phases (us) " + " ".join(f"{(t[i + 1] - t[i]).item() / 100:.2f}" for i in range(5)), flush=True)

@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--out", default="gpurun_out/tuned_inmodel.json")
     ap.add_argument("--epi", type=lambda v: [int(x) for x in v.split(",")], default=None,
                     help="only GEMMs with these epilogues (e.g. 1,2: bias, bias+relu)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="time HIP-graph replays (one capture per candidate) instead of eager steps")
+    ap.add_argument("--cands", type=lambda v: [(int(x), 1) for x in v.split(",")], default=None,
+                    help="tile configs to try (default: CANDS)")
     args = ap.parse_args()
 
     dev = torch.device("cuda", 0)
@@ -71,6 +75,8 @@ def main():
     kk.gemm = orig
 
     def timed():
+        if args.graph:
+            step.capture(s, t)  # (the current table, captured)
         for _ in range(3):
             step(s, t)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -87,8 +93,10 @@ def main():
         M, N, K = key[:3]
         if 2.0 * M * N * K * calls < args.min_flops:
             continue
-        cands = list(CANDS)
         cur = kk._TUNED.get(key, (None,))[0]
+        cands = list(args.cands or CANDS)
+        if cur is not None and cur not in cands:
+            cands.append(cur)
         times = {c: [] for c in cands}
         for _ in range(args.rounds):
             for c in cands:

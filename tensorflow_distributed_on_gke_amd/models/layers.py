@@ -65,6 +65,9 @@ class RunCtx:
     fp8: Optional[object] = None
     # WgradQueue: weight gradients deferred to the end of backward (grouped)
     wgrad: Optional["WgradQueue"] = None
+    # {embedding site: ops.kernels.EmbCsr}: the token sorts of this forward's
+    # embedding backwards (one launch for both tables, Transformer.features)
+    emb_csr: Optional[dict] = None
 
     @property
     def p(self) -> float:
@@ -511,7 +514,8 @@ class EmbedFn(torch.autograd.Function):
         if tok.is_cuda:
             # training with dropout: the keep bits for the CSR backward
             ctx.kbits = None
-            if K.EMBED_CSR and K.DETERMINISTIC_EMBED and rt.training and rt.p > 0 and d % 512 == 0:
+            ctx.csr = rt.emb_csr.get(site) if rt.emb_csr else None
+            if ctx.csr is not None and rt.p > 0 and d % 512 == 0:
                 ctx.kbits = torch.empty(tok.numel(), d // 8, dtype=torch.uint8, device=tok.device)
             return K.embed_fwd(tok, table.compute, pe, scale, rt.p, rt.seed, rt.ctr, site,
                                kbits=ctx.kbits)
@@ -528,7 +532,7 @@ class EmbedFn(torch.autograd.Function):
         if dout.is_cuda:
             dc = dout.contiguous()
             K.embed_bwd(tok, dc, table.grad, ctx.scale, rt.p, rt.seed, rt.ctr, ctx.site,
-                        accumulate=rt.accumulate, kbits=ctx.kbits)
+                        accumulate=rt.accumulate, kbits=ctx.kbits, csr=ctx.csr)
             _ready(rt, table)
             return None, None, None, None, None, None
         else:

@@ -263,6 +263,15 @@ class Transformer:
 
     def features(self, src, tgt_in, rt: RunCtx, lengths=None):
         src_len, tgt_len = lengths if lengths is not None else (seq_lengths(src), seq_lengths(tgt_in))
+        rt.emb_csr = None
+        if (src.is_cuda and rt.training and torch.is_grad_enabled()
+                and K.embed_csr_ok(src.numel(), self.cfg.src_vocab)
+                and K.embed_csr_ok(tgt_in.numel(), self.cfg.tgt_vocab)):
+            # both embedding backwards' token sorts in one launch, now: the
+            # tokens are known (ops.kernels.EmbCsr)
+            cs = K.embed_csr_sort([(src, self.enc_emb.shape[0], "enc"),
+                                   (tgt_in, self.dec_emb.shape[0], "dec")])
+            rt.emb_csr = {self.enc_site: cs[0], self.dec_site: cs[1]}
         enc = self.encode(src, src_len, rt)
         return self.decode(tgt_in, enc, src_len, tgt_len, rt)
 

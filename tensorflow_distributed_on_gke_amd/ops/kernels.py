@@ -543,21 +543,50 @@ DETERMINISTIC_EMBED = os.environ.get("TDG_DETERMINISTIC", "1") != "0"
 EMBED_CSR = os.environ.get("TDG_EMBED_CSR", "1") != "0"
 
 
-def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False, kbits=None):
+class EmbCsr:
+    """The token sort of one table's CSR embedding backward (its work items in
+    an int32 workspace of its own, `name`)."""
+
+    def __init__(self, tok: torch.Tensor, V: int, name: str):
+        self.tok, self.V, self.M = tok, int(V), tok.numel()
+        n32, _ = C().embed_csr_ws(self.M, self.V, 128)
+        self.w32 = workspace("embed_csr32_" + name, n32, tok.device, torch.int32)
+
+
+def embed_csr_ok(M: int, V: int) -> bool:
+    return DETERMINISTIC_EMBED and EMBED_CSR and C().embed_csr_ok(M, V)
+
+
+def embed_csr_sort(tables, stamps=None) -> list:
+    """[(tok, V, name)] (one or two tables) -> [EmbCsr]: their token sorts in
+    one launch (one workgroup per table). stamps: lab phase clocks."""
+    cs = [EmbCsr(t.contiguous(), V, name) for t, V, name in tables]
+    C().embed_csr_sort([c.tok for c in cs], [c.V for c in cs], [c.w32 for c in cs], stamps)
+    return cs
+
+
+def embed_csr_apply(cs: EmbCsr, dout, dtable, scale, p, seed, ctr, site, accumulate=False,
+                    kbits=None) -> None:
+    """dtable (=|+=) the embedding gradient from a sorted table (bitwise the
+    fixed-point atomic path's)."""
+    _, n64 = C().embed_csr_ws(cs.M, cs.V, dtable.shape[1])
+    w64 = workspace("embed_csr64", n64, dtable.device, torch.int64)
+    C().embed_csr_apply(dout, dtable, cs.w32, w64, cs.M, scale, p, seed, ctr, site, accumulate, kbits)
+
+
+def embed_bwd(tok, dout, dtable, scale, p, seed, ctr, site, accumulate=False, kbits=None,
+              csr: Optional[EmbCsr] = None):
     """dtable (=|+=) scatter-add of the embedding gradient. Default: the
     deterministic paths (bitwise reproducible and bitwise equal to each
-    other): the CSR kernels, else fixed-point int64 atomics;
-    TDG_DETERMINISTIC=0 uses plain f32 atomics (dtable must then be zero
-    unless accumulating). kbits: the forward's keep bits (CSR path; else the
-    Philox mask is regenerated)."""
-    if DETERMINISTIC_EMBED and EMBED_CSR:
-        M, V, D = tok.numel(), dtable.shape[0], dtable.shape[1]
-        n32, n64 = C().embed_csr_ws(M, V, D)
-        w32 = workspace("embed_csr32", n32, dtable.device, torch.int32)
-        w64 = workspace("embed_csr64", n64, dtable.device, torch.int64)
-        if C().embed_bwd_csr(tok, dout, dtable, w32, w64, scale, p, seed, ctr, site, accumulate,
-                             kbits):
-            return
+    other): the CSR kernels (`csr`: the forward already sorted the tokens),
+    else fixed-point int64 atomics; TDG_DETERMINISTIC=0 uses plain f32
+    atomics (dtable must then be zero unless accumulating). kbits: the
+    forward's keep bits (CSR path; else the Philox mask is regenerated)."""
+    if csr is not None or embed_csr_ok(tok.numel(), dtable.shape[0]):
+        if csr is None:
+            csr = embed_csr_sort([(tok, dtable.shape[0], "bwd")])[0]
+        embed_csr_apply(csr, dout.contiguous(), dtable, scale, p, seed, ctr, site, accumulate, kbits)
+        return
     if DETERMINISTIC_EMBED:
         acc = workspace("embed_fx", dtable.numel(), dtable.device, torch.int64, zero=True)
         C().embed_bwd_det(tok, dout, dtable, acc, scale, p, seed, ctr, site, accumulate)

@@ -110,3 +110,26 @@ def test_embed_csr_forward_keep_bits(D):
     kk.embed_bwd(tok.to(DEV), dout, b, math.sqrt(D), 0.1, 99, ctr, 4)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_embed_csr_two_table_sort():
+    """Both tables sorted by one launch (the training forward's form), each
+    applied later: bitwise the fixed-point atomic gradients."""
+    g = torch.Generator().manual_seed(21)
+    D = 512
+    ctr = torch.tensor([5], dtype=torch.int64, device=DEV)
+    specs = [(7765, (64, 128)), (7010, (64, 127))]
+    toks = []
+    for V, (B, L) in specs:
+        t = torch.randint(1, V, (B, L), generator=g)
+        lens = torch.randint(5, L + 1, (B,), generator=g)
+        t[torch.arange(L)[None, :] >= lens[:, None]] = 0
+        toks.append(t.to(DEV))
+    cs = kk.embed_csr_sort([(toks[0], specs[0][0], "t0"), (toks[1], specs[1][0], "t1")])
+    for i, (V, (B, L)) in enumerate(specs):
+        dout = (torch.randn(B, L, D, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+        a = torch.zeros(V, D, device=DEV)
+        kk.embed_bwd(toks[i], dout, a, math.sqrt(D), 0.1, 99, ctr, 4, csr=cs[i])
+        b = _both(toks[i], dout, V, D, 0.1, False, torch.zeros(V, D, device=DEV))[1]
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), f"table {i}"
