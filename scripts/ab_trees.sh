@@ -8,7 +8,7 @@ mkdir -p $O
 for r in $(seq 1 $R); do
   for t in "$A" "$B"; do
     n=$(basename "$t")
-    (cd "$t" && timeout -k 10 300 python -u bench.py --steps 60 --warmup 15 > $O/${n}_$r.log 2>&1) || { echo "$t failed"; tail -5 $O/${n}_$r.log; exit 1; }
+    (cd "$t" && timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 60 --warmup 15} > $O/${n}_$r.log 2>&1) || { echo "$t failed"; tail -5 $O/${n}_$r.log; exit 1; }
     echo "[$n] run=$r $(tail -1 $O/${n}_$r.log | python -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])') ms/step"
   done
 done
