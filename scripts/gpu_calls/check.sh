@@ -32,7 +32,8 @@ bench big512_fp8 300 --preset big --seq-len 512 --local-batch 16 --dtype fp8 --s
 step profile
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pbase -o p -- python3 bench.py --steps 10 --warmup 3 --graph 0 > $O/pbase.log 2>&1 || { tail -20 $O/pbase.log; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p8 -o p -- python3 bench.py --preset big --seq-len 512 --local-batch 16 --dtype fp8 --steps 10 --warmup 3 --graph 0 > $O/p8.log 2>&1 || { tail -20 $O/p8.log; exit 1; }
-for d in pbase p8; do
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pbig -o p -- python3 bench.py --preset big --steps 10 --warmup 3 --graph 0 > $O/pbig.log 2>&1 || { tail -20 $O/pbig.log; exit 1; }
+for d in pbase p8 pbig; do
   f=$(find $O/$d -name "*kernel_stats.csv" | head -1)
   python3 scripts/kstats.py "$f" 13 > $O/$d.txt
   head -30 $O/$d.txt
