@@ -8,4 +8,4 @@ O=gpurun_out/tune
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 export TDG_NO_AUTOBUILD=1
-timeout -k 10 1000 python -u scripts/tune_in_model.py --preset $P --graph 1 --cands $C --rounds 3 --steps 20 --out $O/$P.json 2>&1 | tee $O/$P.log
+timeout -k 10 1000 python -u scripts/tune_in_model.py --preset $P --graph 1 --cands $C --rounds 3 --steps 20 ${TUNE_ARGS:-} --out $O/$P${TAG:-}.json 2>&1 | tee $O/$P${TAG:-}.log
