@@ -21,6 +21,7 @@ int tdg_gemm(const void* A, const void* B, void* C, const float* bias, const voi
 void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld, int rows_per_block,
                 float beta, hipStream_t st);
 int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
+int tdg_qkv_attn_fwd(const tdg::QkvAttnArgs* qa, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
 int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
@@ -290,6 +291,62 @@ void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   a.causal = causal;
   c10::DeviceGuard g(q.device());
   check_err(tdg_attn_fwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_fwd");
+}
+
+// Fused self-attention input projection + attention forward (L <= 128, hd
+// 64): qkv[M, 3d] = x2 @ w^T + bias (written for the backward) and out / lse
+// of the attention over it, in one launch. Returns false (nothing launched)
+// when the shape is not covered.
+bool qkv_attn_fwd(const Tensor& x2, const Tensor& w, const Tensor& bias, const Tensor& qkv,
+                  const Tensor& out, const Tensor& lse, const optional<Tensor>& kv_len,
+                  double scale, bool causal, int64_t B, int64_t heads) {
+  check_bf16(x2, "x2");
+  check_bf16(w, "w");
+  check_bf16(qkv, "qkv");
+  check_contig(qkv, "qkv");
+  check_f32(bias, "bias");
+  TORCH_CHECK(x2.dim() == 2 && w.dim() == 2 && x2.stride(1) == 1 && w.stride(1) == 1, "x2 / w rows");
+  const int64_t M = x2.size(0), d = x2.size(1);
+  TORCH_CHECK(M % B == 0 && w.size(0) == 3 * d && w.size(1) == d && bias.numel() >= 3 * d &&
+                  qkv.numel() == M * 3 * d,
+              "qkv_attn_fwd: shapes");
+  const int64_t L = M / B;
+  if (L > 128 || d != 64 * heads || d % 64 || x2.stride(0) % 8 || w.stride(0) % 8) return false;
+  for (const Tensor* t : {&x2, &w, &qkv})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "qkv_attn_fwd: 16-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(bias.data_ptr()) & 15) == 0, "bias 16-byte aligned");
+  tdg::QkvAttnArgs qa{};
+  tdg::AttnArgs& a = qa.a;
+  a.xcd = 0;
+  a.B = (int)B;
+  a.H = (int)heads;
+  a.Lq = a.Lk = (int)L;
+  check_like(out, a, a.Lq, "out");
+  check_f32(lse, "lse");
+  check_contig(lse, "lse");
+  TORCH_CHECK(lse.numel() == (int64_t)a.B * a.H * a.Lq, "lse must be [B,H,Lq]");
+  a.out = (uint16_t*)out.data_ptr();
+  a.o_sb = out.stride(0); a.o_sl = out.stride(1); a.o_sh = (int)out.stride(2);
+  a.lse = lse.data_ptr<float>();
+  if (kv_len.has_value()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == a.B, "kv_len: int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.scale = (float)scale;
+  a.causal = causal;
+  qa.x = (const uint16_t*)x2.data_ptr();
+  qa.w = (const uint16_t*)w.data_ptr();
+  qa.bias = bias.data_ptr<float>();
+  qa.qkv = (uint16_t*)qkv.data_ptr();
+  qa.d = (int)d;
+  qa.ldx = (int)x2.stride(0);
+  qa.ldw = (int)w.stride(0);
+  qa.L = (int)L;
+  c10::DeviceGuard g(x2.device());
+  const int rc = tdg_qkv_attn_fwd(&qa, stream_of(x2));
+  if (rc == -1) return false;
+  check_err(rc, "tdg qkv_attn_fwd");
+  return true;
 }
 
 // e4m3 forward: q8/k8/v8 are [B, L, H, 64] float8_e4m3fn views (hd
@@ -1471,6 +1528,7 @@ void to_bf16(const Tensor& p, const Tensor& o) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
+  m.def("qkv_attn_fwd", &qkv_attn_fwd);
   m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),

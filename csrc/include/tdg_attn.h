@@ -67,4 +67,16 @@ struct AttnArgs {
   // 0 = the plain grid order (one head per XCD)
   int xcd;
 };
+
+// Fused self-attention input projection + attention forward
+// (attention.hip qkv_attn_fwd_kernel): a's out / lse / kv_len / o strides /
+// B / H / Lq / Lk / scale / causal, plus the projection's operands
+struct QkvAttnArgs {
+  AttnArgs a;
+  const uint16_t* x;  // [B * L, d] bf16 (row stride ldx)
+  const uint16_t* w;  // [3d, d] bf16: Q rows, then K, then V (row stride ldw)
+  const float* bias;  // [3d]
+  uint16_t* qkv;      // [B * L, 3d] bf16 projection output (for the backward)
+  int d, ldx, ldw, L;
+};
 }  // namespace tdg

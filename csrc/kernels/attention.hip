@@ -2442,6 +2442,221 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
   for (int k = lane; k < a.Lk; k += 64) out[k] = k < klim ? out[k] * inv : 0.f;
 }
 
+// ============================================================================ fused Q|K|V projection + attention forward
+// Self-attention of sequences of <= 128 tokens at head dim 64: one workgroup
+// per (batch, head) computes the head's Q|K|V = X_b W_h^T + b_h (128 x 192,
+// K = d_model; the GEMM main loop of gemm_impl.h: LDS-DMA K tiles, 8 waves as
+// 2 x 4 of 64 x 48, MFMAs with swapped operands) and keeps them in LDS as the
+// attention's K / V images and Q rows, writes them to the [M, 3d] projection
+// output (the backward reads it), and runs the attention forward of
+// attn_fwd_kernel on them (8 waves x 16 queries, one 128-key tile). The
+// separate projection launch, its Q|K|V write and the attention's re-read of
+// them (the attention forward at L = 128 is a load burst + a short compute
+// phase) become one launch whose attention phase reads LDS.
+// (reference: transformer_model.py:112-166 -- the Q / K / V Dense layers and
+// scaled_dot_product_attention of MultiHeadAttention)
+template <int STAGES>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void qkv_attn_fwd_kernel(
+    const QkvAttnArgs qa) {
+  constexpr int NW = 8, WM = 2, WN = 4, BM = 128, BN = 192;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 4 x 3 subtiles per wave
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, SB = A_BYTES + B_BYTES;
+  using GA = Glds<true, BM, NW>;
+  using GB = Glds<true, BN, NW>;
+  constexpr int PT = GA::P + GB::P;
+  using T = ATile<64>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const AttnArgs& a = qa.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  // (head, batch): each XCD a contiguous run of batch elements, so a batch
+  // element's X panel is read into one XCD's L2 for its heads
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int h = t % a.H, b = t / a.H;
+  const int L = qa.L, d = qa.d, K = d;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(qa.x) + (size_t)b * L * qa.ldx;
+
+  // ------------------------------------------------ Q|K|V GEMM (K = d_model)
+  GA ga;
+  GB gb;
+  ga.init(wid, lane);
+  gb.init(wid, lane);
+  // B rows r of the tile: W row (r / 64) * d + 64 h + r % 64 (a 1 KiB piece
+  // covers 8 rows of one 64-row block)
+  int wrow[GB::P];
+#pragma unroll
+  for (int i = 0; i < GB::P; ++i) wrow[i] = (gb.row[i] >> 6) * d + 64 * h + (gb.row[i] & 63);
+  auto issue_b = [&](int k0, char* lds) {
+#pragma unroll
+    for (int i = 0; i < GB::P; ++i) {
+      const long long off = (long long)wrow[i] * qa.ldw + k0 + gb.col[i];
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const bf16_t*>(qa.w) + off),
+                                       (__attribute__((address_space(3))) void*)(lds + (wid * GB::P + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+  const int nk = K / BK;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < STAGES; ++st) {
+    if (st < nk) {
+      ga.issue(X, qa.ldx, L, K, 0, st * BK, smem + st * SB, wid);
+      issue_b(st * BK, smem + st * SB + A_BYTES);
+    }
+  }
+  const int abase = wm * (BM / WM), bbase = wn * (BN / WN);
+  short8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  if (nk >= STAGES)
+    wait_vmcnt<(STAGES - 1) * PT>();
+  else
+    wait_vmcnt<0>();
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa0[i] = frag<true, BM>(smem, abase + 16 * i, 0, lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb0[j] = frag<true, BN>(smem + A_BYTES, bbase + 16 * j, 0, lane);
+  constexpr int STEP_OPS = TM + TN;
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
+    const char* st = smem + (kt % STAGES) * SB;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa1[i] = frag<true, BM>(st, abase + 16 * i, 1, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb1[j] = frag<true, BN>(st + A_BYTES, bbase + 16 * j, 1, lane);
+    lgkm_wait<STEP_OPS>();
+    tie_all(fa0);
+    tie_all(fb0);
+    prio_hi();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb0[j], fa0[i], acc[i][j]);
+    prio_lo();
+    if constexpr (MODE >= 1) {
+      if constexpr (MODE >= 2) wait_vmcnt<(STAGES - 2) * PT>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+      const char* nx = smem + ((kt + 1) % STAGES) * SB;
+      if constexpr (MODE == 3) {
+        char* ns = smem + (kt % STAGES) * SB;
+        ga.issue(X, qa.ldx, L, K, 0, (kt + STAGES) * BK, ns, wid);
+        issue_b((kt + STAGES) * BK, ns + A_BYTES);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa0[i] = frag<true, BM>(nx, abase + 16 * i, 0, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb0[j] = frag<true, BN>(nx + A_BYTES, bbase + 16 * j, 0, lane);
+    } else {
+      lgkm_wait<0>();
+    }
+    tie_all(fa1);
+    tie_all(fb1);
+    prio_hi();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
+    prio_lo();
+  };
+  {
+    int kt = 0;
+    for (; kt + STAGES < nk; ++kt) kstep(kt, std::integral_constant<int, 3>{});
+    if (kt + STAGES - 1 < nk && kt + 1 < nk) kstep(kt++, std::integral_constant<int, 2>{});
+    for (; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<int, 1>{});
+    if (kt < nk) kstep(kt, std::integral_constant<int, 0>{});
+  }
+  lds_barrier();  // the pipeline stages become the Q / K / V images
+
+  // ------------------------------------------------ bias, bf16, LDS images
+  // image p (0 Q, 1 K, 2 V): 128 rows x 64 head dims in the attention's
+  // K-image layout (T::off over 128 rows = two 64-row tiles)
+  char* img = smem;
+  constexpr int IMG = 2 * T::BYTES;
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bbase + 16 * j + 4 * g;  // 4 consecutive columns of one image
+    const int part = n >> 6, hc = n & 63;
+    const f32x4 bn = *reinterpret_cast<const f32x4*>(qa.bias + part * d + 64 * h + hc);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = abase + 16 * i + cl;
+      short4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[i][j][r] + bn[r]);
+      *reinterpret_cast<short4_t*>(img + part * IMG + T::off(m, hc * 2)) = o;
+    }
+  }
+  __syncthreads();
+  // the projection output for the backward: rows < L, 16-byte chunks
+  {
+    const WtBuf wt(qa.qkv, ((size_t)(b + 1) * L * 3 * d) * sizeof(bf16_t));
+#pragma unroll
+    for (int pass = 0; pass < 3 * 128 * 8 / 512; ++pass) {
+      const int id = tid + 512 * pass;
+      const int part = id >> 10, row = (id >> 3) & 127, c = id & 7;
+      const short8_t v = *reinterpret_cast<const short8_t*>(img + part * IMG + T::off(row, c * 16));
+      if (row < L)
+        wt.st16(reinterpret_cast<bf16_t*>(qa.qkv) + ((size_t)b * L + row) * 3 * d + part * d + 64 * h + c * 8, v);
+    }
+  }
+
+  // ------------------------------------------------ attention (attn_fwd_kernel, 8 x 16 queries)
+  const char* ldsQ = img;
+  const char* ldsK = img + IMG;
+  const char* ldsV = img + 2 * IMG;
+  const int w = wid;
+  const int qrow = 16 * w + cl;
+  int klim;
+  float scl;
+  bool causal;
+  key_window(a, b, klim, scl, causal);
+  if (causal) klim = min(klim, 128);
+  const float c = scl * LOG2E;
+  const int wq0 = 16 * w;
+  short8_t qf[T::KS];
+#pragma unroll
+  for (int s2 = 0; s2 < T::KS; ++s2) qf[s2] = T::frag_row(ldsQ, 16 * w, s2, lane);
+  f32x4 oacc[T::DT];
+#pragma unroll
+  for (int i = 0; i < T::DT; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  constexpr int NT16 = 8;
+  if (klim > 0) {
+    f32x4 sc[NT16];
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt) {
+      sc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < T::KS; ++ks) sc[tt] = mfma16(T::frag_row(ldsK, 16 * tt, ks, lane), qf[ks], sc[tt]);
+    }
+    short8_t pf[NT16 / 2];
+    softmax_tile<NT16, T::DT>(sc, m, l, oacc, pf, tile_masked(0, 128, klim, causal, wq0), 0, klim, causal,
+                              qrow, g, c);
+#pragma unroll
+    for (int s2 = 0; s2 < NT16 / 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < T::DT; ++dt) oacc[dt] = mfma16(T::frag_tr(ldsV, s2, dt, lane), pf[s2], oacc[dt]);
+  }
+  {
+    float lu = rows_sum(l);
+    const bool ok = qrow < a.Lq;
+    const float inv = lu > 0.f ? 1.f / lu : 0.f;
+    bf16_t* op = a.out + b * a.o_sb + (long long)qrow * a.o_sl + h * a.o_sh;
+    uint32_t lo[T::DT], hi[T::DT];
+#pragma unroll
+    for (int dt = 0; dt < T::DT; ++dt) pack_acc(oacc[dt], inv, lo[dt], hi[dt]);
+    store_row16<T::DT>(op, lo, hi, g, ok);
+    if (ok && g == 0)
+      a.lse[((long long)b * a.H + h) * a.Lq + qrow] = lu > 0.f ? m + log2f(lu) : INFINITY;
+  }
+}
+
 }  // namespace tdg
 
 using namespace tdg;
@@ -2616,4 +2831,25 @@ extern "C" int tdg_attn_bwd_f8(const AttnArgs* a, int hd, hipStream_t st) {
 }
 extern "C" int tdg_attn_probs(const AttnArgs* a, int hd, float* probs, hipStream_t st) {
   TDG_HD_CASES(probs_hd, *a, probs, st)
+}
+
+// Fused Q|K|V projection + attention forward (qkv_attn_fwd_kernel): L <= 128,
+// hd 64, d % 64 == 0; 3 pipeline stages, one workgroup per CU (2 stages at
+// two workgroups per CU spilled and measured slower: 32.1 vs 26.8 us per call
+// at B 64, L 128, H 8; profiles/r6/qkv_attn_fwd.txt). Returns -1 when the
+// shape is not covered.
+extern "C" int tdg_qkv_attn_fwd(const QkvAttnArgs* qa, hipStream_t st) {
+  const AttnArgs& a = qa->a;
+  if (qa->L > 128 || qa->L <= 0 || a.Lq != qa->L || a.Lk != qa->L || qa->d % 64 || qa->d != 64 * a.H ||
+      qa->ldx % 8 || qa->ldw % 8)
+    return -1;
+  constexpr int STAGES = 3, SB = (128 + 192) * BK * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)qkv_attn_fwd_kernel<STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(qkv_attn_fwd_kernel<STAGES>, dim3(a.B * a.H), dim3(512), STAGES * SB, st, *qa);
+  return 0;
 }

@@ -1,0 +1,44 @@
+"""Per-call time (HIP events, back to back) of the fused Q|K|V projection +
+attention forward against the projection GEMM + attention forward it
+replaces, at the Transformer-base / big self-attention shapes."""
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk  # noqa: E402
+
+
+def t(fn, n=50):
+    for _ in range(5):
+        fn()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    for _ in range(n):
+        fn()
+    e[1].record()
+    e[1].synchronize()
+    return e[0].elapsed_time(e[1]) / n * 1000.0
+
+
+dev = "cuda"
+for B, L, H, causal in [(64, 128, 8, False), (64, 128, 8, True), (64, 128, 16, False)]:
+    d = 64 * H
+    x = torch.randn(B * L, d, device=dev).bfloat16()
+    w = (torch.randn(3 * d, d, device=dev) / math.sqrt(d)).bfloat16()
+    b = torch.randn(3 * d, device=dev) * 0.1
+    kv = torch.randint(L // 2, L + 1, (B,), device=dev, dtype=torch.int32)
+
+    def two():
+        q5 = kk.linear_fwd(x, w, b).view(B, L, 3, H, 64)
+        kk.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv, 0.125, causal)
+
+    def gemm_only():
+        kk.linear_fwd(x, w, b)
+
+    r = {"gemm": t(gemm_only), "gemm+attn": t(two)}
+    r["fused"] = t(lambda: kk.qkv_attn_fwd(x, w, b, B, H, kv, 0.125, causal))
+    print(f"B{B} L{L} H{H} causal={causal}: "
+          + "  ".join(f"{k}={v:.2f}us" for k, v in r.items()), flush=True)

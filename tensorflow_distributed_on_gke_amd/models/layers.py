@@ -597,12 +597,20 @@ class SelfAttnBlockFn(torch.autograd.Function):
             r = (rt.fp8.linear(x2, wqkv, bqkv, want8=f8, keep_x8=kx, want_y=not ctx.f8b)
                  if rt.fp8 is not None else None)
             qkv, qkv8 = (r[0], r[1]) if f8 and r is not None else (r, None)
+            fused = None
+            if qkv is None and not ctx.f8b and rt.fp8 is None and rt.attn_maps is None:
+                # projection + attention forward in one launch (L <= 128)
+                fused = K.qkv_attn_fwd(x2, wqkv.compute, bqkv.master, B, heads, kv_len, scale, causal)
+                if fused is not None:
+                    qkv = fused[0]
             if qkv is None and not ctx.f8b:
                 qkv = K.linear_fwd(x2, wqkv.compute, bqkv.master)  # [M, 3d]
             q5 = qkv.view(B, L, 3, heads, hd) if qkv is not None else None
             o8e = None
             ctx.q8 = None
-            if qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
+            if fused is not None:
+                o, aux = fused[1], fused[2]
+            elif qkv8 is not None:  # e4m3 attention on the projection's e4m3 output
                 q85 = qkv8.view(B, L, 3, heads, hd)
                 s8 = rt.fp8.meta.s(r[2])
                 ctx.q8 = (qkv8, r[2])  # (the fp8 attention backward's operands)

@@ -362,6 +362,27 @@ def attn_fwd(q, k, v, kv_len, scale: float, causal: bool):
     return out, lse
 
 
+# self-attention of <= 128 tokens: the Q|K|V projection and the attention
+# forward in one launch (attention.hip qkv_attn_fwd_kernel)
+QKV_ATTN = os.environ.get("TDG_QKV_ATTN", "1") != "0"
+
+
+def qkv_attn_fwd(x2, w, bias, B: int, heads: int, kv_len, scale: float, causal: bool):
+    """(qkv [M, 3d], out [B, L, H, hd], lse [B, H, L]) of the self-attention
+    over qkv = x2 @ w^T + bias, one launch; None when the shape is not covered
+    (L > 128, hd != 64)."""
+    M, d = x2.shape
+    L, hd = M // B, d // heads
+    if not QKV_ATTN or L > 128 or hd != 64:
+        return None
+    qkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=x2.device)
+    out = torch.empty(B, L, heads, hd, dtype=torch.bfloat16, device=x2.device)
+    lse = torch.empty(B, heads, L, dtype=torch.float32, device=x2.device)
+    if not C().qkv_attn_fwd(x2, w, bias, qkv, out, lse, kv_len, scale, causal, B, heads):
+        return None
+    return qkv, out, lse
+
+
 def attn_fwd_fp8_ok(Lq: int, Lk: int, hd: int) -> bool:
     """Shapes the e4m3 attention forward covers (attention.hip
     attn_fwd_fp8_kernel): hd 64, the long-sequence path."""

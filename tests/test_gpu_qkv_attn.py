@@ -1,0 +1,67 @@
+"""The fused self-attention input projection + attention forward
+(attention.hip qkv_attn_fwd_kernel: one launch per layer for sequences of
+<= 128 tokens) against the two-launch path it replaces -- the Q|K|V GEMM
+(linear_fwd) then attn_fwd on its output -- and the attention against a plain
+fp32 PyTorch softmax(Q K^T / sqrt(hd) + mask) V (reference:
+transformer_model.py:73-166, MultiHeadAttention with the padding / look-ahead
+masks)."""
+import math
+
+import pytest
+import torch
+
+from tensorflow_distributed_on_gke_amd.ops import kernels as kk
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _case(B, L, H, causal, lens, seed=0):
+    d = 64 * H
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(B * L, d, generator=g)).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(3 * d, d, generator=g) / math.sqrt(d)).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(3 * d, generator=g) * 0.1).to(DEV)
+    kv = torch.tensor(lens, dtype=torch.int32, device=DEV) if lens is not None else None
+    return x, w, b, kv, d
+
+
+@pytest.mark.parametrize("B,L,H,causal,pad", [
+    (64, 128, 8, False, True), (64, 128, 8, True, True), (16, 100, 8, False, True),
+    (8, 37, 8, True, False), (16, 128, 16, False, True), (4, 128, 8, False, False),
+])
+def test_qkv_attn_matches_two_launches(B, L, H, causal, pad):
+    g = torch.Generator().manual_seed(B + L)
+    lens = torch.randint(1, L + 1, (B,), generator=g).tolist() if pad else None
+    if pad:
+        lens[0] = 0  # an all-padding row: the reference's uniform softmax
+    x, w, b, kv, d = _case(B, L, H, causal, lens)
+    hd = 64
+    scale = 1.0 / math.sqrt(hd)
+    r = kk.qkv_attn_fwd(x, w, b, B, H, kv, scale, causal)
+    assert r is not None
+    qkv, o, lse = r
+    qkv0 = kk.linear_fwd(x, w, b)
+    q5 = qkv0.view(B, L, 3, H, hd)
+    o0, lse0 = kk.attn_fwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv, scale, causal)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv, qkv0), "projection output differs from the GEMM's"
+    assert torch.equal(o, o0), f"O differs: {(o.float() - o0.float()).abs().max().item()}"
+    assert torch.equal(lse, lse0)
+    # fp32 reference of the attention on the (bf16) projection output
+    qf, kf, vf = (q5[:, :, i].float().permute(0, 2, 1, 3) for i in range(3))
+    s = qf @ kf.transpose(-1, -2) * scale
+    mask = torch.zeros(B, 1, L, L, device=DEV)
+    if kv is not None:
+        mask = mask + (torch.arange(L, device=DEV)[None, None, None, :] >= kv[:, None, None, None]).float()
+    if causal:
+        mask = torch.maximum(mask, torch.triu(torch.ones(L, L, device=DEV), 1)[None, None])
+    p = torch.softmax(s + mask * -1e9, dim=-1)
+    ref = (p @ vf).permute(0, 2, 1, 3)
+    err = (o.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-3, err
+
+
+def test_qkv_attn_declines_long_sequences():
+    x, w, b, kv, d = _case(2, 200, 8, False, None)
+    assert kk.qkv_attn_fwd(x, w, b, 2, 8, None, 0.125, False) is None
