@@ -22,6 +22,7 @@ void tdg_colsum(const void* X, float* out, float* part, int M, int N, int ld, in
                 float beta, hipStream_t st);
 int tdg_attn_fwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_qkv_attn_fwd(const tdg::QkvAttnArgs* qa, hipStream_t st);
+int tdg_attn_bwd_fdo(const tdg::AttnArgs* a, hipStream_t st);
 int tdg_attn_bwd(const tdg::AttnArgs* a, int hd, hipStream_t st);
 int tdg_attn_probs(const tdg::AttnArgs* a, int hd, float* probs, hipStream_t st);
 int tdg_attn_fwd_fp8(const tdg::AttnArgs* a, int hd, hipStream_t st);
@@ -464,6 +465,39 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   tdg::AttnArgs a = attn_bwd_args(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal);
   c10::DeviceGuard g(q.device());
   check_err(tdg_attn_bwd(&a, (int)q.size(3), stream_of(q)), "tdg attn_bwd");
+}
+
+// attn_bwd with the output-projection dgrad in-kernel: dO = dy2 @ wo[:, head
+// columns] per (batch, head) (dy2 [B * Lq, d], wo [d, d] bf16), never
+// written to memory. Returns false (nothing launched) when not covered
+// (Lq / Lk > 128, hd != 64).
+bool attn_bwd_fdo(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                  const Tensor& dy2, const Tensor& wo, const Tensor& lse, const Tensor& delta,
+                  const Tensor& dq, const Tensor& dk, const Tensor& dv,
+                  const optional<Tensor>& kv_len, double scale, bool causal) {
+  // (o stands in for dout in the checks: the kernel computes dO itself)
+  tdg::AttnArgs a = attn_bwd_args(q, k, v, o, o, lse, delta, dq, dk, dv, kv_len, scale, causal);
+  a.dout = nullptr;
+  check_bf16(dy2, "dy2");
+  check_bf16(wo, "wo");
+  const int64_t d = wo.size(1);
+  TORCH_CHECK(dy2.dim() == 2 && wo.dim() == 2 && dy2.stride(1) == 1 && wo.stride(1) == 1 &&
+                  dy2.size(0) == (int64_t)a.B * a.Lq && dy2.size(1) == d && wo.size(0) == d,
+              "attn_bwd_fdo: dy2 [B * Lq, d], wo [d, d]");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(dy2.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(wo.data_ptr()) & 15) == 0,
+              "attn_bwd_fdo: 16-byte aligned operands");
+  if (q.size(3) != 64 || a.Lq > 128 || a.Lk > 128 || d != 64 * a.H) return false;
+  a.fdo_dy = (const uint16_t*)dy2.data_ptr();
+  a.fdo_w = (const uint16_t*)wo.data_ptr();
+  a.fdo_d = (int)d;
+  a.fdo_ldy = (int)dy2.stride(0);
+  a.fdo_ldw = (int)wo.stride(0);
+  c10::DeviceGuard g(q.device());
+  const int rc = tdg_attn_bwd_fdo(&a, stream_of(q));
+  if (rc == -1) return false;
+  check_err(rc, "tdg attn_bwd_fdo");
+  return true;
 }
 
 // attn_bwd that also emits e5m2 copies of dQ (and of dK / dV when given),
@@ -1529,6 +1563,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
   m.def("qkv_attn_fwd", &qkv_attn_fwd);
+  m.def("attn_bwd_fdo", &attn_bwd_fdo);
   m.def("gemm_grouped", &gemm_grouped);
   m.def("gemm_ragged", &gemm_ragged, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("shapes"),
         py::arg("K"), py::arg("a_kc"), py::arg("b_kc"), py::arg("alpha"), py::arg("beta"),

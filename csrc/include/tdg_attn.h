@@ -66,6 +66,12 @@ struct AttnArgs {
   // xcd_remap'd tiles do: their Q/K/V / dO tiles are then in that XCD's L2),
   // 0 = the plain grid order (one head per XCD)
   int xcd;
+  // fused backward with the output-projection dgrad (attn_bwd_fused_kernel
+  // FDO): dO_bh = dY_b [Lq rows, d] @ Wo[:, 64 h ..] computed in-kernel
+  // (dout unused); dY rows b * Lq + r (row stride fdo_ldy), Wo [d][d]
+  const uint16_t* fdo_dy;
+  const uint16_t* fdo_w;
+  int fdo_d, fdo_ldy, fdo_ldw;
 };
 
 // Fused self-attention input projection + attention forward

@@ -1684,8 +1684,105 @@ struct DsImg {
   }
 };
 
-template <int HD, int U>
+// dO tile of the fused backward with the output-projection dgrad (FDO):
+// dO_bh [128 x 64] = dY_b [128 rows, d] @ Wo[:, 64 h .. 64 h + 63], K = d,
+// on 8 waves as 4 x 2 of 32 x 32 -- the main loop of gemm_impl.h's
+// gemm_kernel (3 LDS-DMA stages of 64-deep K tiles, swapped-operand MFMAs,
+// the same k order per element as the standalone NN dgrad, so the bf16 dO is
+// bitwise that kernel's). Uses smem[0, 3 * 24 KiB); returns the accumulators.
+constexpr int FDO_STAGES = 3, FDO_SB = (128 + 64) * BK * 2;
+__device__ __forceinline__ void fdo_tile(const AttnArgs& a, int b, int h, char* smem, int wid,
+                                         int lane, f32x4 (&acc)[2][2]) {
+  constexpr int NW = 8, BM = 128, BN = 64, WN = 2, TM = 2, TN = 2, STAGES = FDO_STAGES;
+  constexpr int A_BYTES = BM * BK * 2, SB = FDO_SB;
+  using GA = Glds<true, BM, NW>;
+  using GB = Glds<false, BN, NW>;
+  constexpr int PT = GA::P + GB::P;
+  const int wm = wid / WN, wn = wid % WN;
+  const int K = a.fdo_d;
+  const bf16_t* Y = reinterpret_cast<const bf16_t*>(a.fdo_dy) + (size_t)b * a.Lq * a.fdo_ldy;
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(a.fdo_w) + 64 * h;
+  GA ga;
+  GB gb;
+  ga.init(wid, lane);
+  gb.init(wid, lane);
+  const int nk = K / BK;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < STAGES; ++st) {
+    if (st < nk) {
+      ga.issue(Y, a.fdo_ldy, a.Lq, K, 0, st * BK, smem + st * SB, wid);
+      gb.issue(W, a.fdo_ldw, BN, K, 0, st * BK, smem + st * SB + A_BYTES, wid);
+    }
+  }
+  const int abase = wm * (BM / 4), bbase = wn * (BN / WN);
+  short8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  if (nk >= STAGES)
+    wait_vmcnt<(STAGES - 1) * PT>();
+  else
+    wait_vmcnt<0>();
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa0[i] = frag<true, BM>(smem, abase + 16 * i, 0, lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb0[j] = frag<false, BN>(smem + A_BYTES, bbase + 16 * j, 0, lane);
+  constexpr int STEP_OPS = TM * frag_ops<true>() + TN * frag_ops<false>();
+  auto kstep = [&](int kt, auto modec) {
+    constexpr int MODE = decltype(modec)::value;
+    const char* st = smem + (kt % STAGES) * SB;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa1[i] = frag<true, BM>(st, abase + 16 * i, 1, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb1[j] = frag<false, BN>(st + A_BYTES, bbase + 16 * j, 1, lane);
+    lgkm_wait<STEP_OPS>();
+    tie_all(fa0);
+    tie_all(fb0);
+    prio_hi();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb0[j], fa0[i], acc[i][j]);
+    prio_lo();
+    if constexpr (MODE >= 1) {
+      if constexpr (MODE >= 2) wait_vmcnt<(STAGES - 2) * PT>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+      const char* nx = smem + ((kt + 1) % STAGES) * SB;
+      if constexpr (MODE == 3) {
+        char* ns = smem + (kt % STAGES) * SB;
+        ga.issue(Y, a.fdo_ldy, a.Lq, K, 0, (kt + STAGES) * BK, ns, wid);
+        gb.issue(W, a.fdo_ldw, BN, K, 0, (kt + STAGES) * BK, ns + A_BYTES, wid);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa0[i] = frag<true, BM>(nx, abase + 16 * i, 0, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb0[j] = frag<false, BN>(nx + A_BYTES, bbase + 16 * j, 0, lane);
+    } else {
+      lgkm_wait<0>();
+    }
+    tie_all(fa1);
+    tie_all(fb1);
+    prio_hi();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
+    prio_lo();
+  };
+  int kt = 0;
+  for (; kt + STAGES < nk; ++kt) kstep(kt, std::integral_constant<int, 3>{});
+  if (kt + STAGES - 1 < nk && kt + 1 < nk) kstep(kt++, std::integral_constant<int, 2>{});
+  for (; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<int, 1>{});
+  if (kt < nk) kstep(kt, std::integral_constant<int, 0>{});
+  lds_barrier();  // the stages are free for the attention's images
+}
+
+template <int HD, int U, bool FDO = false>
 __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 ? (HD <= 64 ? 4 : 2) : 2))) void attn_bwd_fused_kernel(AttnArgs a) {
+  static_assert(!FDO || (HD == 64 && U == 1), "in-kernel dO: hd 64, 8 waves");
   using T = ATile<HD>;
   using TS = DsImg;  // dS image: 128 key rows x 128 queries (bf16)
   constexpr int R = 128;
@@ -1747,13 +1844,13 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
       if constexpr (TOTAL % NT == 0) {  // (clamped rows, zeroed: no branch per load)
         const int rq = min(row, a.Lq - 1), rk = min(row, a.Lk - 1);
         vq[i] = ld8_or0(qb + (long long)rq * a.q_sl + cc * 8, row < a.Lq);
-        vo[i] = ld8_or0(ob + (long long)rq * a.do_sl + cc * 8, row < a.Lq);
+        if constexpr (!FDO) vo[i] = ld8_or0(ob + (long long)rq * a.do_sl + cc * 8, row < a.Lq);
         vx[i] = ld8_or0(obo + (long long)rq * a.o_sl + cc * 8, row < a.Lq);
         vk[i] = ld8_or0(kbp + (long long)rk * a.k_sl + cc * 8, row < a.Lk);
       } else {
         if (id < TOTAL && row < a.Lq) {
           vq[i] = *reinterpret_cast<const short8_t*>(qb + (long long)row * a.q_sl + cc * 8);
-          vo[i] = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
+          if constexpr (!FDO) vo[i] = *reinterpret_cast<const short8_t*>(ob + (long long)row * a.do_sl + cc * 8);
           vx[i] = *reinterpret_cast<const short8_t*>(obo + (long long)row * a.o_sl + cc * 8);
         }
         if (id < TOTAL && row < a.Lk)
@@ -1761,13 +1858,38 @@ __global__ __launch_bounds__(512 / U) __attribute__((amdgpu_waves_per_eu(U == 1 
       }
     }
     const float lse_v = (tid < R && tid < a.Lq) ? a.lse[((long long)b * a.H + h) * a.Lq + tid] : INFINITY;
+    if constexpr (FDO) {
+      // dO from the in-kernel output-projection dgrad (rows >= Lq zero, as
+      // the loads above give them), into its image; then read back in the
+      // chunk layout for delta
+      f32x4 acc[2][2];
+      fdo_tile(a, b, h, smem, w, lane, acc);
+      const int wm = w / 2, wn = w % 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int m = 32 * wm + 16 * i + cl, n = 32 * wn + 16 * j + 4 * g;
+          short4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = m < a.Lq ? (short)f2bf(acc[i][j][r]) : (short)0;
+          *reinterpret_cast<short4_t*>(ldsO + T::off(m, n * 2)) = o;
+        }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int id = tid + i * NT;
+        const int row = id / CPR, cc = id % CPR;
+        if (id < TOTAL) vo[i] = *reinterpret_cast<const short8_t*>(ldsO + T::off(row, cc * 16));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int id = tid + i * NT;
       const int row = id / CPR, cc = id % CPR;
       if (id < TOTAL) {
         *reinterpret_cast<short8_t*>(ldsQ + T::off(row, cc * 16)) = vq[i];
-        *reinterpret_cast<short8_t*>(ldsO + T::off(row, cc * 16)) = vo[i];
+        if constexpr (!FDO) *reinterpret_cast<short8_t*>(ldsO + T::off(row, cc * 16)) = vo[i];
         *reinterpret_cast<short8_t*>(ldsK + T::off(row, cc * 16)) = vk[i];
       }
       // delta[row] = sum_d dO * O: partial over this chunk, then over the
@@ -2709,6 +2831,29 @@ constexpr int fused_bwd_lds() {
   return (2 * TB >= SB ? 3 * TB : 3 * TB + SB) + 2 * 128 * 4;
 }
 
+template <int HD>
+int bwd_hd(const AttnArgs& a, hipStream_t st);
+}  // namespace
+
+// Fused backward with the output-projection dgrad in-kernel (FDO): Lq, Lk <=
+// 128, hd 64, d = 64 H. Returns -1 when not covered.
+extern "C" int tdg_attn_bwd_fdo(const AttnArgs* ap, hipStream_t st) {
+  const AttnArgs& a = *ap;
+  if (a.Lq > 128 || a.Lk > 128 || a.fdo_d != 64 * a.H || a.fdo_d % BK || a.fdo_ldy % 8 ||
+      a.fdo_ldw % 8 || !a.fdo_dy || !a.fdo_w)
+    return -1;
+  constexpr int lds = fused_bwd_lds<64>() > FDO_STAGES * FDO_SB ? fused_bwd_lds<64>() : FDO_STAGES * FDO_SB;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<64, 1, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_fused_kernel<64, 1, true>), dim3(a.B * a.H), dim3(512), lds, st, a);
+  return 0;
+}
+
+namespace {
 template <int HD>
 int bwd_hd(const AttnArgs& a, hipStream_t st) {
   if (a.Lq <= 128 && a.Lk <= 128) {

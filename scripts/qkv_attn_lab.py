@@ -42,3 +42,25 @@ for B, L, H, causal in [(64, 128, 8, False), (64, 128, 8, True), (64, 128, 16, F
     r["fused"] = t(lambda: kk.qkv_attn_fwd(x, w, b, B, H, kv, 0.125, causal))
     print(f"B{B} L{L} H{H} causal={causal}: "
           + "  ".join(f"{k}={v:.2f}us" for k, v in r.items()), flush=True)
+
+# backward: output-projection dgrad + attention backward vs the in-kernel dO
+for B, L, H, causal in [(64, 128, 8, False), (64, 128, 8, True), (64, 128, 16, False)]:
+    d = 64 * H
+    q, k, v = (torch.randn(B, L, H, 64, device=dev).bfloat16() for _ in range(3))
+    kv = torch.randint(L // 2, L + 1, (B,), device=dev, dtype=torch.int32)
+    o, lse = kk.attn_fwd(q, k, v, kv, 0.125, causal)
+    dy2 = (torch.randn(B * L, d, device=dev) * 0.1).bfloat16()
+    wo = (torch.randn(d, d, device=dev) / math.sqrt(d)).bfloat16()
+    dq, dk, dv = (torch.empty_like(x) for x in (q, k, v))
+
+    def two():
+        do = kk.linear_dgrad(dy2, wo, d)
+        kk.attn_bwd(q, k, v, o, do.view(B, L, H, 64), lse, dq, dk, dv, kv, 0.125, causal)
+
+    def attn_only():
+        kk.attn_bwd(q, k, v, o, o, lse, dq, dk, dv, kv, 0.125, causal)
+
+    r = {"attn_bwd": t(attn_only), "dgrad+attn_bwd": t(two),
+         "fused": t(lambda: kk.attn_bwd_fdo(q, k, v, o, dy2, wo, lse, dq, dk, dv, kv, 0.125, causal))}
+    print(f"bwd B{B} L{L} H{H} causal={causal}: " + "  ".join(f"{k_}={v_:.2f}us" for k_, v_ in r.items()),
+          flush=True)

@@ -656,11 +656,15 @@ class SelfAttnBlockFn(torch.autograd.Function):
         q5 = qkv.view(B, L, 3, heads, hd)
         if dy.is_cuda:
             _wgrad(rt, ds2, o.view(M, d), d, wo)
-            do = K.linear_dgrad(ds2, wo.compute, d)
             dqkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=dy.device)
             g5 = dqkv.view(B, L, 3, heads, hd)
-            K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
-                       g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
+            # (L <= 128: the output projection's dgrad dO = ds @ Wo inside the
+            # attention backward)
+            if not K.attn_bwd_fdo(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, ds2, wo.compute, aux,
+                                  g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal):
+                do = K.linear_dgrad(ds2, wo.compute, d)
+                K.attn_bwd(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, do.view(B, L, heads, hd), aux,
+                           g5[:, :, 0], g5[:, :, 1], g5[:, :, 2], kv_len, scale, causal)
             _wgrad(rt, dqkv, x2, 3 * d, wqkv, bqkv)
             dx = _dgrad_res(dqkv, wqkv, 3 * d, dh)
             if rt.wgrad is not None:
@@ -1012,11 +1016,14 @@ class CrossAttnBlockFn(torch.autograd.Function):
         ds2 = ds.reshape(M, d)
         if dy.is_cuda:
             _wgrad(rt, ds2, o.view(M, d), d, wo)
-            do = K.linear_dgrad(ds2, wo.compute, d)
             dq = torch.empty(M, d, dtype=torch.bfloat16, device=dy.device)
-            K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
-                       do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
-                       g5[:, :, 1], kv_len, scale, False)
+            if not K.attn_bwd_fdo(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o, ds2,
+                                  wo.compute, aux, dq.view(B, T, heads, hd), g5[:, :, 0],
+                                  g5[:, :, 1], kv_len, scale, False):
+                do = K.linear_dgrad(ds2, wo.compute, d)
+                K.attn_bwd(q.view(B, T, heads, hd), kv5[:, :, 0], kv5[:, :, 1], o,
+                           do.view(B, T, heads, hd), aux, dq.view(B, T, heads, hd), g5[:, :, 0],
+                           g5[:, :, 1], kv_len, scale, False)
             _wgrad(rt, dq, x2, d, wq, bq)
         else:
             _write_grad(wo, ds2.t() @ o.reshape(M, d), rt)

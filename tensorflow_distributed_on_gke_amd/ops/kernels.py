@@ -407,6 +407,20 @@ def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, kv_len, scale: float, causal: bo
     C().attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, kv_len, scale, causal)
 
 
+# the fused backward of <= 128-token attention computes dO = dY @ Wo[:, head]
+# itself (the output projection's dgrad, never written to memory)
+ATTN_BWD_FDO = os.environ.get("TDG_ATTN_BWD_FDO", "1") != "0"
+
+
+def attn_bwd_fdo(q, k, v, o, dy2, wo, lse, dq, dk, dv, kv_len, scale: float, causal: bool) -> bool:
+    """attn_bwd with dout = (dy2 @ wo).view(q.shape) computed in-kernel; False
+    (nothing launched) when not covered (Lq / Lk > 128, hd != 64)."""
+    if not ATTN_BWD_FDO:
+        return False
+    delta = workspace("attn_delta", lse.numel(), q.device)[: lse.numel()]
+    return C().attn_bwd_fdo(q, k, v, o, dy2, wo, lse, delta, dq, dk, dv, kv_len, scale, causal)
+
+
 def attn_bwd_g8_ok(Lq: int, Lk: int, hd: int) -> bool:
     """Shapes whose attention backward can emit e5m2 gradients (the hd-64
     pipelined kernels, attention.hip attn_emit_g8)."""

@@ -65,3 +65,37 @@ def test_qkv_attn_matches_two_launches(B, L, H, causal, pad):
 def test_qkv_attn_declines_long_sequences():
     x, w, b, kv, d = _case(2, 200, 8, False, None)
     assert kk.qkv_attn_fwd(x, w, b, 2, 8, None, 0.125, False) is None
+
+
+@pytest.mark.parametrize("B,Lq,Lk,H,causal,pad", [
+    (64, 128, 128, 8, False, True), (64, 128, 128, 8, True, True), (16, 100, 100, 8, False, True),
+    (8, 37, 37, 8, True, False), (16, 128, 128, 16, False, True), (16, 127, 128, 8, False, True),
+])
+def test_attn_bwd_fdo_matches_two_launches(B, Lq, Lk, H, causal, pad):
+    """The fused backward with the output-projection dgrad in-kernel
+    (attn_bwd_fused_kernel FDO) against linear_dgrad + attn_bwd: bitwise."""
+    d, hd = 64 * H, 64
+    g = torch.Generator().manual_seed(B * Lq + H)
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(torch.bfloat16).to(DEV)  # noqa: E731
+    q, k, v = mk(B, Lq, H, hd), mk(B, Lk, H, hd), mk(B, Lk, H, hd)
+    lens = torch.randint(1, Lk + 1, (B,), generator=g) if pad else None
+    if pad:
+        lens[0] = 0
+    kv = lens.to(torch.int32).to(DEV) if pad else None
+    scale = 1.0 / math.sqrt(hd)
+    o, lse = kk.attn_fwd(q, k, v, kv, scale, causal and Lq == Lk)
+    causal = causal and Lq == Lk
+    dy2 = mk(B * Lq, d, sc=0.1)
+    wo = mk(d, d, sc=1.0 / math.sqrt(d))
+    outs = []
+    for fused in (True, False):
+        dq, dk, dv = (torch.empty_like(t) for t in (q, k, v))
+        if fused:
+            assert kk.attn_bwd_fdo(q, k, v, o, dy2, wo, lse, dq, dk, dv, kv, scale, causal)
+        else:
+            do = kk.linear_dgrad(dy2, wo, d)
+            kk.attn_bwd(q, k, v, o, do.view(B, Lq, H, hd), lse, dq, dk, dv, kv, scale, causal)
+        outs.append((dq, dk, dv))
+    torch.cuda.synchronize()
+    for a, b, n in zip(outs[0], outs[1], ("dq", "dk", "dv")):
+        assert torch.equal(a, b), f"{n}: {(a.float() - b.float()).abs().max().item()}"
