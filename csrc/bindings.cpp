@@ -300,7 +300,13 @@ void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
 // when the shape is not covered.
 bool qkv_attn_fwd(const Tensor& x2, const Tensor& w, const Tensor& bias, const Tensor& qkv,
                   const Tensor& out, const Tensor& lse, const optional<Tensor>& kv_len,
-                  double scale, bool causal, int64_t B, int64_t heads) {
+                  double scale, bool causal, int64_t B, int64_t heads,
+                  const optional<Tensor>& k, const optional<Tensor>& v) {
+  // k / v given: the cross-attention form (w / bias / qkv = the Q
+  // projection's; k / v the [B, Lk, H, 64] views of the batched K|V)
+  const bool cross = k.has_value();
+  TORCH_CHECK(cross == v.has_value(), "qkv_attn_fwd: k and v together");
+  const int np = cross ? 1 : 3;
   check_bf16(x2, "x2");
   check_bf16(w, "w");
   check_bf16(qkv, "qkv");
@@ -308,8 +314,8 @@ bool qkv_attn_fwd(const Tensor& x2, const Tensor& w, const Tensor& bias, const T
   check_f32(bias, "bias");
   TORCH_CHECK(x2.dim() == 2 && w.dim() == 2 && x2.stride(1) == 1 && w.stride(1) == 1, "x2 / w rows");
   const int64_t M = x2.size(0), d = x2.size(1);
-  TORCH_CHECK(M % B == 0 && w.size(0) == 3 * d && w.size(1) == d && bias.numel() >= 3 * d &&
-                  qkv.numel() == M * 3 * d,
+  TORCH_CHECK(M % B == 0 && w.size(0) == np * d && w.size(1) == d && bias.numel() >= np * d &&
+                  qkv.numel() == M * np * d,
               "qkv_attn_fwd: shapes");
   const int64_t L = M / B;
   if (L > 128 || d != 64 * heads || d % 64 || x2.stride(0) % 8 || w.stride(0) % 8) return false;
@@ -318,10 +324,31 @@ bool qkv_attn_fwd(const Tensor& x2, const Tensor& w, const Tensor& bias, const T
   TORCH_CHECK((reinterpret_cast<uintptr_t>(bias.data_ptr()) & 15) == 0, "bias 16-byte aligned");
   tdg::QkvAttnArgs qa{};
   tdg::AttnArgs& a = qa.a;
+  if (cross) {
+    for (const Tensor* t : {&*k, &*v}) {
+      check_bf16(*t, "k/v");
+      TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1 && t->size(0) == B && t->size(2) == heads &&
+                      t->size(3) == 64 && t->size(1) == k->size(1),
+                  "qkv_attn_fwd: k / v [B, Lk, H, 64], head dim contiguous");
+      TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) == 0 && t->stride(0) % 8 == 0 &&
+                      t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0,
+                  "qkv_attn_fwd: k / v rows 16-byte aligned");
+    }
+    a.B = (int)B;
+    a.H = (int)heads;
+    a.Lk = (int)k->size(1);
+    a.k = (const uint16_t*)k->data_ptr();
+    a.v = (const uint16_t*)v->data_ptr();
+    a.k_sb = k->stride(0); a.k_sl = k->stride(1); a.k_sh = (int)k->stride(2);
+    a.v_sb = v->stride(0); a.v_sl = v->stride(1); a.v_sh = (int)v->stride(2);
+    if (a.Lk > 128) return false;
+  } else {
+    a.B = (int)B;
+    a.H = (int)heads;
+    a.Lk = (int)L;
+  }
   a.xcd = 0;
-  a.B = (int)B;
-  a.H = (int)heads;
-  a.Lq = a.Lk = (int)L;
+  a.Lq = (int)L;
   check_like(out, a, a.Lq, "out");
   check_f32(lse, "lse");
   check_contig(lse, "lse");
@@ -343,6 +370,7 @@ bool qkv_attn_fwd(const Tensor& x2, const Tensor& w, const Tensor& bias, const T
   qa.ldx = (int)x2.stride(0);
   qa.ldw = (int)w.stride(0);
   qa.L = (int)L;
+  qa.cross = cross;
   c10::DeviceGuard g(x2.device());
   const int rc = tdg_qkv_attn_fwd(&qa, stream_of(x2));
   if (rc == -1) return false;

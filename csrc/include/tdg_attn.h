@@ -84,5 +84,8 @@ struct QkvAttnArgs {
   const float* bias;  // [3d]
   uint16_t* qkv;      // [B * L, 3d] bf16 projection output (for the backward)
   int d, ldx, ldw, L;
+  // cross-attention: w / bias / qkv are the Q projection's ([d, d], [d],
+  // [B * L, d]); K / V are a.k / a.v (the batched K|V projection), Lk = a.Lk
+  int cross;
 };
 }  // namespace tdg

@@ -2577,11 +2577,15 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 // phase) become one launch whose attention phase reads LDS.
 // (reference: transformer_model.py:112-166 -- the Q / K / V Dense layers and
 // scaled_dot_product_attention of MultiHeadAttention)
-template <int STAGES>
+// CROSS (cross-attention): the GEMM is the head's Q projection only (128 x
+// 64, 8 waves as 4 x 2 of 32 x 32) and K / V come from the batched K|V
+// projection in memory (a.k / a.v), their loads issued before the GEMM.
+template <int STAGES, bool CROSS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void qkv_attn_fwd_kernel(
     const QkvAttnArgs qa) {
-  constexpr int NW = 8, WM = 2, WN = 4, BM = 128, BN = 192;
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 4 x 3 subtiles per wave
+  constexpr int NW = 8, WM = CROSS ? 4 : 2, WN = CROSS ? 2 : 4, BM = 128, BN = CROSS ? 64 : 192;
+  constexpr int NPART = BN / 64;                      // projection parts computed here
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 4 x 3 (2 x 2) subtiles per wave
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, SB = A_BYTES + B_BYTES;
   using GA = Glds<true, BM, NW>;
   using GB = Glds<true, BN, NW>;
@@ -2598,6 +2602,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
   const int h = t % a.H, b = t / a.H;
   const int L = qa.L, d = qa.d, K = d;
   const bf16_t* X = reinterpret_cast<const bf16_t*>(qa.x) + (size_t)b * L * qa.ldx;
+  // cross-attention K / V (128 keys each, two 64-row tiles): global loads now,
+  // LDS after the GEMM
+  using Ch = typename ATile<64>::template Chunks<512>;
+  Ch ck[2], cv[2];
+  if constexpr (CROSS) {
+    const bf16_t* kb = a.k + b * a.k_sb + h * a.k_sh;
+    const bf16_t* vb = a.v + b * a.v_sb + h * a.v_sh;
+#pragma unroll
+    for (int h64 = 0; h64 < 2; ++h64) {
+      ATile<64>::template fetch<512>(ck[h64], kb, a.k_sl, 64 * h64, a.Lk, tid);
+      ATile<64>::template fetch<512>(cv[h64], vb, a.v_sl, 64 * h64, a.Lk, tid);
+    }
+  }
 
   // ------------------------------------------------ Q|K|V GEMM (K = d_model)
   GA ga;
@@ -2700,6 +2717,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
   char* img = smem;
   constexpr int IMG = 2 * T::BYTES;
   const int g = lane >> 4, cl = lane & 15;
+  if constexpr (CROSS) {
+#pragma unroll
+    for (int h64 = 0; h64 < 2; ++h64) {
+      ATile<64>::template put<512>(img + IMG + h64 * T::BYTES, ck[h64], tid);
+      ATile<64>::template put<512>(img + 2 * IMG + h64 * T::BYTES, cv[h64], tid);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = bbase + 16 * j + 4 * g;  // 4 consecutive columns of one image
@@ -2715,16 +2739,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     }
   }
   __syncthreads();
-  // the projection output for the backward: rows < L, 16-byte chunks
+  // the projection output for the backward ([M, NPART d]): rows < L,
+  // 16-byte chunks
   {
-    const WtBuf wt(qa.qkv, ((size_t)(b + 1) * L * 3 * d) * sizeof(bf16_t));
+    const WtBuf wt(qa.qkv, ((size_t)(b + 1) * L * NPART * d) * sizeof(bf16_t));
 #pragma unroll
-    for (int pass = 0; pass < 3 * 128 * 8 / 512; ++pass) {
+    for (int pass = 0; pass < NPART * 128 * 8 / 512; ++pass) {
       const int id = tid + 512 * pass;
       const int part = id >> 10, row = (id >> 3) & 127, c = id & 7;
       const short8_t v = *reinterpret_cast<const short8_t*>(img + part * IMG + T::off(row, c * 16));
       if (row < L)
-        wt.st16(reinterpret_cast<bf16_t*>(qa.qkv) + ((size_t)b * L + row) * 3 * d + part * d + 64 * h + c * 8, v);
+        wt.st16(reinterpret_cast<bf16_t*>(qa.qkv) + ((size_t)b * L + row) * NPART * d + part * d + 64 * h + c * 8,
+                v);
     }
   }
 
@@ -2981,20 +3007,31 @@ extern "C" int tdg_attn_probs(const AttnArgs* a, int hd, float* probs, hipStream
 // Fused Q|K|V projection + attention forward (qkv_attn_fwd_kernel): L <= 128,
 // hd 64, d % 64 == 0; 3 pipeline stages, one workgroup per CU (2 stages at
 // two workgroups per CU spilled and measured slower: 32.1 vs 26.8 us per call
-// at B 64, L 128, H 8; profiles/r6/qkv_attn_fwd.txt). Returns -1 when the
-// shape is not covered.
-extern "C" int tdg_qkv_attn_fwd(const QkvAttnArgs* qa, hipStream_t st) {
-  const AttnArgs& a = qa->a;
-  if (qa->L > 128 || qa->L <= 0 || a.Lq != qa->L || a.Lk != qa->L || qa->d % 64 || qa->d != 64 * a.H ||
-      qa->ldx % 8 || qa->ldw % 8)
-    return -1;
-  constexpr int STAGES = 3, SB = (128 + 192) * BK * 2;
+// at B 64, L 128, H 8; profiles/r6/attn_fused_projections.txt). qa->cross:
+// the cross-attention form (Q projection only, K / V from a.k / a.v, Lk <=
+// 128). Returns -1 when the shape is not covered.
+namespace {
+template <bool CROSS>
+void qkv_attn_launch(const QkvAttnArgs& qa, hipStream_t st) {
+  constexpr int STAGES = 3, SB = (128 + (CROSS ? 64 : 192)) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)qkv_attn_fwd_kernel<STAGES>,
+    hipFuncSetAttribute((const void*)qkv_attn_fwd_kernel<STAGES, CROSS>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(qkv_attn_fwd_kernel<STAGES>, dim3(a.B * a.H), dim3(512), STAGES * SB, st, *qa);
+  hipLaunchKernelGGL((qkv_attn_fwd_kernel<STAGES, CROSS>), dim3(qa.a.B * qa.a.H), dim3(512),
+                     STAGES * SB, st, qa);
+}
+}  // namespace
+extern "C" int tdg_qkv_attn_fwd(const QkvAttnArgs* qa, hipStream_t st) {
+  const AttnArgs& a = qa->a;
+  if (qa->L > 128 || qa->L <= 0 || a.Lq != qa->L || a.Lk > 128 || a.Lk <= 0 || qa->d % 64 ||
+      qa->d != 64 * a.H || qa->ldx % 8 || qa->ldw % 8 || (!qa->cross && a.Lk != qa->L))
+    return -1;
+  if (qa->cross)
+    qkv_attn_launch<true>(*qa, st);
+  else
+    qkv_attn_launch<false>(*qa, st);
   return 0;
 }

@@ -12,7 +12,7 @@ rc=$?; tail -2 $O/pytest.log
 [ $rc -eq 0 ] || { grep -B5 -A30 "Error\|assert" $O/pytest.log | head -80; exit $rc; }
 echo "== lab"
 timeout -k 10 200 python -u scripts/qkv_attn_lab.py > $O/lab.log 2>&1 || { tail -20 $O/lab.log; exit 1; }
-grep "^B\|^bwd" $O/lab.log
+grep "^B\|^bwd\|^cross" $O/lab.log
 [ "${AB:-1}" = "1" ] || exit 0
 echo "== pytest model/graph"
 timeout -k 10 400 python -u -m pytest -q --maxfail=5 --timeout 200 --timeout-method thread -m gpu tests/test_gpu_model.py tests/test_gpu_graph.py > $O/pytest2.log 2>&1

@@ -64,3 +64,20 @@ for B, L, H, causal in [(64, 128, 8, False), (64, 128, 8, True), (64, 128, 16, F
          "fused": t(lambda: kk.attn_bwd_fdo(q, k, v, o, dy2, wo, lse, dq, dk, dv, kv, 0.125, causal))}
     print(f"bwd B{B} L{L} H{H} causal={causal}: " + "  ".join(f"{k_}={v_:.2f}us" for k_, v_ in r.items()),
           flush=True)
+
+# cross-attention forward: Q projection + attention vs the fused form
+for B, L, H in [(64, 128, 8), (64, 128, 16)]:
+    d = 64 * H
+    x = torch.randn(B * L, d, device=dev).bfloat16()
+    w = (torch.randn(d, d, device=dev) / math.sqrt(d)).bfloat16()
+    b = torch.randn(d, device=dev) * 0.1
+    kv5 = torch.randn(B, L, 2, H, 64, device=dev).bfloat16()
+    kv = torch.randint(L // 2, L + 1, (B,), device=dev, dtype=torch.int32)
+
+    def two():
+        q = kk.linear_fwd(x, w, b)
+        kk.attn_fwd(q.view(B, L, H, 64), kv5[:, :, 0], kv5[:, :, 1], kv, 0.125, False)
+
+    r = {"qproj+attn": t(two),
+         "fused": t(lambda: kk.qkv_attn_fwd(x, w, b, B, H, kv, 0.125, False, k=kv5[:, :, 0], v=kv5[:, :, 1]))}
+    print(f"cross B{B} L{L} H{H}: " + "  ".join(f"{k_}={v_:.2f}us" for k_, v_ in r.items()), flush=True)

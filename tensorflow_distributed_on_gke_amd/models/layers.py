@@ -883,10 +883,19 @@ class CrossAttnBlockFn(torch.autograd.Function):
             r = (rt.fp8.linear(x2, wq, bq, want8=f8, keep_x8=kx, want_y=not ctx.f8b)
                  if rt.fp8 is not None else None)
             q, q8 = (r[0], r[1]) if f8 and r is not None else (r, None)
+            fused = None
+            if q is None and not ctx.f8b and rt.fp8 is None and rt.attn_maps is None and kv5 is not None:
+                # Q projection + attention forward in one launch (<= 128 tokens)
+                fused = K.qkv_attn_fwd(x2, wq.compute, bq.master, B, heads, kv_len, scale, False,
+                                       k=kv5[:, :, 0], v=kv5[:, :, 1])
+                if fused is not None:
+                    q = fused[0]
             if q is None and not ctx.f8b:
                 q = K.linear_fwd(x2, wq.compute, bq.master)
             ctx.q8 = None
-            if q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
+            if fused is not None:
+                o, aux = fused[1], fused[2]
+            elif q8 is not None:  # e4m3 attention: e4m3 Q and the batched e4m3 K|V
                 kv8, kvs = rt.fp8.kv8
                 if kv8.shape != kv_all.shape:
                     raise RuntimeError(f"fp8 cross K|V {tuple(kv8.shape)} is not this forward's "

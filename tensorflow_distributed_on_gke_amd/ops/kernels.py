@@ -367,18 +367,21 @@ def attn_fwd(q, k, v, kv_len, scale: float, causal: bool):
 QKV_ATTN = os.environ.get("TDG_QKV_ATTN", "1") != "0"
 
 
-def qkv_attn_fwd(x2, w, bias, B: int, heads: int, kv_len, scale: float, causal: bool):
+def qkv_attn_fwd(x2, w, bias, B: int, heads: int, kv_len, scale: float, causal: bool,
+                 k=None, v=None):
     """(qkv [M, 3d], out [B, L, H, hd], lse [B, H, L]) of the self-attention
     over qkv = x2 @ w^T + bias, one launch; None when the shape is not covered
-    (L > 128, hd != 64)."""
+    (L > 128, hd != 64). k / v ([B, Lk, H, 64] views): the cross-attention
+    form -- w / bias the Q projection's, the first result q [M, d]."""
     M, d = x2.shape
     L, hd = M // B, d // heads
-    if not QKV_ATTN or L > 128 or hd != 64:
+    if not QKV_ATTN or L > 128 or hd != 64 or (k is not None and k.shape[1] > 128):
         return None
-    qkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=x2.device)
+    np_ = 1 if k is not None else 3
+    qkv = torch.empty(M, np_ * d, dtype=torch.bfloat16, device=x2.device)
     out = torch.empty(B, L, heads, hd, dtype=torch.bfloat16, device=x2.device)
     lse = torch.empty(B, heads, L, dtype=torch.float32, device=x2.device)
-    if not C().qkv_attn_fwd(x2, w, bias, qkv, out, lse, kv_len, scale, causal, B, heads):
+    if not C().qkv_attn_fwd(x2, w, bias, qkv, out, lse, kv_len, scale, causal, B, heads, k, v):
         return None
     return qkv, out, lse
 

@@ -99,3 +99,38 @@ def test_attn_bwd_fdo_matches_two_launches(B, Lq, Lk, H, causal, pad):
     torch.cuda.synchronize()
     for a, b, n in zip(outs[0], outs[1], ("dq", "dk", "dv")):
         assert torch.equal(a, b), f"{n}: {(a.float() - b.float()).abs().max().item()}"
+
+
+@pytest.mark.parametrize("B,T,S,H,pad", [(64, 128, 128, 8, True), (16, 100, 77, 8, True),
+                                         (8, 37, 128, 16, False), (4, 128, 64, 8, True)])
+def test_cross_q_attn_matches_two_launches(B, T, S, H, pad):
+    """The cross-attention form of the fused forward (Q projection in-kernel,
+    K / V from the batched K|V projection) against linear_fwd + attn_fwd."""
+    d, hd = 64 * H, 64
+    g = torch.Generator().manual_seed(B * T + S)
+    x = torch.randn(B * T, d, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(d, d, generator=g) / math.sqrt(d)).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(d, generator=g) * 0.1).to(DEV)
+    layers = 3  # the batched K|V buffer of several decoder layers: [B, S, layers * 2d]
+    kv_all = torch.randn(B, S, layers * 2 * d, generator=g).to(torch.bfloat16).to(DEV)
+    kv5 = kv_all[:, :, 2 * d:4 * d].view(B, S, 2, H, hd)
+    lens = torch.randint(1, S + 1, (B,), generator=g) if pad else None
+    if pad:
+        lens[0] = 0
+    kv = lens.to(torch.int32).to(DEV) if pad else None
+    scale = 1.0 / math.sqrt(hd)
+    r = kk.qkv_attn_fwd(x, w, b, B, H, kv, scale, False, k=kv5[:, :, 0], v=kv5[:, :, 1])
+    assert r is not None
+    q, o, lse = r
+    q0 = kk.linear_fwd(x, w, b)
+    o0, lse0 = kk.attn_fwd(q0.view(B, T, H, hd), kv5[:, :, 0], kv5[:, :, 1], kv, scale, False)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q0)
+    if T > 64 or S <= 64:
+        assert torch.equal(o, o0), f"O differs: {(o.float() - o0.float()).abs().max().item()}"
+        assert torch.equal(lse, lse0)
+    else:
+        # (attn_fwd takes <= 64 queries in 64-key tiles with the online-softmax
+        # rescale, the fused kernel all keys in one tile: rounding differs)
+        assert (o.float() - o0.float()).abs().max().item() <= 1e-2 * o0.float().abs().max().item()
+        assert (lse - lse0).abs().max().item() <= 1e-4 * lse0[lse0.isfinite()].abs().max().item()
