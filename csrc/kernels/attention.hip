@@ -2580,8 +2580,10 @@ __global__ void attn_probs_kernel(AttnArgs a, float* __restrict__ probs) {
 // CROSS (cross-attention): the GEMM is the head's Q projection only (128 x
 // 64, 8 waves as 4 x 2 of 32 x 32) and K / V come from the batched K|V
 // projection in memory (a.k / a.v), their loads issued before the GEMM.
-template <int STAGES, bool CROSS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void qkv_attn_fwd_kernel(
+// SB1: single-buffered fragments and a two-barrier K loop (the register
+// budget of two workgroups per CU), STAGES = 2.
+template <int STAGES, bool CROSS, bool SB1 = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SB1 ? 4 : 2))) void qkv_attn_fwd_kernel(
     const QkvAttnArgs qa) {
   constexpr int NW = 8, WM = CROSS ? 4 : 2, WN = CROSS ? 2 : 4, BM = 128, BN = CROSS ? 64 : 192;
   constexpr int NPART = BN / 64;                      // projection parts computed here
@@ -2649,6 +2651,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     }
   }
   const int abase = wm * (BM / WM), bbase = wn * (BN / WN);
+  if constexpr (SB1) {
+    short8_t fa[TM], fb[TN];
+    for (int kt = 0; kt < nk; ++kt) {
+      // tile kt landed (the younger tile, if any, stays in flight)
+      if (kt + 1 < nk) wait_vmcnt<PT>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+      const char* st = smem + (kt % STAGES) * SB;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag<true, BM>(st, abase + 16 * i, s2, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag<true, BN>(st + A_BYTES, bbase + 16 * j, s2, lane);
+        lgkm_wait<0>();
+        tie_all(fa);
+        tie_all(fb);
+        prio_hi();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+        prio_lo();
+      }
+      lds_barrier();  // everyone done with the stage: refill it
+      if (kt + STAGES < nk) {
+        char* ns = smem + (kt % STAGES) * SB;
+        ga.issue(X, qa.ldx, L, K, 0, (kt + STAGES) * BK, ns, wid);
+        issue_b((kt + STAGES) * BK, ns + A_BYTES);
+      }
+    }
+  } else {
   short8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
   if (nk >= STAGES)
     wait_vmcnt<(STAGES - 1) * PT>();
@@ -2708,6 +2742,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     if (kt + STAGES - 1 < nk && kt + 1 < nk) kstep(kt++, std::integral_constant<int, 2>{});
     for (; kt + 1 < nk; ++kt) kstep(kt, std::integral_constant<int, 1>{});
     if (kt < nk) kstep(kt, std::integral_constant<int, 0>{});
+  }
   }
   lds_barrier();  // the pipeline stages become the Q / K / V images
 
@@ -3005,24 +3040,27 @@ extern "C" int tdg_attn_probs(const AttnArgs* a, int hd, float* probs, hipStream
 }
 
 // Fused Q|K|V projection + attention forward (qkv_attn_fwd_kernel): L <= 128,
-// hd 64, d % 64 == 0; 3 pipeline stages, one workgroup per CU (2 stages at
-// two workgroups per CU spilled and measured slower: 32.1 vs 26.8 us per call
-// at B 64, L 128, H 8; profiles/r6/attn_fused_projections.txt). qa->cross:
+// hd 64, d % 64 == 0. Self-attention: 2 stages, single-buffered fragments,
+// two workgroups per CU (116 VGPRs): 21.5 us per call at B 64, L 128, H 8
+// against 25.7 for 3 stages with double-buffered fragments at one workgroup
+// per CU (144 VGPRs; with 2 stages and double buffering it spilled, 32.1 us;
+// profiles/r6/attn_fused_projections.txt). qa->cross:
 // the cross-attention form (Q projection only, K / V from a.k / a.v, Lk <=
 // 128). Returns -1 when the shape is not covered.
 namespace {
-template <bool CROSS>
+template <int STAGES, bool CROSS, bool SB1>
 void qkv_attn_launch(const QkvAttnArgs& qa, hipStream_t st) {
-  constexpr int STAGES = 3, SB = (128 + (CROSS ? 64 : 192)) * BK * 2;
+  constexpr int SB = (128 + (CROSS ? 64 : 192)) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)qkv_attn_fwd_kernel<STAGES, CROSS>,
+    hipFuncSetAttribute((const void*)qkv_attn_fwd_kernel<STAGES, CROSS, SB1>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((qkv_attn_fwd_kernel<STAGES, CROSS>), dim3(qa.a.B * qa.a.H), dim3(512),
+  hipLaunchKernelGGL((qkv_attn_fwd_kernel<STAGES, CROSS, SB1>), dim3(qa.a.B * qa.a.H), dim3(512),
                      STAGES * SB, st, qa);
 }
+
 }  // namespace
 extern "C" int tdg_qkv_attn_fwd(const QkvAttnArgs* qa, hipStream_t st) {
   const AttnArgs& a = qa->a;
@@ -3030,8 +3068,8 @@ extern "C" int tdg_qkv_attn_fwd(const QkvAttnArgs* qa, hipStream_t st) {
       qa->d != 64 * a.H || qa->ldx % 8 || qa->ldw % 8 || (!qa->cross && a.Lk != qa->L))
     return -1;
   if (qa->cross)
-    qkv_attn_launch<true>(*qa, st);
+    qkv_attn_launch<3, true, false>(*qa, st);
   else
-    qkv_attn_launch<false>(*qa, st);
+    qkv_attn_launch<2, false, true>(*qa, st);
   return 0;
 }
