@@ -1,3 +1,6 @@
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <vector>
 // Python bindings for the gfx950 kernels (module `_C`).
 // Every op launches on the current HIP stream of the tensors' device, takes
@@ -104,6 +107,9 @@ int tdg_adam_chunks(float* p, float* g, float* m, float* v, void* shadow, long l
 int tdg_to_bf16(const float* p, void* o, long long n, hipStream_t st);
 int tdg_transpose_grouped(const void* const* src, void* const* dst, int G, int R, int C,
                           hipStream_t st);
+int tdg_signal_create(unsigned long long** host, unsigned long long** dhost,
+                      unsigned long long** cnt);
+int tdg_signal_emit(unsigned long long* cnt, unsigned long long* dhost, hipStream_t st);
 }
 
 namespace {
@@ -1585,11 +1591,60 @@ void to_bf16(const Tensor& p, const Tensor& o) {
             "tdg to_bf16");
 }
 
+// ---- stream-position signal (csrc/kernels/signal.hip, parallel/ddp.py)
+// (host word, its device address, device counter) as integers
+std::vector<int64_t> signal_create() {
+  unsigned long long *h = nullptr, *d = nullptr, *c = nullptr;
+  const int rc = tdg_signal_create(&h, &d, &c);
+  TORCH_CHECK(rc == 0, "signal_create failed (rc=", rc, ")");
+  return {reinterpret_cast<int64_t>(h), reinterpret_cast<int64_t>(d), reinterpret_cast<int64_t>(c)};
+}
+
+// launches the signal kernel on the current stream of `device` (captured
+// into a graph when the stream is capturing)
+void signal_emit(int64_t dhost, int64_t cnt, int64_t device) {
+  hipStream_t st = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device)).stream();
+  const int rc = tdg_signal_emit(reinterpret_cast<unsigned long long*>(cnt),
+                                 reinterpret_cast<unsigned long long*>(dhost), st);
+  TORCH_CHECK(rc == 0, "signal_emit: launch failed");
+}
+
+// Spins (pause, then yield) until the host word reaches `expected`; false on
+// timeout. Runs without the GIL: the comm thread waits here while the main
+// thread keeps launching.
+bool signal_wait(int64_t host, int64_t expected, double timeout_s) {
+  py::gil_scoped_release nogil;
+  const volatile unsigned long long* p = reinterpret_cast<const volatile unsigned long long*>(host);
+  const unsigned long long want = static_cast<unsigned long long>(expected);
+  const auto t0 = std::chrono::steady_clock::now();
+  unsigned spins = 0;
+  while (*p < want) {
+    if (++spins < 4096) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    spins = 0;
+    std::this_thread::yield();
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      return false;
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
+}
+
+int64_t signal_read(int64_t host) {
+  return static_cast<int64_t>(*reinterpret_cast<const volatile unsigned long long*>(host));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for tensorflow_distributed_on_gke_amd";
   m.def("gemm", &gemm);
+  m.def("signal_create", &signal_create);
+  m.def("signal_emit", &signal_emit);
+  m.def("signal_wait", &signal_wait);
+  m.def("signal_read", &signal_read);
   m.def("qkv_attn_fwd", &qkv_attn_fwd);
   m.def("attn_bwd_fdo", &attn_bwd_fdo);
   m.def("gemm_grouped", &gemm_grouped);

@@ -700,3 +700,29 @@ def adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup,
          weight_decay=0.0, sched=1, zero_grad=True, inc_step=True):
     C().adam(p, g, m, v, shadow, step, beta1, beta2, eps, lr_const, d_model, warmup, grad_scale,
              weight_decay, sched, zero_grad, inc_step)
+
+
+# ------------------------------------------------------------------ stream signal
+class StreamSignal:
+    """A host-visible position marker on a HIP stream (csrc/kernels/signal.hip):
+    emit() enqueues a one-wave kernel that bumps a device counter and publishes
+    it to a coherent pinned host word; wait(n) spins (GIL released) until the
+    n-th emitted kernel has run. Captured into a HIP graph, each replay
+    publishes again, so a host thread can follow a graph's progress without
+    the graph being cut or an event recorded (parallel/ddp.py's comm thread)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device.index if device.index is not None else torch.cuda.current_device()
+        with torch.cuda.device(self.device):
+            self._host, self._dhost, self._cnt = C().signal_create()
+        # emits handed to the host side so far (the value the next wait expects)
+        self.expected = 0
+
+    def emit(self) -> None:
+        C().signal_emit(self._dhost, self._cnt, self.device)
+
+    def wait(self, n: int, timeout_s: float) -> bool:
+        return C().signal_wait(self._host, n, timeout_s)
+
+    def value(self) -> int:
+        return C().signal_read(self._host)

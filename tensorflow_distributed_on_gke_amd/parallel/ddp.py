@@ -23,7 +23,10 @@ reached the span's issue point, so communication overlaps the rest of backward
 without the communication stream ever waiting on the compute stream on the
 GPU (that handoff costs the compute stream ~55 us per span on MI355X); the
 compute stream waits on the finished all-reduce device-side, and the host only
-waits until the collective has been enqueued. Large spans (tens of MB) are what a
+waits until the collective has been enqueued. In the segmented HIP graph the
+issue point is a signal kernel inside the graph (ops/kernels.StreamSignal) the
+thread spins on, so issuing costs no graph cut and no event record
+(DP_SIGNAL; one-rank step 4.58 -> 4.54 ms, profiles/r6/dp_signal_issue.txt). Large spans (tens of MB) are what a
 ring all-reduce over point-to-point xGMI needs to spread over RCCL's channels
 and the 7 links per GPU.
 """
@@ -68,9 +71,16 @@ ISSUE_JITTER_MS = float(os.environ.get("TDG_DP_ISSUE_JITTER_MS", "0") or 0)
 # timeout (parallel/dist.py). A stall is reported every ISSUE_REPORT_S.
 COMM_ISSUE_TIMEOUT_S = PG_TIMEOUT_S
 ISSUE_REPORT_S = 60.0
+# Segmented graph + comm thread: mark issue points with a signal kernel inside
+# the graph (ops/kernels.StreamSignal) instead of cutting the graph and
+# recording an event there ("0": the event cut).
+DP_SIGNAL = os.environ.get("TDG_DP_SIGNAL", "1") != "0"
+
+
 class CommThread:
     """Issues the data-parallel collectives from one host thread, each once the
-    compute-stream event recorded at its issue point has completed, on a
+    compute stream has passed its issue point (an event recorded there, or in
+    a segmented graph the StreamSignal kernel captured there), on a
     communication stream that never waits on the compute stream on the GPU.
 
     Why: on MI355X a stream waiting on an event still pending on another
@@ -86,6 +96,11 @@ class CommThread:
         self.device = device
         self.cuda = device.type == "cuda"
         self.stream = torch.cuda.Stream(device) if self.cuda else None
+        self.signal = None
+        if self.cuda and DP_SIGNAL:
+            from tensorflow_distributed_on_gke_amd.ops.kernels import StreamSignal
+
+            self.signal = StreamSignal(device)
         self._q: "queue.Queue[Optional[Callable[[], None]]]" = queue.Queue()
         self._t = threading.Thread(target=self._run, name="tdg-comm", daemon=True)
         self._t.start()
@@ -297,6 +312,11 @@ class DataParallel:
         grp = self.group
         th = self._thread
 
+        # under a segmented capture with the comm thread: no cut at the issue
+        # point -- a signal kernel captured here tells the thread when the
+        # span is final, and the job is handed over before the graph replays
+        sig = (th.signal if th is not None and self.recorder is not None else None)
+
         def issue():
             self._check_poison()
             self._outstanding += 1
@@ -304,8 +324,11 @@ class DataParallel:
                 h.work = dist.all_reduce(t, group=grp, async_op=True)
                 return
             cuda = th.cuda
-            ready = None
-            if cuda:
+            ready = expect = None
+            if sig is not None:
+                sig.expected += 1
+                expect = sig.expected
+            elif cuda:
                 ready = torch.cuda.Event()
                 ready.record()  # the current (compute) stream: t is final here
             h.issued = threading.Event()
@@ -319,7 +342,12 @@ class DataParallel:
                         import time
                         time.sleep(random.uniform(0.0, jitter) / 1e3)
                     if cuda:
-                        ready.synchronize()
+                        if sig is not None:
+                            if not sig.wait(expect, COMM_ISSUE_TIMEOUT_S):
+                                raise RuntimeError(f"stream signal {expect} not reached within "
+                                                   f"{COMM_ISSUE_TIMEOUT_S:.0f} s (at {sig.value()})")
+                        else:
+                            ready.synchronize()
                         with torch.cuda.stream(th.stream):
                             w = dist.all_reduce(t, group=grp, async_op=True)
                             w.wait()  # comm stream after the collective
@@ -337,7 +365,10 @@ class DataParallel:
 
             th.submit(job)
 
-        if self.recorder is not None:
+        if sig is not None:
+            sig.emit()  # captured at the issue point
+            self.recorder.pre(issue)
+        elif self.recorder is not None:
             self.recorder.cut(issue)
         else:
             issue()

@@ -10,6 +10,11 @@ everything between them:
     graph 0 | all_reduce(span 0) | graph 1 | all_reduce(span 1) | ... |
     wait(span 0) | graph k (Adam of span 0) | wait(span 1) | ...
 
+With the host comm thread (parallel/ddp.py) an issue point does not cut the
+graph at all: a signal kernel captured at that point tells the thread when
+the span is final, and the thread's job is handed over before the graph is
+replayed (pre()). Only the waits remain as cuts.
+
 While the step is captured, every point where the data-parallel code would
 issue or wait for a collective ends the current graph and records the host
 call instead; replay launches the graphs and the recorded calls in the same
@@ -40,6 +45,8 @@ class SegmentedGraph:
         self.pool = pool
         self.items: List[Tuple[str, object]] = []
         self._cur: Optional[torch.cuda.CUDAGraph] = None
+        # host calls to replay before the graph now being captured (pre())
+        self._pre: List[Callable[[], None]] = []
         self.capturing = False
 
     # ------------------------------------------------------------------ capture
@@ -65,6 +72,8 @@ class SegmentedGraph:
         with torch.cuda.stream(self.stream), warnings.catch_warnings():
             warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
             self._cur.capture_end()
+        self.items.extend(("call", fn) for fn in self._pre)
+        self._pre = []
         self.items.append(("graph", self._cur))
         self._cur = None
 
@@ -76,6 +85,15 @@ class SegmentedGraph:
         self._close()
         self.items.append(("call", fn))
         self._open()
+
+    def pre(self, fn: Callable[[], None]) -> None:
+        """Record `fn` as a host call replayed just BEFORE the graph now being
+        captured, without cutting it: for work the host hands off ahead of
+        the GPU (a comm-thread job that waits for a signal kernel captured
+        later in this same graph, parallel/ddp.py)."""
+        if not self.capturing:
+            raise RuntimeError("SegmentedGraph.pre outside a capture")
+        self._pre.append(fn)
 
     def end(self) -> None:
         self._close()
@@ -92,6 +110,7 @@ class SegmentedGraph:
             self._cur = None
         self.capturing = False
         self.items = []
+        self._pre = []
 
     # ------------------------------------------------------------------ replay
     @property
