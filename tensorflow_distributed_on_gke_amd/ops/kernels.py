@@ -310,7 +310,7 @@ RAGGED_MAX_PROBLEMS, RAGGED_MAX_SHAPES = 64, 8
 # main loop of the ragged weight-gradient launch: 0 = lock-step 256x256 tiles
 # at 2 waves per SIMD (gemm256_kernel), 1 / 2 = the pipelined loop at one wave
 # per SIMD with a 4 / 5-slot LDS ring (wgrad_pipe_kernel)
-WGRAD_IMPL = 0
+WGRAD_IMPL = int(os.environ.get("TDG_WGRAD_IMPL", "0") or 0)
 
 
 def wgrad_ragged(dys, xs, dws, beta: float = 0.0, biases=None, ranges=None) -> None:
