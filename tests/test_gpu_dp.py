@@ -40,10 +40,11 @@ def _batch(rank, i):
     return src, tgt
 
 
-def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1", comm_bf16=False):
+def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1", comm_bf16=False,
+            signal="1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TDG_DIST_BACKEND="gloo",
-                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD=comm_thread)
+                      TDG_DP_GRAPH=graph or "0", TDG_DP_COMM_THREAD=comm_thread, TDG_DP_SIGNAL=signal)
     from tensorflow_distributed_on_gke_amd.train import step as step_mod
     step_mod.WAVE_TILES = 37  # small waves: problems cut across launches
     step_mod.DP_OVERLAP_OPT = opt_mode
@@ -60,6 +61,8 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1",
     opt = Adam(m.store, m.cfg.d_model, **ADAM)
     ddp = DataParallel(m.store, bucket_mb=1.0, comm_dtype=torch.bfloat16 if comm_bf16 else None)
     assert (ddp._thread is not None) == (comm_thread == "force")
+    if ddp._thread is not None:  # issue points in a segmented graph: signal kernel or cut + event
+        assert (ddp._thread.signal is not None) == (signal != "0")
     ddp.broadcast_params(0)
     step = TrainStep(m, opt, ddp, workers=world, seed=5, loss_mode=loss_mode)
     assert step.global_mean == (loss_mode == "global_mean")
@@ -69,6 +72,9 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1",
         assert step.capture(src.to(info.device), tgt.to(info.device))  # trains nothing
         assert step.segments is not None and step.segments.num_calls >= 2
         assert opt.iterations == 0
+        if ddp._thread is not None and signal != "0":
+            # one signal per span, issue jobs handed over before their segment
+            assert ddp._thread.signal.value() == 0
     losses = []
     for i in range(STEPS):
         src, tgt = _batch(rank, i)
@@ -76,6 +82,11 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1",
         ddp.verify_replicas()
     torch.cuda.synchronize()
     assert opt.iterations == STEPS
+    if graph and ddp._thread is not None and signal != "0":
+        # every handed-over issue job met its signal (one per span, plus the
+        # global token count's all-reduce under global_mean)
+        sig = ddp._thread.signal
+        assert sig.value() == sig.expected >= STEPS * len(ddp.last_buckets)
     torch.save({"flat": m.store.flat.cpu(), "loss": torch.stack(losses), "nb": len(ddp.last_buckets)},
                f"{out}.{rank}")
     ddp.close()
@@ -83,25 +94,29 @@ def _worker(rank, world, port, out, opt_mode, loss_mode, graph, comm_thread="1",
     tdist.shutdown()
 
 
-@pytest.mark.parametrize("world,opt_mode,loss_mode,graph,comm_thread,comm_bf16", [
-    (2, "0", "replica_mean", "", "0", False), (2, "tail", "replica_mean", "", "0", False),
-    (2, "tail", "global_mean", "", "0", False), (2, "tail", "replica_mean", "seg", "0", False),
-    (2, "0", "global_mean", "seg", "0", False),
+@pytest.mark.parametrize("world,opt_mode,loss_mode,graph,comm_thread,comm_bf16,signal", [
+    (2, "0", "replica_mean", "", "0", False, "1"), (2, "tail", "replica_mean", "", "0", False, "1"),
+    (2, "tail", "global_mean", "", "0", False, "1"), (2, "tail", "replica_mean", "seg", "0", False, "1"),
+    (2, "0", "global_mean", "seg", "0", False, "1"),
     # the host comm thread (default on RCCL, TDG_DP_COMM_THREAD) driven over gloo
-    (2, "tail", "replica_mean", "", "force", False), (2, "tail", "replica_mean", "seg", "force", False),
-    (2, "tail", "global_mean", "seg", "force", False),
+    (2, "tail", "replica_mean", "", "force", False, "1"), (2, "tail", "replica_mean", "seg", "force", False, "1"),
+    (2, "tail", "global_mean", "seg", "force", False, "1"),
+    # ... with the segmented graph cut at each issue point (event) instead of
+    # the in-graph signal kernel (TDG_DP_SIGNAL=0)
+    (2, "tail", "global_mean", "seg", "force", False, "0"),
     # four ranks on the production path: segmented graph, bf16 gradient
     # all-reduce, global token-mean loss -- with either issue path
-    (4, "tail", "global_mean", "seg", "0", True), (4, "tail", "global_mean", "seg", "force", True)])
+    (4, "tail", "global_mean", "seg", "0", True, "1"), (4, "tail", "global_mean", "seg", "force", True, "1")])
 def test_gpu_dp_rehearsal_matches_single_process(tmp_path, world, opt_mode, loss_mode, graph, comm_thread,
-                                                 comm_bf16, monkeypatch):
+                                                 comm_bf16, signal, monkeypatch):
     from tensorflow_distributed_on_gke_amd.models.layers import RunCtx
     from tensorflow_distributed_on_gke_amd.ops import kernels as kk
     from tensorflow_distributed_on_gke_amd.models.transformer import Transformer, model_config
     from tensorflow_distributed_on_gke_amd.train.optim import Adam
 
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode, graph, comm_thread, comm_bf16),
+    mp.start_processes(_worker, args=(world, _port(), out, opt_mode, loss_mode, graph, comm_thread, comm_bf16,
+                                      signal),
                        nprocs=world, join=True, start_method="spawn")
     rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     r0 = rs[0]
