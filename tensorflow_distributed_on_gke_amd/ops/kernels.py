@@ -505,7 +505,7 @@ def ln_fwd(x, s, gamma, beta, p, seed, ctr, site, eps=1e-6, save=True, y8=None, 
 # 5.02-5.05 ms, LN backward 308 vs 321 us + fold 10.6 vs 20.4 us), 16 for
 # D = 1024 (big 13.14-13.19 vs 13.20-13.22 ms); 64 loses 3.5 % (two serial
 # row passes). Non-zero LN_BWD_RPB forces one value (tests).
-LN_BWD_RPB = 0
+LN_BWD_RPB = int(os.environ.get("TDG_LN_BWD_RPB", "0") or 0)
 
 
 def ln_bwd_rpb(D: int) -> int:
