@@ -23,6 +23,11 @@ import os
 import sys
 import time
 
+# RCCL / HIP IPC between the ranks' processes needs the dmabuf IPC mode on
+# these hosts (the legacy mode fails in hipIpcGetMemHandle); set before the
+# first HIP call, for this process and the ranks it may launch
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
